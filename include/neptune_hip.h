@@ -1,0 +1,108 @@
+/*
+ * neptune_hip.h — C ABI of libneptune_hip.so, the MI355X (gfx950) batched verifier
+ * library for neptune-core's proof-validation hot path.
+ *
+ * Conventions (mirroring the reference's Rust types; see INTEGRATION.md for bindings):
+ *   - Field elements are passed as canonical u64 (BFieldElement::value()).  Inputs >= p are
+ *     reduced mod p, i.e. BFieldElement::new semantics.
+ *   - A Digest is 5 consecutive u64 (Digest::values()), 40 bytes.
+ *   - The caller owns every buffer; buffers are borrowed for the duration of the call.
+ *   - Return value: 0 (NHIP_OK) or an infrastructure error code (no device, HIP failure,
+ *     out of memory, bad argument).  A verification *failure* is never an error: it is a
+ *     verdict byte 0.  Callers must treat a non-zero return as "unknown", never as "accept"
+ *     (SURVEY.md §8b).
+ *   - Thread safety: a context may be shared by threads; calls on one context are serialized
+ *     onto that context's HIP stream.
+ *   - One context drives one GPU (one process per GPU; multi-GPU sharding is done by the
+ *     caller, see bench.py / DESIGN.md).
+ *
+ * Reference interfaces replaced (paths relative to /root/reference):
+ *   nhip_tip5_hash_pair     <- twenty-first 1.0.0 Tip5::hash_pair, as called by
+ *                              neptune-core/src/protocol/consensus/block/pow.rs:112,130,171-175
+ *   nhip_tip5_hash_varlen   <- Tip5::hash_varlen, as called by
+ *                              neptune-core/src/protocol/proof_abstractions/mast_hash.rs:26,
+ *                              neptune-core/src/state/wallet/wallet_entropy.rs:76-82 and the
+ *                              STARK row hashing inside triton_vm::verify
+ *   nhip_tip5_permutation   <- Tip5::permutation (twenty-first, the sponge core)
+ *   nhip_mtree_build        <- MTree::build_inplace, neptune-core/src/protocol/consensus/block/pow.rs:73-119
+ *   nhip_mtree_verify       <- MTree::verify,        neptune-core/src/protocol/consensus/block/pow.rs:162-180
+ *   nhip_sponge_*           <- Tip5 Sponge (pad_and_absorb_all / squeeze / sample_indices /
+ *                              sample_scalars) as driven by triton_vm's ProofStream Fiat-Shamir
+ *                              (SURVEY.md §8a a13); single call site of the verifier:
+ *                              neptune-core/src/protocol/proof_abstractions/verifier.rs:60-63
+ */
+#ifndef NEPTUNE_HIP_H
+#define NEPTUNE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct nhip_ctx nhip_ctx;
+
+enum {
+    NHIP_OK = 0,
+    NHIP_ERR_NO_DEVICE = 1,
+    NHIP_ERR_HIP = 2,
+    NHIP_ERR_OOM = 3,
+    NHIP_ERR_ARG = 4
+};
+
+/* ---- context --------------------------------------------------------------------------- */
+/* Bind to the lowest HIP device whose bit is set in device_mask (0 = device 0). */
+int nhip_init(uint32_t device_mask, nhip_ctx **out);
+void nhip_destroy(nhip_ctx *ctx);
+const char *nhip_strerror(int code);
+int nhip_device_ordinal(const nhip_ctx *ctx);
+/* ABI version: major * 1000 + minor */
+int nhip_abi_version(void);
+
+/* ---- Tip5 primitives (host buffers) ----------------------------------------------------- */
+/* states: n x 16 u64, permuted in place. */
+int nhip_tip5_permutation(nhip_ctx *ctx, uint64_t *states, size_t n);
+/* out[i] = Tip5::hash_pair(left[i], right[i]); left/right/out: n digests. */
+int nhip_tip5_hash_pair(nhip_ctx *ctx, const uint64_t *left, const uint64_t *right, size_t n, uint64_t *out);
+/* Ragged rows: row i = data[offsets[i] .. offsets[i+1]); offsets has n+1 entries.
+ * out[i] = Tip5::hash_varlen(row i). */
+int nhip_tip5_hash_varlen(nhip_ctx *ctx, const uint64_t *data, const uint64_t *offsets, size_t n, uint64_t *out);
+
+/* ---- MTree (pow.rs) (host buffers) ------------------------------------------------------ */
+/* n_leafs a power of two >= 2.  nodes_out: n_leafs digests; nodes_out[1] is the root,
+ * node i = hash_pair(node 2i, node 2i+1), leaf k acts as node n_leafs + k; nodes_out[0] = 0. */
+int nhip_mtree_build(nhip_ctx *ctx, const uint64_t *leafs, size_t n_leafs, uint64_t *nodes_out);
+/* verdicts[i] = MTree::verify(root_i, indices[i], path_i, leafs[i]).
+ * roots: n_roots digests with n_roots == 1 (shared root) or n_roots == n.
+ * paths: n x depth digests (sibling of the leaf first).  verdicts: n bytes, 1 = accept. */
+int nhip_mtree_verify(nhip_ctx *ctx, const uint64_t *roots, size_t n_roots, const uint64_t *indices,
+                      const uint64_t *leafs, const uint64_t *paths, uint32_t depth, size_t n, uint8_t *verdicts);
+
+/* ---- device-resident form (pointers from nhip_dev_alloc; asynchronous on the ctx stream) -- */
+int nhip_dev_alloc(nhip_ctx *ctx, size_t bytes, void **dptr);
+int nhip_dev_free(nhip_ctx *ctx, void *dptr);
+int nhip_memcpy_h2d(nhip_ctx *ctx, void *dst, const void *src, size_t bytes);
+int nhip_memcpy_d2h(nhip_ctx *ctx, void *dst, const void *src, size_t bytes);
+int nhip_synchronize(nhip_ctx *ctx);
+int nhip_tip5_permutation_dev(nhip_ctx *ctx, uint64_t *d_states, size_t n);
+int nhip_tip5_hash_pair_dev(nhip_ctx *ctx, const uint64_t *d_left, const uint64_t *d_right, size_t n,
+                            uint64_t *d_out);
+int nhip_tip5_hash_varlen_dev(nhip_ctx *ctx, const uint64_t *d_data, const uint64_t *d_offsets, size_t n,
+                              uint64_t *d_out);
+int nhip_mtree_build_dev(nhip_ctx *ctx, const uint64_t *d_leafs, size_t n_leafs, uint64_t *d_nodes);
+int nhip_mtree_verify_dev(nhip_ctx *ctx, const uint64_t *d_roots, size_t n_roots, const uint64_t *d_indices,
+                          const uint64_t *d_leafs, const uint64_t *d_paths, uint32_t depth, size_t n,
+                          uint8_t *d_verdicts);
+/* *all_ok = AND of n verdict bytes (device buffer), the per-batch / per-block verdict. */
+int nhip_verdicts_all_dev(nhip_ctx *ctx, const uint8_t *d_verdicts, size_t n, uint8_t *all_ok);
+
+/* ---- kernel timing (HIP events on the ctx stream around every kernel launch) ------------ */
+int nhip_timing_enable(nhip_ctx *ctx, int on);
+/* Total device time of the kernels launched since the last reset, and their count. */
+int nhip_timing_read(nhip_ctx *ctx, double *total_ms, uint64_t *launches, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NEPTUNE_HIP_H */

@@ -1,0 +1,428 @@
+// C-ABI layer of libneptune_hip.so (declarations: include/neptune_hip.h).
+//
+// One nhip_ctx = one GPU, one non-blocking HIP stream, a grow-only device workspace for the
+// host-buffer entry points, and an optional event timer around every kernel launch.  Calls on
+// one context are serialized by a mutex (the reference calls verify() concurrently from many
+// tokio tasks: neptune-core/src/protocol/proof_abstractions/verifier.rs:60-63).
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/neptune_hip.h"
+#include "kernels.hpp"
+
+struct nhip_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    void* ws = nullptr;  // workspace for host-buffer calls
+    size_t ws_bytes = 0;
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;  // recorded, not yet read
+    std::vector<hipEvent_t> free_events;
+    double timed_ms = 0.0;
+    uint64_t timed_launches = 0;
+};
+
+namespace {
+
+int hip_fail(hipError_t e) {
+    if (e == hipSuccess) return NHIP_OK;
+    if (e == hipErrorOutOfMemory) return NHIP_ERR_OOM;
+    return NHIP_ERR_HIP;
+}
+
+hipEvent_t take_event(nhip_ctx* c) {
+    if (!c->free_events.empty()) {
+        hipEvent_t e = c->free_events.back();
+        c->free_events.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// Launch helper: brackets the launch with events when timing is on.
+template <class F>
+int timed_launch(nhip_ctx* c, F&& f) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (c->timing) {
+        a = take_event(c);
+        b = take_event(c);
+        if (a && b) (void)hipEventRecord(a, c->stream);
+    }
+    hipError_t e = f();
+    if (c->timing && a && b) {
+        (void)hipEventRecord(b, c->stream);
+        c->pending.emplace_back(a, b);
+    }
+    return hip_fail(e);
+}
+
+int ensure_ws(nhip_ctx* c, size_t bytes) {
+    if (bytes <= c->ws_bytes) return NHIP_OK;
+    if (c->ws) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(c->ws);
+        c->ws = nullptr;
+        c->ws_bytes = 0;
+    }
+    size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
+    hipError_t e = hipMalloc(&c->ws, want);
+    if (e != hipSuccess) return hip_fail(e);
+    c->ws_bytes = want;
+    return NHIP_OK;
+}
+
+inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Carve a list of sizes out of the workspace.
+template <size_t N>
+int carve(nhip_ctx* c, const size_t (&sizes)[N], void* (&ptrs)[N]) {
+    size_t total = 0;
+    for (size_t i = 0; i < N; ++i) total += align_up(sizes[i] ? sizes[i] : 1);
+    int rc = ensure_ws(c, total);
+    if (rc) return rc;
+    char* base = (char*)c->ws;
+    size_t off = 0;
+    for (size_t i = 0; i < N; ++i) {
+        ptrs[i] = base + off;
+        off += align_up(sizes[i] ? sizes[i] : 1);
+    }
+    return NHIP_OK;
+}
+
+__global__ void k_all_verdicts(const uint8_t* __restrict__ v, size_t n, uint32_t* __restrict__ out) {
+    __shared__ uint32_t ok;
+    if (threadIdx.x == 0) ok = 1u;
+    __syncthreads();
+    uint32_t mine = 1u;
+    for (size_t i = threadIdx.x; i < n; i += blockDim.x) mine &= (v[i] == 1) ? 1u : 0u;
+    if (!mine) atomicAnd(&ok, 0u);
+    __syncthreads();
+    if (threadIdx.x == 0) *out = ok;
+}
+
+int build_tree_dev(nhip_ctx* c, const uint64_t* d_leafs, size_t n, uint64_t* d_nodes) {
+    // level 0: leafs -> nodes[n/2 .. n)
+    int rc = timed_launch(c, [&] { return nhip::launch_mtree_level(d_leafs, d_nodes + 5 * (n / 2), n / 2, c->stream); });
+    if (rc) return rc;
+    for (size_t parents = n / 4; parents >= 1; parents /= 2) {
+        rc = timed_launch(c, [&] {
+            return nhip::launch_mtree_level(d_nodes + 5 * (2 * parents), d_nodes + 5 * parents, parents, c->stream);
+        });
+        if (rc) return rc;
+    }
+    hipError_t e = hipMemsetAsync(d_nodes, 0, 5 * sizeof(uint64_t), c->stream);
+    return hip_fail(e);
+}
+
+bool is_pow2(size_t n) { return n >= 2 && (n & (n - 1)) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int nhip_abi_version(void) { return 1000; }
+
+const char* nhip_strerror(int code) {
+    switch (code) {
+        case NHIP_OK: return "ok";
+        case NHIP_ERR_NO_DEVICE: return "no HIP device";
+        case NHIP_ERR_HIP: return "HIP runtime error";
+        case NHIP_ERR_OOM: return "out of device memory";
+        case NHIP_ERR_ARG: return "invalid argument";
+        default: return "unknown error";
+    }
+}
+
+int nhip_init(uint32_t device_mask, nhip_ctx** out) {
+    if (!out) return NHIP_ERR_ARG;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return NHIP_ERR_NO_DEVICE;
+    int dev = 0;
+    if (device_mask) {
+        dev = __builtin_ctz(device_mask);
+        if (dev >= count) return NHIP_ERR_NO_DEVICE;
+    }
+    nhip_ctx* c = new (std::nothrow) nhip_ctx();
+    if (!c) return NHIP_ERR_OOM;
+    c->device = dev;
+    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return NHIP_ERR_HIP;
+    }
+    *out = c;
+    return NHIP_OK;
+}
+
+void nhip_destroy(nhip_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (auto& p : c->pending) {
+        (void)hipEventDestroy(p.first);
+        (void)hipEventDestroy(p.second);
+    }
+    for (auto e : c->free_events) (void)hipEventDestroy(e);
+    if (c->ws) (void)hipFree(c->ws);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int nhip_device_ordinal(const nhip_ctx* c) { return c ? c->device : -1; }
+
+// ------------------------------------------------------------------ device-resident form
+int nhip_dev_alloc(nhip_ctx* c, size_t bytes, void** dptr) {
+    if (!c || !dptr) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    return hip_fail(hipMalloc(dptr, bytes ? bytes : 1));
+}
+
+int nhip_dev_free(nhip_ctx* c, void* d) {
+    if (!c) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    return hip_fail(hipFree(d));
+}
+
+int nhip_memcpy_h2d(nhip_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!c) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return hip_fail(e);
+}
+
+int nhip_memcpy_d2h(nhip_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!c) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return hip_fail(e);
+}
+
+int nhip_synchronize(nhip_ctx* c) {
+    if (!c) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    return hip_fail(hipStreamSynchronize(c->stream));
+}
+
+int nhip_tip5_permutation_dev(nhip_ctx* c, uint64_t* d_states, size_t n) {
+    if (!c || (n && !d_states)) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    return timed_launch(c, [&] { return nhip::launch_permutation(d_states, n, c->stream); });
+}
+
+int nhip_tip5_hash_pair_dev(nhip_ctx* c, const uint64_t* l, const uint64_t* r, size_t n, uint64_t* o) {
+    if (!c || (n && (!l || !r || !o))) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    return timed_launch(c, [&] { return nhip::launch_hash_pair(l, r, o, n, c->stream); });
+}
+
+int nhip_tip5_hash_varlen_dev(nhip_ctx* c, const uint64_t* d, const uint64_t* off, size_t n, uint64_t* o) {
+    if (!c || (n && (!off || !o))) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    return timed_launch(c, [&] { return nhip::launch_hash_varlen(d, off, n, o, c->stream); });
+}
+
+int nhip_mtree_build_dev(nhip_ctx* c, const uint64_t* d_leafs, size_t n, uint64_t* d_nodes) {
+    if (!c || !is_pow2(n) || !d_leafs || !d_nodes) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    return build_tree_dev(c, d_leafs, n, d_nodes);
+}
+
+int nhip_mtree_verify_dev(nhip_ctx* c, const uint64_t* roots, size_t n_roots, const uint64_t* idx,
+                          const uint64_t* leafs, const uint64_t* paths, uint32_t depth, size_t n, uint8_t* v) {
+    if (!c || (n_roots != 1 && n_roots != n)) return NHIP_ERR_ARG;
+    if (n && (!roots || !idx || !leafs || !v || (depth && !paths))) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    const int per_path = (n_roots == n && n != 1) ? 1 : 0;
+    return timed_launch(c, [&] {
+        return nhip::launch_mtree_verify(roots, per_path, idx, leafs, paths, depth, n, v, c->stream);
+    });
+}
+
+int nhip_verdicts_all_dev(nhip_ctx* c, const uint8_t* d_v, size_t n, uint8_t* all_ok) {
+    if (!c || !all_ok || (n && !d_v)) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    size_t sizes[1] = {sizeof(uint32_t)};
+    void* p[1];
+    int rc = carve(c, sizes, p);
+    if (rc) return rc;
+    uint32_t* d_out = (uint32_t*)p[0];
+    rc = timed_launch(c, [&] {
+        hipLaunchKernelGGL(k_all_verdicts, dim3(1), dim3(1024), 0, c->stream, d_v, n, d_out);
+        return hipGetLastError();
+    });
+    if (rc) return rc;
+    uint32_t h = 0;
+    hipError_t e = hipMemcpyAsync(&h, d_out, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(e);
+    *all_ok = (uint8_t)(h ? 1 : 0);
+    return NHIP_OK;
+}
+
+// ------------------------------------------------------------------ host-buffer form
+int nhip_tip5_permutation(nhip_ctx* c, uint64_t* states, size_t n) {
+    if (!c || (n && !states)) return NHIP_ERR_ARG;
+    if (n == 0) return NHIP_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    const size_t bytes = n * 16 * sizeof(uint64_t);
+    size_t sizes[1] = {bytes};
+    void* p[1];
+    int rc = carve(c, sizes, p);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(p[0], states, bytes, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_fail(e);
+    rc = timed_launch(c, [&] { return nhip::launch_permutation((uint64_t*)p[0], n, c->stream); });
+    if (rc) return rc;
+    e = hipMemcpyAsync(states, p[0], bytes, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return hip_fail(e);
+}
+
+int nhip_tip5_hash_pair(nhip_ctx* c, const uint64_t* l, const uint64_t* r, size_t n, uint64_t* o) {
+    if (!c || (n && (!l || !r || !o))) return NHIP_ERR_ARG;
+    if (n == 0) return NHIP_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    const size_t db = n * 5 * sizeof(uint64_t);
+    size_t sizes[3] = {db, db, db};
+    void* p[3];
+    int rc = carve(c, sizes, p);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(p[0], l, db, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(p[1], r, db, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_fail(e);
+    rc = timed_launch(c, [&] {
+        return nhip::launch_hash_pair((const uint64_t*)p[0], (const uint64_t*)p[1], (uint64_t*)p[2], n, c->stream);
+    });
+    if (rc) return rc;
+    e = hipMemcpyAsync(o, p[2], db, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return hip_fail(e);
+}
+
+int nhip_tip5_hash_varlen(nhip_ctx* c, const uint64_t* data, const uint64_t* offsets, size_t n, uint64_t* o) {
+    if (!c || (n && (!offsets || !o))) return NHIP_ERR_ARG;
+    if (n == 0) return NHIP_OK;
+    for (size_t i = 0; i < n; ++i)
+        if (offsets[i + 1] < offsets[i]) return NHIP_ERR_ARG;
+    const size_t total = (size_t)offsets[n];
+    if (total && !data) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    size_t sizes[3] = {total * sizeof(uint64_t), (n + 1) * sizeof(uint64_t), n * 5 * sizeof(uint64_t)};
+    void* p[3];
+    int rc = carve(c, sizes, p);
+    if (rc) return rc;
+    hipError_t e = hipSuccess;
+    if (total) e = hipMemcpyAsync(p[0], data, sizes[0], hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(p[1], offsets, sizes[1], hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_fail(e);
+    rc = timed_launch(c, [&] {
+        return nhip::launch_hash_varlen((const uint64_t*)p[0], (const uint64_t*)p[1], n, (uint64_t*)p[2], c->stream);
+    });
+    if (rc) return rc;
+    e = hipMemcpyAsync(o, p[2], sizes[2], hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return hip_fail(e);
+}
+
+int nhip_mtree_build(nhip_ctx* c, const uint64_t* leafs, size_t n, uint64_t* nodes_out) {
+    if (!c || !is_pow2(n) || !leafs || !nodes_out) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    const size_t db = n * 5 * sizeof(uint64_t);
+    size_t sizes[2] = {db, db};
+    void* p[2];
+    int rc = carve(c, sizes, p);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(p[0], leafs, db, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_fail(e);
+    rc = build_tree_dev(c, (const uint64_t*)p[0], n, (uint64_t*)p[1]);
+    if (rc) return rc;
+    e = hipMemcpyAsync(nodes_out, p[1], db, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return hip_fail(e);
+}
+
+int nhip_mtree_verify(nhip_ctx* c, const uint64_t* roots, size_t n_roots, const uint64_t* idx,
+                      const uint64_t* leafs, const uint64_t* paths, uint32_t depth, size_t n, uint8_t* v) {
+    if (!c || (n_roots != 1 && n_roots != n)) return NHIP_ERR_ARG;
+    if (n == 0) return NHIP_OK;
+    if (!roots || !idx || !leafs || !v || (depth && !paths)) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    size_t sizes[5] = {n_roots * 5 * sizeof(uint64_t), n * sizeof(uint64_t), n * 5 * sizeof(uint64_t),
+                       n * (size_t)depth * 5 * sizeof(uint64_t), n};
+    void* p[5];
+    int rc = carve(c, sizes, p);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(p[0], roots, sizes[0], hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(p[1], idx, sizes[1], hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(p[2], leafs, sizes[2], hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && depth) e = hipMemcpyAsync(p[3], paths, sizes[3], hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_fail(e);
+    const int per_path = (n_roots == n && n != 1) ? 1 : 0;
+    rc = timed_launch(c, [&] {
+        return nhip::launch_mtree_verify((const uint64_t*)p[0], per_path, (const uint64_t*)p[1],
+                                         (const uint64_t*)p[2], (const uint64_t*)p[3], depth, n, (uint8_t*)p[4],
+                                         c->stream);
+    });
+    if (rc) return rc;
+    e = hipMemcpyAsync(v, p[4], n, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return hip_fail(e);
+}
+
+// ------------------------------------------------------------------ timing
+int nhip_timing_enable(nhip_ctx* c, int on) {
+    if (!c) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->timing = on != 0;
+    return NHIP_OK;
+}
+
+int nhip_timing_read(nhip_ctx* c, double* total_ms, uint64_t* launches, int reset) {
+    if (!c) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(e);
+    for (auto& pr : c->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) c->timed_ms += ms;
+        c->timed_launches += 1;
+        c->free_events.push_back(pr.first);
+        c->free_events.push_back(pr.second);
+    }
+    c->pending.clear();
+    if (total_ms) *total_ms = c->timed_ms;
+    if (launches) *launches = c->timed_launches;
+    if (reset) {
+        c->timed_ms = 0.0;
+        c->timed_launches = 0;
+    }
+    return NHIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,116 @@
+// Tip5 permutation for CDNA4 (gfx950): one 16-word state per lane, held in VGPRs in raw
+// Montgomery form; S-box lookup table staged in LDS.
+//
+// Restates twenty-first 1.0.0 `Tip5::permutation` (crate pinned at /root/reference/Cargo.lock:4297;
+// behaviour pinned by KAT-V neptune-core/src/state/wallet/mod.rs:1379-1383 and KAT-F
+// neptune-core/test_data/precalculated_pow_solution.json):
+//   5 rounds of  { S-box: split-and-lookup of the 8 raw Montgomery LE bytes of state[0..4],
+//                          x^7 on state[4..16];
+//                  MDS:   out[i] = sum_j MDS[(i-j) & 15] * in[j]   (integer-linear on raw words);
+//                  ARK:   state[i] += RC[r*16 + i] }
+//
+// Sponge conventions used by the kernels (twenty-first `Sponge` for Tip5):
+//   FixedLength domain (hash_pair): capacity words state[10..16] = 1 (canonical 1).
+//   VariableLength domain (hash_varlen, Fiat-Shamir): state starts all-zero; absorb overwrites
+//   state[0..10]; padding appends a single 1 then zeros to a multiple of 10.
+#pragma once
+#include "goldilocks.hpp"
+#include "tip5_constants.h"
+
+namespace nhip {
+
+static constexpr int TIP5_STATE = 16;
+static constexpr int TIP5_RATE = 10;
+static constexpr int TIP5_ROUNDS = 5;
+static constexpr uint64_t MONT_ONE = 0x00000000FFFFFFFFull;  // raw Montgomery word of 1 (= 2^64 mod p)
+
+__constant__ static uint64_t c_tip5_rc_raw[80] = {
+#define NHIP_RC(i) TIP5_RC_RAW[i]
+    NHIP_RC(0), NHIP_RC(1), NHIP_RC(2), NHIP_RC(3), NHIP_RC(4), NHIP_RC(5), NHIP_RC(6), NHIP_RC(7),
+    NHIP_RC(8), NHIP_RC(9), NHIP_RC(10), NHIP_RC(11), NHIP_RC(12), NHIP_RC(13), NHIP_RC(14), NHIP_RC(15),
+    NHIP_RC(16), NHIP_RC(17), NHIP_RC(18), NHIP_RC(19), NHIP_RC(20), NHIP_RC(21), NHIP_RC(22), NHIP_RC(23),
+    NHIP_RC(24), NHIP_RC(25), NHIP_RC(26), NHIP_RC(27), NHIP_RC(28), NHIP_RC(29), NHIP_RC(30), NHIP_RC(31),
+    NHIP_RC(32), NHIP_RC(33), NHIP_RC(34), NHIP_RC(35), NHIP_RC(36), NHIP_RC(37), NHIP_RC(38), NHIP_RC(39),
+    NHIP_RC(40), NHIP_RC(41), NHIP_RC(42), NHIP_RC(43), NHIP_RC(44), NHIP_RC(45), NHIP_RC(46), NHIP_RC(47),
+    NHIP_RC(48), NHIP_RC(49), NHIP_RC(50), NHIP_RC(51), NHIP_RC(52), NHIP_RC(53), NHIP_RC(54), NHIP_RC(55),
+    NHIP_RC(56), NHIP_RC(57), NHIP_RC(58), NHIP_RC(59), NHIP_RC(60), NHIP_RC(61), NHIP_RC(62), NHIP_RC(63),
+    NHIP_RC(64), NHIP_RC(65), NHIP_RC(66), NHIP_RC(67), NHIP_RC(68), NHIP_RC(69), NHIP_RC(70), NHIP_RC(71),
+    NHIP_RC(72), NHIP_RC(73), NHIP_RC(74), NHIP_RC(75), NHIP_RC(76), NHIP_RC(77), NHIP_RC(78), NHIP_RC(79),
+#undef NHIP_RC
+};
+
+// LDS copy of the byte lookup table, one per workgroup.  256 B = 64 dwords: a random byte
+// gather from a wave touches at most 2 distinct dwords per bank for ds_read_u8 (bank = dword % 32).
+struct Tip5Lds {
+    uint8_t lut[256];
+};
+
+__device__ __forceinline__ void tip5_lds_init(Tip5Lds& lds) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lds.lut[i] = TIP5_LUT[i];
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t lookup4(const uint8_t* __restrict__ lut, uint32_t w) {
+    const uint32_t b0 = lut[w & 0xFFu];
+    const uint32_t b1 = lut[(w >> 8) & 0xFFu];
+    const uint32_t b2 = lut[(w >> 16) & 0xFFu];
+    const uint32_t b3 = lut[w >> 24];
+    return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+}
+
+__device__ __forceinline__ uint64_t split_and_lookup(const uint8_t* __restrict__ lut, uint64_t r) {
+    const uint32_t lo = lookup4(lut, (uint32_t)r);
+    const uint32_t hi = lookup4(lut, (uint32_t)(r >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t pow7(uint64_t x) {
+    const uint64_t x2 = mont_sqr(x);
+    const uint64_t x4 = mont_sqr(x2);
+    const uint64_t x3 = mont_mul(x, x2);
+    return mont_mul(x3, x4);
+}
+
+// MDS: circulant 16x16 with small (< 2^16) coefficients applied to the raw words.  Each word is
+// split into 32-bit halves; the two half-products are accumulated exactly in 64 bits
+// (sum < 2^16 * 2^32 * 16 < 2^53) and recombined: acc_lo + acc_hi * 2^32, reduced mod p.
+__device__ __forceinline__ void mds(uint64_t s[16]) {
+    uint32_t lo[16], hi[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        lo[j] = (uint32_t)s[j];
+        hi[j] = (uint32_t)(s[j] >> 32);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        uint64_t al = 0, ah = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint64_t c = TIP5_MDS[(i - j) & 15];
+            al += c * lo[j];
+            ah += c * hi[j];
+        }
+        // value = al + ah * 2^32 (< 2^86).  low 64 bits and the carry part above 2^64:
+        const uint64_t ah_shift = ah << 32;
+        const uint64_t sl = al + ah_shift;
+        const uint32_t carry = sl < al ? 1u : 0u;
+        const uint32_t sh = (uint32_t)(ah >> 32) + carry;
+        s[i] = reduce96(sl, sh);
+    }
+}
+
+// One permutation on a raw Montgomery state.
+__device__ __forceinline__ void tip5_permute_raw(uint64_t s[16], const uint8_t* __restrict__ lut) {
+#pragma unroll 1
+    for (int r = 0; r < TIP5_ROUNDS; ++r) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
+#pragma unroll
+        for (int i = 4; i < 16; ++i) s[i] = pow7(s[i]);
+        mds(s);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[i] = gl_add(s[i], c_tip5_rc_raw[r * 16 + i]);
+    }
+}
+
+}  // namespace nhip

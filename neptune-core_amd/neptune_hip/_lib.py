@@ -1,0 +1,82 @@
+"""ctypes binding of libneptune_hip.so (C ABI: include/neptune_hip.h).
+
+The shared library is built in-tree (``make -C neptune-core_amd``) and loaded from this
+directory.  There is no CPU fallback: if the library is missing or no GPU is present the
+calls raise, so a product path can never silently run on something else.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libneptune_hip.so")
+
+NHIP_OK = 0
+_ERRORS = {1: "no HIP device", 2: "HIP runtime error", 3: "out of device memory", 4: "invalid argument"}
+
+_u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+# (name, argtypes) for every symbol of include/neptune_hip.h
+SIGNATURES = {
+    "nhip_init": ([ctypes.c_uint32, ctypes.POINTER(_vp)], ctypes.c_int),
+    "nhip_destroy": ([_vp], None),
+    "nhip_strerror": ([ctypes.c_int], ctypes.c_char_p),
+    "nhip_device_ordinal": ([_vp], ctypes.c_int),
+    "nhip_abi_version": ([], ctypes.c_int),
+    "nhip_tip5_permutation": ([_vp, _u64p, _sz], ctypes.c_int),
+    "nhip_tip5_hash_pair": ([_vp, _u64p, _u64p, _sz, _u64p], ctypes.c_int),
+    "nhip_tip5_hash_varlen": ([_vp, _u64p, _u64p, _sz, _u64p], ctypes.c_int),
+    "nhip_mtree_build": ([_vp, _u64p, _sz, _u64p], ctypes.c_int),
+    "nhip_mtree_verify": ([_vp, _u64p, _sz, _u64p, _u64p, _u64p, ctypes.c_uint32, _sz, _u8p], ctypes.c_int),
+    "nhip_dev_alloc": ([_vp, _sz, ctypes.POINTER(_vp)], ctypes.c_int),
+    "nhip_dev_free": ([_vp, _vp], ctypes.c_int),
+    "nhip_memcpy_h2d": ([_vp, _vp, _vp, _sz], ctypes.c_int),
+    "nhip_memcpy_d2h": ([_vp, _vp, _vp, _sz], ctypes.c_int),
+    "nhip_synchronize": ([_vp], ctypes.c_int),
+    "nhip_tip5_permutation_dev": ([_vp, _vp, _sz], ctypes.c_int),
+    "nhip_tip5_hash_pair_dev": ([_vp, _vp, _vp, _sz, _vp], ctypes.c_int),
+    "nhip_tip5_hash_varlen_dev": ([_vp, _vp, _vp, _sz, _vp], ctypes.c_int),
+    "nhip_mtree_build_dev": ([_vp, _vp, _sz, _vp], ctypes.c_int),
+    "nhip_mtree_verify_dev": ([_vp, _vp, _sz, _vp, _vp, _vp, ctypes.c_uint32, _sz, _vp], ctypes.c_int),
+    "nhip_verdicts_all_dev": ([_vp, _vp, _sz, ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
+    "nhip_timing_enable": ([_vp, ctypes.c_int], ctypes.c_int),
+    "nhip_timing_read": ([_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int],
+                         ctypes.c_int),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NhipError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load libneptune_hip.so (raises if it has not been built)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NhipError(f"{LIB_PATH} is missing: build it with `make -C neptune-core_amd` "
+                            "(or __graft_entry__.build()); there is no CPU fallback")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != NHIP_OK:
+        raise NhipError(f"{what}: {_ERRORS.get(rc, f'error {rc}')}")

@@ -1,0 +1,94 @@
+"""ctypes loader for the C restatement oracle (oracle/liboracle_tip5.so) — TEST ORACLE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle_tip5.so")
+_lib = None
+
+_u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB):
+        build()
+    L = ctypes.CDLL(_LIB)
+    L.oracle_init.argtypes = [_u64p]
+    L.oracle_tip5_permutation.argtypes = [_u64p]
+    L.oracle_hash_pair.argtypes = [_u64p, _u64p, _u64p]
+    L.oracle_hash_varlen.argtypes = [_u64p, ctypes.c_size_t, _u64p]
+    L.oracle_hash_varlen_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t, _u64p]
+    L.oracle_mtree_verify.argtypes = [_u64p, ctypes.c_uint64, _u64p, ctypes.c_uint32, _u64p]
+    L.oracle_mtree_verify.restype = ctypes.c_int
+    L.oracle_mtree_verify_batch.argtypes = [_u64p, ctypes.c_size_t, _u64p, _u64p, _u64p, ctypes.c_uint32,
+                                            ctypes.c_size_t, _u8p, ctypes.c_int]
+    L.oracle_mtree_build.argtypes = [_u64p, ctypes.c_size_t, _u64p]
+    # round constants: derived independently in Python from BLAKE3 (see tip5_ref.py)
+    import tip5_ref
+    rc_raw = np.array([tip5_ref.to_mont(c) for c in tip5_ref.ROUND_CONSTANTS], dtype=np.uint64)
+    L.oracle_init(rc_raw)
+    _lib = L
+    return L
+
+
+def permutation_batch(states: np.ndarray) -> np.ndarray:
+    L = lib()
+    out = np.ascontiguousarray(states, dtype=np.uint64).copy()
+    for i in range(out.shape[0]):
+        row = np.ascontiguousarray(out[i])
+        L.oracle_tip5_permutation(row)
+        out[i] = row
+    return out
+
+
+def hash_pair(left, right) -> np.ndarray:
+    out = np.zeros(5, dtype=np.uint64)
+    lib().oracle_hash_pair(np.ascontiguousarray(left, dtype=np.uint64),
+                           np.ascontiguousarray(right, dtype=np.uint64), out)
+    return out
+
+
+def hash_varlen_batch(data: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+    n = len(offsets) - 1
+    out = np.zeros((n, 5), dtype=np.uint64)
+    d = np.ascontiguousarray(data, dtype=np.uint64)
+    if d.size == 0:
+        d = np.zeros(1, dtype=np.uint64)
+    lib().oracle_hash_varlen_batch(d, np.ascontiguousarray(offsets, dtype=np.uint64), n, out)
+    return out
+
+
+def mtree_build(leaves: np.ndarray) -> np.ndarray:
+    n = leaves.shape[0]
+    nodes = np.zeros((n, 5), dtype=np.uint64)
+    lib().oracle_mtree_build(np.ascontiguousarray(leaves, dtype=np.uint64), n, nodes)
+    return nodes
+
+
+def mtree_verify_batch(roots, indices, leaves, paths, depth: int, nthreads: int = 1) -> np.ndarray:
+    roots = np.ascontiguousarray(roots, dtype=np.uint64).reshape(-1, 5)
+    n = int(np.asarray(indices).shape[0])
+    verdicts = np.zeros(max(n, 1), dtype=np.uint8)
+    paths = np.ascontiguousarray(paths, dtype=np.uint64)
+    if paths.size == 0:
+        paths = np.zeros(1, dtype=np.uint64)
+    lib().oracle_mtree_verify_batch(roots, roots.shape[0], np.ascontiguousarray(indices, dtype=np.uint64),
+                                    np.ascontiguousarray(leaves, dtype=np.uint64).reshape(-1) if n else np.zeros(1, np.uint64),
+                                    paths, depth, n, verdicts, nthreads)
+    return verdicts[:n]
