@@ -34,7 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
 P = (1 << 64) - (1 << 32) + 1
 # Algorithmic VALU work of one Tip5 permutation, in 32-bit VALU lane-ops, frozen once from the
 # v1 kernel ISA: 5 rounds x 2364 VALU instructions per round.
-TIP5_VALU_OPS_PER_PERM = 5 * 2364
+TIP5_VALU_OPS_PER_PERM = 5 * 1504
 # gfx950: 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz (wave64 VALU issues over 2 cycles on SIMD-32)
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
 # algorithmic HBM bytes per path: leaf (40) + index (8) + depth siblings (40 each) + verdict (1)

@@ -33,11 +33,76 @@ __host__ __device__ __forceinline__ uint64_t montyred(uint64_t xl, uint64_t xh) 
     return xh < b ? r - GL_EPS : r;
 }
 
+// Montgomery product on 32-bit VALU pieces: 4 v_mad_u64_u32 for the 128-bit product,
+// then twenty-first's montyred written as explicit carry chains (v_add_co / v_sub_co / subb),
+// 14 VALU instructions in total.
 __host__ __device__ __forceinline__ uint64_t mont_mul(uint64_t a, uint64_t b) {
-    return montyred(a * b, mulhi64(a, b));
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
+    const uint32_t b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const uint64_t p00 = (uint64_t)a0 * b0;
+    const uint64_t t = (uint64_t)a0 * b1 + (p00 >> 32);
+    const uint64_t u = (uint64_t)a1 * b0 + (uint32_t)t;
+    const uint64_t v = (uint64_t)a1 * b1 + (t >> 32);
+    const uint64_t xh = v + (u >> 32);
+    const uint32_t xl0 = (uint32_t)p00, xl1 = (uint32_t)u;
+    // a = xl + (xl << 32):  a.lo = xl0, a.hi = xl1 + xl0 (carry e)
+    unsigned int e, br1, br2, c1, c, c2;
+    const uint32_t ah = __builtin_addc(xl1, xl0, 0u, &e);
+    // b = a - (a >> 32) - e
+    const uint32_t bl = __builtin_subc(xl0, ah, e, &br1);
+    const uint32_t bh = __builtin_subc(ah, 0u, br1, &br2);
+    // r = xh - b; if borrow: r -= 2^32 - 1
+    uint32_t rl = __builtin_subc((uint32_t)xh, bl, 0u, &c1);
+    uint32_t rh = __builtin_subc((uint32_t)(xh >> 32), bh, c1, &c);
+    const uint32_t m = 0u - c;
+    rl = __builtin_subc(rl, m, 0u, &c2);
+    rh = rh - c2;
+    return ((uint64_t)rh << 32) | rl;
 }
 
 __host__ __device__ __forceinline__ uint64_t mont_sqr(uint64_t a) { return mont_mul(a, a); }
+
+// N independent Montgomery products, written stage by stage so that the carry-chain
+// instructions of different elements interleave (fills the VALU->VCC->VALU wait states that a
+// single chain would pad with s_nop).
+template <int N>
+__host__ __device__ __forceinline__ void mont_mul_n(const uint64_t* a, const uint64_t* b, uint64_t* out) {
+    uint64_t p00[N], t[N], u[N], xh[N];
+    uint32_t ah[N], e[N], bl[N], bh[N], rl[N], rh[N], c1[N], c[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) p00[i] = (uint64_t)(uint32_t)a[i] * (uint32_t)b[i];
+#pragma unroll
+    for (int i = 0; i < N; ++i) t[i] = (uint64_t)(uint32_t)a[i] * (uint32_t)(b[i] >> 32) + (p00[i] >> 32);
+#pragma unroll
+    for (int i = 0; i < N; ++i) u[i] = (uint64_t)(uint32_t)(a[i] >> 32) * (uint32_t)b[i] + (uint32_t)t[i];
+#pragma unroll
+    for (int i = 0; i < N; ++i) xh[i] = (uint64_t)(uint32_t)(a[i] >> 32) * (uint32_t)(b[i] >> 32) + (t[i] >> 32);
+#pragma unroll
+    for (int i = 0; i < N; ++i) xh[i] += (u[i] >> 32);
+#pragma unroll
+    for (int i = 0; i < N; ++i) ah[i] = __builtin_addc((uint32_t)u[i], (uint32_t)p00[i], 0u, &e[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        unsigned int br1;
+        bl[i] = __builtin_subc((uint32_t)p00[i], ah[i], e[i], &br1);
+        e[i] = br1;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        unsigned int br2;
+        bh[i] = __builtin_subc(ah[i], 0u, e[i], &br2);
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) rl[i] = __builtin_subc((uint32_t)xh[i], bl[i], 0u, &c1[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) rh[i] = __builtin_subc((uint32_t)(xh[i] >> 32), bh[i], c1[i], &c[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        unsigned int c2;
+        const uint32_t lo = __builtin_subc(rl[i], 0u - c[i], 0u, &c2);
+        out[i] = ((uint64_t)(rh[i] - c2) << 32) | lo;
+    }
+}
 
 // a + b mod p for a, b in [0, p)
 __host__ __device__ __forceinline__ uint64_t gl_add(uint64_t a, uint64_t b) {

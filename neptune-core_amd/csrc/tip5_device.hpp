@@ -71,32 +71,74 @@ __device__ __forceinline__ uint64_t pow7(uint64_t x) {
     return mont_mul(x3, x4);
 }
 
-// MDS: circulant 16x16 with small (< 2^16) coefficients applied to the raw words.  Each word is
-// split into 32-bit halves; the two half-products are accumulated exactly in 64 bits
-// (sum < 2^16 * 2^32 * 16 < 2^53) and recombined: acc_lo + acc_hi * 2^32, reduced mod p.
-__device__ __forceinline__ void mds(uint64_t s[16]) {
+// x -> x^7 on 12 words at once (stage-interleaved Montgomery products).
+__device__ __forceinline__ void pow7_12(uint64_t* x) {
+    uint64_t x2[12], x4[12], x3[12];
+    mont_mul_n<12>(x, x, x2);
+    mont_mul_n<12>(x2, x2, x4);
+    mont_mul_n<12>(x, x2, x3);
+    mont_mul_n<12>(x3, x4, x);
+}
+
+// MDS + ARK.  Circulant 16x16 with small (< 2^16) coefficients applied to the raw words: each
+// word is split into 32-bit halves and the two half-products are accumulated exactly in 64 bits
+// (< 2^53) by v_mad_u64_u32.  Recombination and the round-constant add follow twenty-first
+// step by step (s = acc_lo + acc_hi * 2^32; res = s_lo + s_hi * (2^32 - 1) with the +EPS fix on
+// overflow; x = res - (p - rc), + p on borrow), so every intermediate word is bit-identical to the
+// reference's, written as explicit 32-bit carry chains interleaved across the 16 outputs.
+__device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restrict__ rc) {
     uint32_t lo[16], hi[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         lo[j] = (uint32_t)s[j];
         hi[j] = (uint32_t)(s[j] >> 32);
     }
+    uint64_t al[16], ah[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        uint64_t al = 0, ah = 0;
+        al[i] = 0;
+        ah[i] = 0;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const uint64_t c = TIP5_MDS[(i - j) & 15];
-            al += c * lo[j];
-            ah += c * hi[j];
+            al[i] += c * lo[j];
+            ah[i] += c * hi[j];
         }
-        // value = al + ah * 2^32 (< 2^86).  low 64 bits and the carry part above 2^64:
-        const uint64_t ah_shift = ah << 32;
-        const uint64_t sl = al + ah_shift;
-        const uint32_t carry = sl < al ? 1u : 0u;
-        const uint32_t sh = (uint32_t)(ah >> 32) + carry;
-        s[i] = reduce96(sl, sh);
     }
+    uint32_t m1[16], sh[16], rl[16], rh[16];
+    unsigned int k[16], b[16], over[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m1[i] = __builtin_addc((uint32_t)(al[i] >> 32), (uint32_t)ah[i], 0u, &k[i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sh[i] = (uint32_t)(ah[i] >> 32) + k[i];
+    // t = sh * (2^32 - 1) = {0 - sh, sh - (sh != 0)}
+    uint32_t tl[16], th[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tl[i] = __builtin_subc(0u, sh[i], 0u, &b[i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        unsigned int dummy;
+        th[i] = __builtin_subc(sh[i], 0u, b[i], &dummy);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) rl[i] = __builtin_addc((uint32_t)al[i], tl[i], 0u, &k[i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) rh[i] = __builtin_addc(m1[i], th[i], k[i], &over[i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) rl[i] = __builtin_addc(rl[i], 0u - over[i], 0u, &k[i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) rh[i] = rh[i] + k[i];
+    // ARK: x1 = res - (p - rc); borrow => x1 + p  (== x1 - (2^32 - 1) mod 2^64)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint64_t q = GL_P - rc[i];
+        rl[i] = __builtin_subc(rl[i], (uint32_t)q, 0u, &b[i]);
+        rh[i] = __builtin_subc(rh[i], (uint32_t)(q >> 32), b[i], &over[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) rl[i] = __builtin_subc(rl[i], 0u - over[i], 0u, &b[i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] = ((uint64_t)(rh[i] - b[i]) << 32) | rl[i];
 }
 
 // One permutation on a raw Montgomery state.
@@ -105,11 +147,8 @@ __device__ __forceinline__ void tip5_permute_raw(uint64_t s[16], const uint8_t* 
     for (int r = 0; r < TIP5_ROUNDS; ++r) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
-#pragma unroll
-        for (int i = 4; i < 16; ++i) s[i] = pow7(s[i]);
-        mds(s);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[i] = gl_add(s[i], c_tip5_rc_raw[r * 16 + i]);
+        pow7_12(s + 4);
+        mds_ark(s, c_tip5_rc_raw + r * 16);
     }
 }
 
