@@ -32,14 +32,32 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
 
 P = (1 << 64) - (1 << 32) + 1
-# Algorithmic VALU work of one Tip5 permutation, in 32-bit VALU lane-ops, frozen once from the
-# v1 kernel ISA: 5 rounds x 2364 VALU instructions per round.
+# Algorithmic VALU work of one Tip5 permutation in 32-bit VALU lane-ops: a fixed analytic count of
+# a minimal implementation: per round S-box 64 + x^7 672 + MDS 512+160 + ARK 96.
 TIP5_VALU_OPS_PER_PERM = 5 * 1504
 # gfx950: 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz (wave64 VALU issues over 2 cycles on SIMD-32)
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
 # algorithmic HBM bytes per path: leaf (40) + index (8) + depth siblings (40 each) + verdict (1)
 def path_bytes(depth: int) -> int:
     return 40 + 8 + 40 * depth + 1
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the latest committed rocprofv3 PMC passes
+    (profiles/LATEST -> profiles/<tag>/pmc_{fetch,write}_counter_collection.csv), raw
+    (FETCH_SIZE + WRITE_SIZE) x 1024; None when absent."""
+    import csv
+    try:
+        tag = open(os.path.join(ROOT, "profiles", "LATEST")).read().strip()
+        tot = 0.0
+        for part, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+            vals = [float(r["Counter_Value"]) for r in
+                    csv.DictReader(open(os.path.join(ROOT, "profiles", tag, f"pmc_{part}_counter_collection.csv")))
+                    if kernel in r["Kernel_Name"] and r["Counter_Name"] == ctr]
+            tot += sum(vals) / len(vals) * 1024
+        return tot, tag
+    except (OSError, ZeroDivisionError, KeyError):
+        return None, None
 
 
 def log(*a):
@@ -132,9 +150,7 @@ def main():
     n, depth = batch["n"], batch["depth"]
     log(f"[rank {rank}] batch ready: {n} paths, depth {depth}, {time.time() - t0:.1f}s")
 
-    if dist is not None:
-        import torch
-        flag = torch.zeros(1, dtype=torch.uint8, device="cuda")
+    from neptune_hip import shard
 
     def step(timed: bool):
         if timed:
@@ -145,9 +161,7 @@ def main():
             ctx.timing(False)
         ok = ctx.verdicts_all_dev(batch["d_v"], n)
         if dist is not None:
-            flag.fill_(1 if ok else 0)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            ok = bool(flag.item())
+            ok = shard.all_ok(ok, dist)  # the one exchange: RCCL all-reduce(MIN) of the batch verdict
         return ok
 
     def barrier_sync():
@@ -184,6 +198,7 @@ def main():
     value = perms_per_step * args.steps / elapsed
     kern_avg_s = kern_ms / max(launches, 1) / 1e3
     achieved = n * depth * TIP5_VALU_OPS_PER_PERM / kern_avg_s
+    traffic, traffic_tag = pmc_traffic("k_mtree_verify")
     res = {
         "metric": "Tip5 permutations/s verifying synthetic Merkle authentication paths (BASELINE config 2)",
         "value": value,
@@ -204,7 +219,9 @@ def main():
         "verdicts_correct": correct,
         "batch_verdict": batch_ok,
         "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
-                     "unit": "T VALU lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS, "traffic": None,
+                     "unit": "T VALU lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS, "traffic": traffic,
+                     "traffic_unit": "bytes per launch (FETCH_SIZE+WRITE_SIZE, raw; see DESIGN.md §3)",
+                     "traffic_profile": traffic_tag,
                      "kernel": "k_mtree_verify", "kernel_avg_ms": kern_avg_s * 1e3,
                      "valu_ops_per_perm": TIP5_VALU_OPS_PER_PERM,
                      "hbm_algorithmic_GBps": n * path_bytes(depth) / kern_avg_s / 1e9},

@@ -95,15 +95,18 @@ int carve(nhip_ctx* c, const size_t (&sizes)[N], void* (&ptrs)[N]) {
     return NHIP_OK;
 }
 
-__global__ void k_all_verdicts(const uint8_t* __restrict__ v, size_t n, uint32_t* __restrict__ out) {
-    __shared__ uint32_t ok;
-    if (threadIdx.x == 0) ok = 1u;
-    __syncthreads();
-    uint32_t mine = 1u;
-    for (size_t i = threadIdx.x; i < n; i += blockDim.x) mine &= (v[i] == 1) ? 1u : 0u;
-    if (!mine) atomicAnd(&ok, 0u);
-    __syncthreads();
-    if (threadIdx.x == 0) *out = ok;
+// Batch verdict: any_bad |= (v[i] != 1) over n bytes; 16 B per lane per step, one atomic per wave.
+__global__ void __launch_bounds__(256) k_any_bad(const uint8_t* __restrict__ v, size_t n, uint32_t* __restrict__ any_bad) {
+    uint32_t bad = 0;
+    const size_t n16 = (reinterpret_cast<uintptr_t>(v) & 15u) ? 0 : n / 16;  // unaligned: byte path
+    const uint4* __restrict__ v16 = reinterpret_cast<const uint4*>(v);
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
+        const uint4 w = v16[i];
+        bad |= (w.x ^ 0x01010101u) | (w.y ^ 0x01010101u) | (w.z ^ 0x01010101u) | (w.w ^ 0x01010101u);
+    }
+    for (size_t i = n16 * 16 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        bad |= (v[i] != 1) ? 1u : 0u;
+    if (__any(bad != 0) && (threadIdx.x & 63) == 0) atomicOr(any_bad, 1u);
 }
 
 int build_tree_dev(nhip_ctx* c, const uint64_t* d_leafs, size_t n, uint64_t* d_nodes) {
@@ -266,15 +269,21 @@ int nhip_verdicts_all_dev(nhip_ctx* c, const uint8_t* d_v, size_t n, uint8_t* al
     int rc = carve(c, sizes, p);
     if (rc) return rc;
     uint32_t* d_out = (uint32_t*)p[0];
+    hipError_t e = hipMemsetAsync(d_out, 0, sizeof(uint32_t), c->stream);
+    if (e != hipSuccess) return hip_fail(e);
+    size_t blocks = (n / 16 + 255) / 256;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 1024) blocks = 1024;
     rc = timed_launch(c, [&] {
-        hipLaunchKernelGGL(k_all_verdicts, dim3(1), dim3(1024), 0, c->stream, d_v, n, d_out);
+        hipLaunchKernelGGL(k_any_bad, dim3((unsigned)blocks), dim3(256), 0, c->stream, d_v, n, d_out);
         return hipGetLastError();
     });
     if (rc) return rc;
-    uint32_t h = 0;
-    hipError_t e = hipMemcpyAsync(&h, d_out, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+    uint32_t h = 1;
+    e = hipMemcpyAsync(&h, d_out, sizeof(h), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(e);
+    h = h ? 0u : 1u;
     *all_ok = (uint8_t)(h ? 1 : 0);
     return NHIP_OK;
 }

@@ -71,13 +71,22 @@ __device__ __forceinline__ uint64_t pow7(uint64_t x) {
     return mont_mul(x3, x4);
 }
 
-// x -> x^7 on 12 words at once (stage-interleaved Montgomery products).
+// x -> x^7 on 12 words, NHIP_POW7_GROUP words at a time (stage-interleaved Montgomery
+// products: wider groups fill more carry-chain wait states but hold more VGPRs).
+#ifndef NHIP_POW7_GROUP
+#define NHIP_POW7_GROUP 6
+#endif
 __device__ __forceinline__ void pow7_12(uint64_t* x) {
-    uint64_t x2[12], x4[12], x3[12];
-    mont_mul_n<12>(x, x, x2);
-    mont_mul_n<12>(x2, x2, x4);
-    mont_mul_n<12>(x, x2, x3);
-    mont_mul_n<12>(x3, x4, x);
+    constexpr int G = NHIP_POW7_GROUP;
+    static_assert(12 % G == 0, "group must divide 12");
+#pragma unroll
+    for (int g = 0; g < 12; g += G) {
+        uint64_t x2[G], x4[G], x3[G];
+        mont_mul_n<G>(x + g, x + g, x2);
+        mont_mul_n<G>(x2, x2, x4);
+        mont_mul_n<G>(x + g, x2, x3);
+        mont_mul_n<G>(x3, x4, x + g);
+    }
 }
 
 // MDS + ARK.  Circulant 16x16 with small (< 2^16) coefficients applied to the raw words: each

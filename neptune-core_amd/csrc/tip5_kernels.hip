@@ -15,6 +15,10 @@
 #include "tip5_device.hpp"
 #include "kernels.hpp"
 
+#ifndef NHIP_MINWAVES
+#define NHIP_MINWAVES 1  // min waves per SIMD requested from the register allocator
+#endif
+
 namespace nhip {
 
 __device__ __forceinline__ void load_digest_mont(const uint64_t* __restrict__ p, uint64_t* d) {
@@ -27,7 +31,7 @@ __device__ __forceinline__ void store_digest_canon(uint64_t* __restrict__ p, con
     for (int k = 0; k < 5; ++k) p[k] = from_mont(d[k]);
 }
 
-__global__ void __launch_bounds__(256) k_permutation(uint64_t* __restrict__ states, size_t n) {
+__global__ void __launch_bounds__(256, NHIP_MINWAVES) k_permutation(uint64_t* __restrict__ states, size_t n) {
     __shared__ Tip5Lds lds;
     tip5_lds_init(lds);
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -40,7 +44,7 @@ __global__ void __launch_bounds__(256) k_permutation(uint64_t* __restrict__ stat
     }
 }
 
-__global__ void __launch_bounds__(256) k_hash_pair(const uint64_t* __restrict__ left, const uint64_t* __restrict__ right,
+__global__ void __launch_bounds__(256, NHIP_MINWAVES) k_hash_pair(const uint64_t* __restrict__ left, const uint64_t* __restrict__ right,
                                                    uint64_t* __restrict__ out, size_t n) {
     __shared__ Tip5Lds lds;
     tip5_lds_init(lds);
@@ -55,7 +59,7 @@ __global__ void __launch_bounds__(256) k_hash_pair(const uint64_t* __restrict__ 
     }
 }
 
-__global__ void __launch_bounds__(256) k_hash_varlen(const uint64_t* __restrict__ data, const uint64_t* __restrict__ offsets,
+__global__ void __launch_bounds__(256, NHIP_MINWAVES) k_hash_varlen(const uint64_t* __restrict__ data, const uint64_t* __restrict__ offsets,
                                                      size_t n, uint64_t* __restrict__ out) {
     __shared__ Tip5Lds lds;
     tip5_lds_init(lds);
@@ -83,7 +87,7 @@ __global__ void __launch_bounds__(256) k_hash_varlen(const uint64_t* __restrict_
     }
 }
 
-__global__ void __launch_bounds__(256) k_mtree_level(const uint64_t* __restrict__ children, uint64_t* __restrict__ parents,
+__global__ void __launch_bounds__(256, NHIP_MINWAVES) k_mtree_level(const uint64_t* __restrict__ children, uint64_t* __restrict__ parents,
                                                      size_t n_parents) {
     __shared__ Tip5Lds lds;
     tip5_lds_init(lds);
@@ -99,7 +103,7 @@ __global__ void __launch_bounds__(256) k_mtree_level(const uint64_t* __restrict_
     }
 }
 
-__global__ void __launch_bounds__(256) k_mtree_verify(const uint64_t* __restrict__ roots, int per_path_root,
+__global__ void __launch_bounds__(256, NHIP_MINWAVES) k_mtree_verify(const uint64_t* __restrict__ roots, int per_path_root,
                                                       const uint64_t* __restrict__ indices,
                                                       const uint64_t* __restrict__ leaves,
                                                       const uint64_t* __restrict__ paths, uint32_t depth, size_t n,

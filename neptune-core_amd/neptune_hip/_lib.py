@@ -13,7 +13,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libneptune_hip.so")
+LIB_PATH = os.environ.get("NHIP_LIB") or os.path.join(_HERE, "libneptune_hip.so")
 
 NHIP_OK = 0
 _ERRORS = {1: "no HIP device", 2: "HIP runtime error", 3: "out of device memory", 4: "invalid argument"}

@@ -1,0 +1,80 @@
+"""N > 1 host path on CPU: world-size-2 gloo ranks shard independent units, verify their shard
+(with the C oracle standing in for the GPU, test-only), and exchange exactly the verdicts."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    for p in ("oracle", "neptune-core_amd"):
+        sys.path.insert(0, os.path.join(ROOT, p))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    import coracle as C
+    from neptune_hip import shard
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(99)  # same data on every rank
+    n, depth = 128, 7
+    leafs = rng.integers(0, 2**63, size=(n, 5), dtype=np.uint64)
+    nodes = C.mtree_build(leafs)
+    idx = np.arange(n, dtype=np.int64)
+    paths = np.empty((n, depth, 5), dtype=np.uint64)
+    paths[:, 0] = leafs[idx ^ 1]
+    run = idx + n
+    for k in range(1, depth):
+        run >>= 1
+        paths[:, k] = nodes[run ^ 1]
+    el = leafs.copy()
+    el[[5, 77]] ^= np.uint64(1)
+    costs = rng.integers(1, 10, size=n)
+    shards = shard.lpt_shard(costs, world)
+    mine = np.asarray(shards[rank], dtype=np.int64)
+    v = C.mtree_verify_batch(nodes[1], idx[mine].astype(np.uint64), el[mine], paths[mine].reshape(-1), depth)
+    ok = shard.all_ok(bool(v.all()), dist)
+    full = shard.gather_verdicts(v, shards, n, dist)
+    q.put((rank, ok, full.tolist(), [len(s) for s in shards]))
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharded_verdicts():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    expect = np.ones(128, dtype=np.uint8)
+    expect[[5, 77]] = 0
+    for rank, ok, full, sizes in res:
+        assert ok is False
+        assert full == expect.tolist()
+        assert sum(sizes) == 128 and abs(sizes[0] - sizes[1]) <= 16
+
+
+def test_lpt_shard_balances_and_covers():
+    sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
+    from neptune_hip import shard
+    costs = [16, 10, 11, 12, 12, 11, 9, 9] * 32
+    s = shard.lpt_shard(costs, 8)
+    assert sorted(i for r in s for i in r) == list(range(len(costs)))
+    loads = [sum(costs[i] for i in r) for r in s]
+    assert max(loads) - min(loads) <= max(costs)
+    assert shard.contiguous_shard(10, 3, 2) == range(8, 10)
