@@ -97,6 +97,71 @@ int nhip_mtree_verify_dev(nhip_ctx *ctx, const uint64_t *d_roots, size_t n_roots
 /* *all_ok = AND of n verdict bytes (device buffer), the per-batch / per-block verdict. */
 int nhip_verdicts_all_dev(nhip_ctx *ctx, const uint8_t *d_verdicts, size_t n, uint8_t *all_ok);
 
+/* ---- batched STARK verification ---------------------------------------------------------
+ * Replaces triton_vm::verify(Stark::default(), &claim, &proof) -> bool at its single production
+ * call site neptune-core/src/protocol/proof_abstractions/verifier.rs:60-63, batched
+ * (verify_batch) for the sequential callers proof_collection.rs:342-388, block_program.rs:51-65
+ * and state/mod.rs:2226-2272.  Semantics: verdict 1 = accept, 0 = reject (any decode or
+ * verification error, incl. empty / short / garbage proofs, as in the reference's reject tests).
+ * The AIR is data (nhip_air_create; format in DESIGN.md §9): triton-air's generated constraints
+ * are not vendored in the reference, so the AIR is supplied by the caller. */
+typedef struct {
+    uint32_t security_level;          /* Stark::default: 160 */
+    uint32_t log2_fri_expansion;      /* 2 (expansion factor 4) */
+    uint32_t num_collinearity_checks; /* security_level / log2_fri_expansion = 80; <= 256 */
+    uint32_t num_main;                /* main table columns (triton-vm: 379) */
+    uint32_t num_aux;                 /* auxiliary table columns (triton-vm: 88) */
+    uint32_t num_quotient_segments;   /* 4 */
+} nhip_stark_params;
+
+/* triton_vm::proof::Claim { program_digest, version, input, output } (canonical u64) */
+typedef struct {
+    uint64_t program_digest[5];
+    uint32_t version;
+    const uint64_t *input;
+    size_t input_len;
+    const uint64_t *output;
+    size_t output_len;
+} nhip_claim;
+
+/* triton_vm::proof::Proof(Vec<BFieldElement>) */
+typedef struct {
+    const uint64_t *words;
+    size_t len;
+} nhip_proof;
+
+typedef struct {
+    uint64_t num_proofs, proof_words, tip5_perms_static;
+    double ms_decode, ms_upload;  /* host */
+    double ms_fiat_shamir, ms_row_hash, ms_merkle, ms_ood_air, ms_fri, ms_deep, ms_device_total; /* device */
+} nhip_stats;
+
+typedef struct nhip_air nhip_air;
+typedef struct nhip_batch nhip_batch;
+
+void nhip_stark_params_default(nhip_stark_params *out);
+int nhip_air_create(const uint64_t *words, size_t n_words, nhip_air **out);
+void nhip_air_destroy(nhip_air *air);
+int nhip_air_info(const nhip_air *air, uint32_t *num_nodes, uint32_t *num_levels, uint32_t *num_constraints);
+/* Host-only structural decode (no GPU needed): 1 = decodes, 0 = malformed, < 0 = bad argument. */
+int nhip_proof_decodes(const nhip_air *air, const nhip_stark_params *params, const nhip_claim *claim,
+                       const nhip_proof *proof);
+/* One-shot: decode, upload, verify, verdicts[n]. */
+int nhip_verify_batch(nhip_ctx *ctx, nhip_air *air, const nhip_stark_params *params, const nhip_claim *claims,
+                      const nhip_proof *proofs, size_t n, uint8_t *verdicts, nhip_stats *stats);
+/* Device-resident form: prepare (host decode + one upload), run (device phases only) any number
+ * of times, read stats / the Fiat-Shamir transcript of one proof, destroy. */
+int nhip_batch_prepare(nhip_ctx *ctx, nhip_air *air, const nhip_stark_params *params, const nhip_claim *claims,
+                       const nhip_proof *proofs, size_t n, nhip_batch **out);
+int nhip_batch_run(nhip_ctx *ctx, nhip_batch *batch, uint8_t *verdicts, uint8_t *all_ok);
+int nhip_batch_stats(const nhip_batch *batch, nhip_stats *stats);
+/* Samples squeezed for proof `proof` in squeeze order (challenges, quotient weights, z, linear-
+ * combination weights, FRI folding challenges, last-round indeterminate) as canonical XFE
+ * triples, the FRI indices, and the proof's failure bits (0 = accepted). */
+int nhip_batch_transcript(nhip_ctx *ctx, const nhip_batch *batch, size_t proof, uint64_t *xfe_out, size_t xfe_cap,
+                          uint32_t *idx_out, size_t idx_cap, uint32_t *fail_bits, size_t *n_xfe);
+void nhip_batch_destroy(nhip_batch *batch);
+
 /* ---- kernel timing (HIP events on the ctx stream around every kernel launch) ------------ */
 int nhip_timing_enable(nhip_ctx *ctx, int on);
 /* Total device time of the kernels launched since the last reset, and their count. */

@@ -179,6 +179,11 @@ void nhip_destroy(nhip_ctx* c) {
 
 int nhip_device_ordinal(const nhip_ctx* c) { return c ? c->device : -1; }
 
+// internal accessors for the other translation units (not in the public header)
+hipStream_t nhip_internal_stream(nhip_ctx* c) { return c->stream; }
+int nhip_internal_device(nhip_ctx* c) { return c->device; }
+std::mutex* nhip_internal_mutex(nhip_ctx* c) { return &c->mu; }
+
 // ------------------------------------------------------------------ device-resident form
 int nhip_dev_alloc(nhip_ctx* c, size_t bytes, void** dptr) {
     if (!c || !dptr) return NHIP_ERR_ARG;

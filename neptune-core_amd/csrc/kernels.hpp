@@ -4,6 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "stark.hpp"
+
 namespace nhip {
 
 hipError_t launch_permutation(uint64_t* d_states, size_t n, hipStream_t st);
@@ -14,5 +16,37 @@ hipError_t launch_mtree_level(const uint64_t* d_children, uint64_t* d_parents, s
 hipError_t launch_mtree_verify(const uint64_t* d_roots, int per_path_root, const uint64_t* d_indices,
                                const uint64_t* d_leaves, const uint64_t* d_paths, uint32_t depth, size_t n,
                                uint8_t* d_verdicts, hipStream_t st);
+
+// ---- batched STARK verifier (stark_kernels.hip)
+static constexpr uint32_t AIR_LDS_HEADER = (256 + 4 + 4) * 24 + 16;  // red, zinv, derived, flag
+static constexpr uint32_t FRI_LDS_HEADER = 256 * 24 + 256 + 16;      // red, tip5 lut, flag
+
+struct StarkBatchDev {
+    uint32_t n_proofs, max_R;
+    StarkDims dims;
+    const uint64_t* words;
+    const ProofDesc* desc;
+    const FsOp* ops;
+    uint64_t* xs;
+    uint32_t* idx;
+    uint64_t* dig;
+    uint64_t* ood;
+    uint32_t* fail;
+    uint8_t* verdicts;
+    const AirNode* air_nodes;
+    const uint32_t* air_level_nodes;
+    const uint32_t* air_level_off;
+    uint32_t air_n_levels;
+    const uint32_t* air_cons;
+    uint4 air_cons_off;
+    size_t air_lds_bytes, fri_lds_bytes;
+};
+
+struct StarkPhaseTimer {
+    hipEvent_t ev[8];
+};
+
+hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, StarkPhaseTimer* tm);
+hipError_t stark_set_kernel_attributes();
 
 }  // namespace nhip

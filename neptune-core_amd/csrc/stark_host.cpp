@@ -1,0 +1,738 @@
+// Host side of the batched STARK verifier: AIR descriptor parsing/levelization, BFieldCodec
+// proof-stream decoding into ProofDesc offsets, the per-proof Fiat-Shamir program, device
+// staging, and the C ABI (include/neptune_hip.h: nhip_air_*, nhip_batch_*, nhip_verify_batch).
+//
+// Decoding restates triton-vm 1.0's `ProofStream::try_from(&Proof)` + the dequeue order of
+// `Stark::verify` (parity unpinned beyond the Claim layout, which is pinned by
+// neptune-core/src/protocol/consensus/transaction/validity/tasm/claims/new_claim.rs:38-100).
+// Any structural error gives verdict 0 (triton_vm::verify returns false on every Err), never an
+// infrastructure error: the reference's reject tests (verifier.rs:95-118 bogus proof,
+// neptune_proof.rs:118-133 empty / all-zero proofs) must come out as `false`.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/neptune_hip.h"
+#include "goldilocks.hpp"
+#include "kernels.hpp"
+#include "stark.hpp"
+
+using namespace nhip;
+
+namespace {
+
+constexpr uint64_t P = GL_P;
+
+enum ItemKind : uint32_t {
+    MERKLE_ROOT = 0, OOD_MAIN_ROW, OOD_AUX_ROW, OOD_QUOT_SEGMENTS, AUTH_STRUCTURE, MAIN_ROWS, AUX_ROWS,
+    LOG2_PADDED_HEIGHT, QUOT_SEGMENTS_ELEMENTS, FRI_CODEWORD, FRI_POLYNOMIAL, FRI_RESPONSE, N_KINDS
+};
+
+struct Item {
+    uint32_t kind;
+    uint64_t lo, hi;        // item words [lo, hi) (starting at the discriminant), absolute
+    uint64_t payload;       // first payload element (after counts)
+    uint64_t n;             // element count (dynamic kinds) / value (Log2PaddedHeight)
+    // FRI response only
+    uint64_t leaves_off, leaves_n, auth_off, auth_n;
+};
+
+inline uint32_t log2u(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
+
+struct Dims {
+    StarkDims d;
+    uint32_t expansion;
+};
+
+uint32_t fri_num_rounds(const Dims& D, uint64_t fri_len) {
+    const uint64_t dim = fri_len / D.expansion;
+    const uint32_t max_rounds = dim > 1 ? 64u - (uint32_t)__builtin_clzll(dim - 1) : 0u;
+    const uint32_t all = log2u(D.d.num_checks);
+    return max_rounds > all + 1 ? max_rounds - (all + 1) : 0u;
+}
+
+// Decode one ProofItem occupying words[lo, hi).  Returns false on any malformation.
+bool decode_item(const uint64_t* w, uint64_t lo, uint64_t hi, const Dims& D, Item& it) {
+    if (lo >= hi) return false;
+    it = Item{};
+    it.kind = (uint32_t)(w[lo] < N_KINDS ? w[lo] : N_KINDS);
+    it.lo = lo;
+    it.hi = hi;
+    const uint64_t len = hi - lo;
+    const StarkDims& d = D.d;
+    switch (it.kind) {
+        case MERKLE_ROOT: it.payload = lo + 1; return len == 1 + 5;
+        case OOD_MAIN_ROW: it.payload = lo + 1; return len == 1 + 3ull * d.num_main;
+        case OOD_AUX_ROW: it.payload = lo + 1; return len == 1 + 3ull * d.num_aux;
+        case OOD_QUOT_SEGMENTS: it.payload = lo + 1; return len == 1 + 3ull * d.num_quot_seg;
+        case LOG2_PADDED_HEIGHT:
+            if (len != 2) return false;
+            it.n = w[lo + 1];
+            return it.n < (1ull << 32);
+        case N_KINDS: return false;
+        default: break;
+    }
+    // dynamically sized payload: [kind, blen, body(blen)]
+    if (len < 2) return false;
+    const uint64_t blen = w[lo + 1];
+    if (blen != len - 2) return false;
+    const uint64_t b0 = lo + 2;
+    if (it.kind == FRI_RESPONSE) {
+        // FriResponse { auth_structure, revealed_leaves } encoded fields-reversed:
+        // [len(rl), n_leaves, leaves.., len(au), n_auth, digests..]
+        if (blen < 1) return false;
+        const uint64_t lrl = w[b0];
+        if (lrl < 1 || 1 + lrl > blen) return false;
+        const uint64_t nl = w[b0 + 1];
+        if (nl > (lrl - 1) / 3 || 3 * nl != lrl - 1) return false;
+        it.leaves_off = b0 + 2;
+        it.leaves_n = nl;
+        const uint64_t pa = b0 + 1 + lrl;
+        if (pa >= b0 + blen) return false;
+        const uint64_t lau = w[pa];
+        if (lau < 1 || 1 + lrl + 1 + lau != blen) return false;
+        const uint64_t na = w[pa + 1];
+        if (na > (lau - 1) / 5 || 5 * na != lau - 1) return false;
+        it.auth_off = pa + 2;
+        it.auth_n = na;
+        return true;
+    }
+    uint64_t width = 0;
+    switch (it.kind) {
+        case AUTH_STRUCTURE: width = 5; break;
+        case MAIN_ROWS: width = d.num_main; break;
+        case AUX_ROWS: width = 3ull * d.num_aux; break;
+        case QUOT_SEGMENTS_ELEMENTS: width = 3ull * d.num_quot_seg; break;
+        case FRI_CODEWORD: width = 3; break;
+        case FRI_POLYNOMIAL: width = 3; break;
+        default: return false;
+    }
+    if (blen < 1) return false;
+    const uint64_t n = w[b0];
+    if (width == 0 || n > (blen - 1) / width || n * width != blen - 1) return false;
+    it.n = n;
+    it.payload = b0 + 1;
+    return true;
+}
+
+struct HostBatch {
+    Dims D;
+    std::vector<uint64_t> words;
+    std::vector<ProofDesc> desc;
+    std::vector<FsOp> ops;
+    std::vector<uint32_t> fail;
+    uint64_t xs_total = 0, idx_total = 0;
+    uint32_t max_R = 0, max_last_cw = 1;
+    uint64_t perms_static = 0;  // FS + row hashing + last-codeword trees (Merkle paths counted on device)
+    uint64_t proof_words = 0;
+};
+
+uint64_t absorb_perms(uint64_t len) { return len / 10 + 1; }
+
+// Decode proof p into its descriptor; on malformation mark FAIL_DECODE and leave a benign desc.
+void decode_proof(HostBatch& B, const nhip_claim& claim, const nhip_proof& proof) {
+    const Dims& D = B.D;
+    const StarkDims& d = D.d;
+    ProofDesc pd{};
+    uint32_t fail = 0;
+    const uint64_t base = B.words.size();
+    const uint64_t len = proof.len;
+    B.proof_words += len;
+    for (uint64_t i = 0; i < len; ++i) {
+        const uint64_t v = proof.words[i];
+        B.words.push_back(v >= P ? v - P : v);
+    }
+    // stage the claim encoding (pinned layout): [out_n+1, out_n, out.., in_n+1, in_n, in.., version, digest]
+    const uint64_t cbase = B.words.size();
+    B.words.push_back(claim.output_len + 1);
+    B.words.push_back(claim.output_len);
+    for (size_t i = 0; i < claim.output_len; ++i) B.words.push_back(claim.output[i] % P);
+    B.words.push_back(claim.input_len + 1);
+    B.words.push_back(claim.input_len);
+    for (size_t i = 0; i < claim.input_len; ++i) B.words.push_back(claim.input[i] % P);
+    B.words.push_back(claim.version);
+    for (int i = 0; i < 5; ++i) B.words.push_back(claim.program_digest[i] % P);
+    const uint64_t clen = B.words.size() - cbase;
+    pd.claim_out_off = cbase + 2;
+    pd.claim_out_n = (uint32_t)claim.output_len;
+    pd.claim_in_off = cbase + 2 + claim.output_len + 2;
+    pd.claim_in_n = (uint32_t)claim.input_len;
+    pd.claim_digest_off = cbase + clen - 5;
+
+    const uint64_t* w = B.words.data();
+    std::vector<Item> items;
+    bool ok = len >= 2 && w[base] == len - 1;
+    if (ok) {
+        const uint64_t n_items = w[base + 1];
+        uint64_t pos = base + 2;
+        const uint64_t end = base + len;
+        for (uint64_t i = 0; ok && i < n_items; ++i) {
+            if (pos >= end) { ok = false; break; }
+            const uint64_t ln = w[pos++];
+            if (ln > end - pos) { ok = false; break; }
+            Item it;
+            ok = decode_item(w, pos, pos + ln, D, it);
+            items.push_back(it);
+            pos += ln;
+        }
+        ok = ok && pos == end;
+    }
+    // dequeue order of Stark::verify
+    uint32_t R = 0;
+    if (ok) {
+        size_t q = 0;
+        auto take = [&](uint32_t kind) -> const Item* {
+            if (!ok || q >= items.size() || items[q].kind != kind) { ok = false; return nullptr; }
+            return &items[q++];
+        };
+        const Item* lph = take(LOG2_PADDED_HEIGHT);
+        if (ok && lph->n > LOG2_PH_MAX) ok = false;
+        uint32_t log2_ph = 0, log2_T = 0, log2_N = 0;
+        if (ok) {
+            log2_ph = (uint32_t)lph->n;
+            const uint64_t ph = 1ull << log2_ph;
+            const uint64_t need = ph + d.num_trace_randomizers;
+            uint64_t T = 1;
+            while (T < need) T <<= 1;
+            log2_T = log2u(T);
+            log2_N = log2_T + d.log2_expansion;
+            R = fri_num_rounds(D, 1ull << log2_N);
+            if (R > MAX_FRI_ROUNDS || log2_N > 32) ok = false;
+        }
+        const Item* mr = take(MERKLE_ROOT);
+        const Item* ar = take(MERKLE_ROOT);
+        const Item* qr = take(MERKLE_ROOT);
+        const Item* mc = take(OOD_MAIN_ROW);
+        const Item* ac = take(OOD_AUX_ROW);
+        const Item* mn = take(OOD_MAIN_ROW);
+        const Item* an = take(OOD_AUX_ROW);
+        const Item* qs = take(OOD_QUOT_SEGMENTS);
+        const Item* fr[MAX_FRI_ROUNDS + 1] = {};
+        for (uint32_t r = 0; ok && r <= R; ++r) fr[r] = take(MERKLE_ROOT);
+        const Item* cw = take(FRI_CODEWORD);
+        const Item* poly = take(FRI_POLYNOMIAL);
+        const Item* resp[MAX_FRI_ROUNDS + 1] = {};
+        for (uint32_t r = 0; ok && r <= R; ++r) resp[r] = take(FRI_RESPONSE);
+        const Item* mrows = take(MAIN_ROWS);
+        const Item* mauth = take(AUTH_STRUCTURE);
+        const Item* arows = take(AUX_ROWS);
+        const Item* aauth = take(AUTH_STRUCTURE);
+        const Item* qrows = take(QUOT_SEGMENTS_ELEMENTS);
+        const Item* qauth = take(AUTH_STRUCTURE);
+        if (ok && q != items.size()) ok = false;  // items left
+        const uint32_t k = d.num_checks;
+        if (ok) {
+            for (uint32_t r = 0; r <= R; ++r)
+                if (resp[r]->leaves_n != k) ok = false;
+            if (mrows->n != k || arows->n != k || qrows->n != k) ok = false;
+            if (cw->n != (1ull << (log2_N - R))) ok = false;
+        }
+        if (ok) {
+            pd.log2_ph = log2_ph;
+            pd.log2_T = log2_T;
+            pd.log2_N = log2_N;
+            pd.R = R;
+            pd.main_root = mr->payload;
+            pd.aux_root = ar->payload;
+            pd.quot_root = qr->payload;
+            pd.ood_mc = mc->payload;
+            pd.ood_ac = ac->payload;
+            pd.ood_mn = mn->payload;
+            pd.ood_an = an->payload;
+            pd.ood_qs = qs->payload;
+            for (uint32_t r = 0; r <= R; ++r) {
+                pd.fri_root[r] = fr[r]->payload;
+                pd.fri[r].auth_off = resp[r]->auth_off;
+                pd.fri[r].auth_n = (uint32_t)resp[r]->auth_n;
+                pd.fri[r].leaves_off = resp[r]->leaves_off;
+                pd.fri[r].leaves_n = (uint32_t)resp[r]->leaves_n;
+            }
+            pd.last_cw_off = cw->payload;
+            pd.last_cw_n = (uint32_t)cw->n;
+            pd.last_poly_off = poly->payload;
+            pd.last_poly_n = (uint32_t)poly->n;
+            // degree of the last polynomial (highest non-zero coefficient) vs the FRI bound
+            int64_t deg = -1;
+            for (uint64_t c = 0; c < poly->n; ++c) {
+                const uint64_t* x = w + poly->payload + 3 * c;
+                if (x[0] | x[1] | x[2]) deg = (int64_t)c;
+            }
+            const uint64_t first_max = (1ull << log2_N) / D.expansion - 1;
+            const uint64_t last_max = first_max >> R;
+            pd.last_poly_degree_ok = deg <= (int64_t)last_max ? 1u : 0u;
+            pd.main_rows_off = mrows->payload;
+            pd.aux_rows_off = arows->payload;
+            pd.quot_rows_off = qrows->payload;
+            pd.main_auth_off = mauth->payload;
+            pd.main_auth_n = (uint32_t)mauth->n;
+            pd.aux_auth_off = aauth->payload;
+            pd.aux_auth_n = (uint32_t)aauth->n;
+            pd.quot_auth_off = qauth->payload;
+            pd.quot_auth_n = (uint32_t)qauth->n;
+            pd.rows_n = k;
+            // Fiat-Shamir program (order of Stark::verify + Fri::verify)
+            pd.fs_op_off = (uint32_t)B.ops.size();
+            uint64_t perms = 0;
+            auto absorb = [&](uint64_t off, uint64_t n) {
+                B.ops.push_back(FsOp{FS_ABSORB, (uint32_t)n, off});
+                perms += absorb_perms(n);
+            };
+            auto squeeze = [&](uint32_t n) {
+                B.ops.push_back(FsOp{FS_SQUEEZE_X, n, 0});
+                perms += (3ull * n + 9) / 10;
+            };
+            auto absorb_item = [&](const Item* it) { absorb(it->lo, it->hi - it->lo); };
+            absorb(cbase, clen);
+            absorb_item(mr);
+            squeeze(d.num_sampled);
+            absorb_item(ar);
+            squeeze(d.num_constraints);
+            absorb_item(qr);
+            squeeze(1);
+            absorb_item(mc);
+            absorb_item(ac);
+            absorb_item(mn);
+            absorb_item(an);
+            absorb_item(qs);
+            squeeze(d.num_main + d.num_aux + d.num_quot_seg + d.num_deep);
+            for (uint32_t r = 0; r <= R; ++r) {
+                absorb_item(fr[r]);
+                if (r < R) squeeze(1);
+            }
+            B.ops.push_back(FsOp{FS_SAMPLE_IDX, k, 1ull << log2_N});
+            perms += (k + 9) / 10;
+            squeeze(1);
+            pd.fs_op_n = (uint32_t)(B.ops.size() - pd.fs_op_off);
+            // rows + last codeword tree
+            perms += (uint64_t)k * (absorb_perms(d.num_main) + absorb_perms(3ull * d.num_aux) +
+                                    absorb_perms(3ull * d.num_quot_seg));
+            perms += cw->n - 1;
+            B.perms_static += perms;
+        }
+    }
+    if (!ok) {
+        fail |= FAIL_DECODE;
+        pd = ProofDesc{};
+        pd.claim_out_off = cbase + 2;
+        pd.claim_in_off = cbase + 2 + claim.output_len + 2;
+        pd.claim_digest_off = cbase + clen - 5;
+    }
+    const SampleLayout sl = SampleLayout::of(d, pd.R);
+    pd.xs_off = B.xs_total;
+    pd.n_xs = sl.total;
+    B.xs_total += sl.total;
+    pd.idx_off = B.idx_total;
+    B.idx_total += d.num_checks;
+    if (pd.R > B.max_R) B.max_R = pd.R;
+    if (pd.last_cw_n > B.max_last_cw) B.max_last_cw = pd.last_cw_n;
+    B.desc.push_back(pd);
+    B.fail.push_back(fail);
+}
+
+}  // namespace
+
+// ====================================================================== AIR object
+struct nhip_air {
+    StarkDims dims_air{};  // num_main, num_aux, num_sampled, num_constraints filled
+    std::vector<AirNode> nodes;
+    std::vector<uint32_t> level_nodes, level_off, cons;
+    uint4 cons_off{};
+    // device copies per context (one context per process in practice)
+    nhip_ctx* dev_ctx = nullptr;
+    AirNode* d_nodes = nullptr;
+    uint32_t *d_level_nodes = nullptr, *d_level_off = nullptr, *d_cons = nullptr;
+};
+
+struct nhip_batch {
+    HostBatch H;
+    const nhip_air* air = nullptr;
+    int device = 0;
+    // device buffers
+    void* dmem = nullptr;
+    StarkBatchDev dev{};
+    uint32_t* d_fail_init = nullptr;
+    uint64_t* d_perm_counter = nullptr;
+    StarkPhaseTimer tm{};
+    bool timed = false;
+    double last_ms[8] = {};
+    double decode_ms = 0, upload_ms = 0;
+};
+
+// ctx internals live in capi.hip; access the stream / device via these helpers
+extern "C" hipStream_t nhip_internal_stream(nhip_ctx* c);
+extern "C" int nhip_internal_device(nhip_ctx* c);
+extern "C" std::mutex* nhip_internal_mutex(nhip_ctx* c);
+
+namespace {
+
+int hipfail(hipError_t e) { return e == hipSuccess ? NHIP_OK : (e == hipErrorOutOfMemory ? NHIP_ERR_OOM : NHIP_ERR_HIP); }
+
+bool dims_from(const nhip_stark_params* sp, const nhip_air* air, Dims& D) {
+    if (!sp || !air) return false;
+    if (sp->num_collinearity_checks < 1 || sp->num_collinearity_checks > (uint32_t)MAX_CHECKS) return false;
+    if (sp->log2_fri_expansion < 1 || sp->log2_fri_expansion > 8) return false;
+    if (sp->num_main != air->dims_air.num_main || sp->num_aux != air->dims_air.num_aux) return false;
+    if (sp->num_quotient_segments < 1 || sp->num_quotient_segments > 64) return false;
+    StarkDims& d = D.d;
+    d.num_main = sp->num_main;
+    d.num_aux = sp->num_aux;
+    d.num_quot_seg = sp->num_quotient_segments;
+    d.num_checks = sp->num_collinearity_checks;
+    d.num_deep = 3;
+    d.log2_expansion = sp->log2_fri_expansion;
+    d.num_trace_randomizers = sp->num_collinearity_checks + 2 * 3;
+    d.num_sampled = air->dims_air.num_sampled;
+    d.num_constraints = air->dims_air.num_constraints;
+    D.expansion = 1u << sp->log2_fri_expansion;
+    // the last FRI codeword (at most 2^(floor(log2 k) + 1 + log2 expansion) XFEs) is rebuilt into a
+    // Merkle tree in one workgroup's LDS
+    if ((1ull << (log2u(d.num_checks) + 1 + d.log2_expansion)) > 4096) return false;
+    return true;
+}
+
+int air_upload(nhip_ctx* ctx, nhip_air* a) {
+    if (a->dev_ctx == ctx) return NHIP_OK;
+    hipError_t e = hipMalloc(&a->d_nodes, a->nodes.size() * sizeof(AirNode));
+    if (e == hipSuccess) e = hipMalloc(&a->d_level_nodes, a->level_nodes.size() * 4 + 4);
+    if (e == hipSuccess) e = hipMalloc(&a->d_level_off, a->level_off.size() * 4 + 4);
+    if (e == hipSuccess) e = hipMalloc(&a->d_cons, a->cons.size() * 4 + 4);
+    if (e == hipSuccess) e = hipMemcpy(a->d_nodes, a->nodes.data(), a->nodes.size() * sizeof(AirNode), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(a->d_level_nodes, a->level_nodes.data(), a->level_nodes.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(a->d_level_off, a->level_off.data(), a->level_off.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(a->d_cons, a->cons.data(), a->cons.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hipfail(e);
+    a->dev_ctx = ctx;
+    return NHIP_OK;
+}
+
+inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" {
+
+void nhip_stark_params_default(nhip_stark_params* out) {
+    if (!out) return;
+    out->security_level = 160;
+    out->log2_fri_expansion = 2;
+    out->num_collinearity_checks = 80;  // security_level / log2_fri_expansion
+    out->num_main = 379;
+    out->num_aux = 88;
+    out->num_quotient_segments = 4;
+}
+
+int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
+    if (!w || !out || n < 9) return NHIP_ERR_ARG;
+    *out = nullptr;
+    if (w[0] != 0x41495231ull) return NHIP_ERR_ARG;
+    const uint64_t M = w[1], A = w[2], K = w[3], NN = w[4];
+    const uint64_t nc[4] = {w[5], w[6], w[7], w[8]};
+    const uint64_t C = nc[0] + nc[1] + nc[2] + nc[3];
+    if (M > (1u << 20) || A > (1u << 20) || K < 3 || K > (1u << 20) || NN > (1u << 24) || C > (1u << 24)) return NHIP_ERR_ARG;
+    if (n != 9 + 4 * NN + C) return NHIP_ERR_ARG;
+    nhip_air* a = new (std::nothrow) nhip_air();
+    if (!a) return NHIP_ERR_OOM;
+    a->dims_air.num_main = (uint32_t)M;
+    a->dims_air.num_aux = (uint32_t)A;
+    a->dims_air.num_sampled = (uint32_t)K;
+    a->dims_air.num_constraints = (uint32_t)C;
+    a->nodes.resize(NN);
+    std::vector<uint32_t> level(NN, 0);
+    uint32_t max_level = 0;
+    const uint64_t* nw = w + 9;
+    for (uint64_t i = 0; i < NN; ++i) {
+        const uint64_t op = nw[4 * i], x = nw[4 * i + 1], y = nw[4 * i + 2], z = nw[4 * i + 3];
+        AirNode nd{};
+        nd.op = (uint32_t)op;
+        bool ok = true;
+        if (op == AIR_INPUT) {
+            const uint64_t lim = x == IN_MAIN_CURR || x == IN_MAIN_NEXT ? M
+                                 : (x == IN_AUX_CURR || x == IN_AUX_NEXT ? A : (x == IN_CHALLENGE ? K + 3 : 0));
+            ok = x <= IN_CHALLENGE && y < lim;
+            nd.a = (uint32_t)x;
+            nd.b = (uint32_t)y;
+        } else if (op == AIR_CONST) {
+            nd.k0 = to_mont(x);
+            nd.k1 = to_mont(y);
+            nd.k2 = to_mont(z);
+        } else if (op == AIR_ADD || op == AIR_SUB || op == AIR_MUL) {
+            ok = x < i && y < i;
+            nd.a = (uint32_t)x;
+            nd.b = (uint32_t)y;
+            if (ok) level[i] = 1 + std::max(level[x], level[y]);
+        } else {
+            ok = false;
+        }
+        if (!ok) {
+            delete a;
+            return NHIP_ERR_ARG;
+        }
+        a->nodes[i] = nd;
+        max_level = std::max(max_level, level[i]);
+    }
+    a->level_off.assign(max_level + 2, 0);
+    for (uint64_t i = 0; i < NN; ++i) a->level_off[level[i] + 1]++;
+    for (uint32_t l = 0; l <= max_level; ++l) a->level_off[l + 1] += a->level_off[l];
+    a->level_nodes.resize(NN);
+    std::vector<uint32_t> fillp(a->level_off.begin(), a->level_off.end() - 1);
+    for (uint64_t i = 0; i < NN; ++i) a->level_nodes[fillp[level[i]]++] = (uint32_t)i;
+    const uint64_t* cw = nw + 4 * NN;
+    a->cons.resize(C);
+    for (uint64_t i = 0; i < C; ++i) {
+        if (cw[i] >= NN) {
+            delete a;
+            return NHIP_ERR_ARG;
+        }
+        a->cons[i] = (uint32_t)cw[i];
+    }
+    a->cons_off = make_uint4((uint32_t)nc[0], (uint32_t)(nc[0] + nc[1]), (uint32_t)(nc[0] + nc[1] + nc[2]), (uint32_t)C);
+    *out = a;
+    return NHIP_OK;
+}
+
+void nhip_air_destroy(nhip_air* a) {
+    if (!a) return;
+    if (a->dev_ctx) {
+        (void)hipFree(a->d_nodes);
+        (void)hipFree(a->d_level_nodes);
+        (void)hipFree(a->d_level_off);
+        (void)hipFree(a->d_cons);
+    }
+    delete a;
+}
+
+int nhip_air_info(const nhip_air* a, uint32_t* num_nodes, uint32_t* num_levels, uint32_t* num_constraints) {
+    if (!a) return NHIP_ERR_ARG;
+    if (num_nodes) *num_nodes = (uint32_t)a->nodes.size();
+    if (num_levels) *num_levels = (uint32_t)a->level_off.size() - 1;
+    if (num_constraints) *num_constraints = a->dims_air.num_constraints;
+    return NHIP_OK;
+}
+
+// Host-only structural check (no GPU): 1 if the proof stream decodes with the expected item
+// sequence and counts, else 0.  Used by CPU tests of the decoder and by callers that want to
+// reject garbage before touching a device.
+int nhip_proof_decodes(const nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claim,
+                       const nhip_proof* proof) {
+    Dims D{};
+    if (!claim || !proof || (proof->len && !proof->words) || !dims_from(sp, air, D)) return -NHIP_ERR_ARG;
+    HostBatch B;
+    B.D = D;
+    decode_proof(B, *claim, *proof);
+    return B.fail[0] ? 0 : 1;
+}
+
+int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
+                       const nhip_proof* proofs, size_t n, nhip_batch** out) {
+    if (!ctx || !out || (n && (!claims || !proofs))) return NHIP_ERR_ARG;
+    *out = nullptr;
+    Dims D{};
+    if (!dims_from(sp, air, D)) return NHIP_ERR_ARG;
+    for (size_t i = 0; i < n; ++i)
+        if ((proofs[i].len && !proofs[i].words) || (claims[i].input_len && !claims[i].input) ||
+            (claims[i].output_len && !claims[i].output))
+            return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
+    (void)hipSetDevice(nhip_internal_device(ctx));
+    nhip_batch* b = new (std::nothrow) nhip_batch();
+    if (!b) return NHIP_ERR_OOM;
+    b->air = air;
+    b->device = nhip_internal_device(ctx);
+    auto t0 = std::chrono::steady_clock::now();
+    HostBatch& H = b->H;
+    H.D = D;
+    H.desc.reserve(n);
+    H.fail.reserve(n);
+    for (size_t i = 0; i < n; ++i) decode_proof(H, claims[i], proofs[i]);
+    auto t1 = std::chrono::steady_clock::now();
+    b->decode_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    int rc = air_upload(ctx, air);
+    if (rc) {
+        delete b;
+        return rc;
+    }
+    static bool attrs = false;
+    if (!attrs) {
+        if (stark_set_kernel_attributes() != hipSuccess) {
+            delete b;
+            return NHIP_ERR_HIP;
+        }
+        attrs = true;
+    }
+    const uint32_t k = D.d.num_checks;
+    const size_t sz[] = {H.words.size() * 8 + 8,
+                         std::max<size_t>(1, n) * sizeof(ProofDesc),
+                         H.ops.size() * sizeof(FsOp) + 8,
+                         H.xs_total * 24 + 8,
+                         H.idx_total * 4 + 8,
+                         std::max<size_t>(1, n) * 3 * k * 40,
+                         std::max<size_t>(1, n) * 9 * 8,
+                         std::max<size_t>(1, n) * 4,
+                         std::max<size_t>(1, n) * 4,
+                         std::max<size_t>(1, n),
+                         8};
+    size_t total = 0;
+    for (size_t s : sz) total += al(s);
+    hipError_t e = hipMalloc(&b->dmem, total);
+    if (e != hipSuccess) {
+        delete b;
+        return hipfail(e);
+    }
+    char* p = (char*)b->dmem;
+    void* ptr[11];
+    for (int i = 0; i < 11; ++i) {
+        ptr[i] = p;
+        p += al(sz[i]);
+    }
+    hipStream_t st = nhip_internal_stream(ctx);
+    e = hipMemcpyAsync(ptr[0], H.words.data(), H.words.size() * 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && n) e = hipMemcpyAsync(ptr[1], H.desc.data(), n * sizeof(ProofDesc), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && !H.ops.empty())
+        e = hipMemcpyAsync(ptr[2], H.ops.data(), H.ops.size() * sizeof(FsOp), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && n) e = hipMemcpyAsync(ptr[8], H.fail.data(), n * 4, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    auto t2 = std::chrono::steady_clock::now();
+    b->upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    if (e != hipSuccess) {
+        (void)hipFree(b->dmem);
+        delete b;
+        return hipfail(e);
+    }
+    StarkBatchDev& dv = b->dev;
+    dv.n_proofs = (uint32_t)n;
+    dv.max_R = H.max_R;
+    dv.dims = D.d;
+    dv.words = (const uint64_t*)ptr[0];
+    dv.desc = (const ProofDesc*)ptr[1];
+    dv.ops = (const FsOp*)ptr[2];
+    dv.xs = (uint64_t*)ptr[3];
+    dv.idx = (uint32_t*)ptr[4];
+    dv.dig = (uint64_t*)ptr[5];
+    dv.ood = (uint64_t*)ptr[6];
+    dv.fail = (uint32_t*)ptr[7];
+    b->d_fail_init = (uint32_t*)ptr[8];
+    dv.verdicts = (uint8_t*)ptr[9];
+    b->d_perm_counter = (uint64_t*)ptr[10];
+    dv.air_nodes = air->d_nodes;
+    dv.air_level_nodes = air->d_level_nodes;
+    dv.air_level_off = air->d_level_off;
+    dv.air_n_levels = (uint32_t)air->level_off.size() - 1;
+    dv.air_cons = air->d_cons;
+    dv.air_cons_off = air->cons_off;
+    dv.air_lds_bytes = AIR_LDS_HEADER + air->nodes.size() * 24;
+    dv.fri_lds_bytes = FRI_LDS_HEADER + (size_t)H.max_last_cw * 40;
+    if (dv.air_lds_bytes > 160 * 1024 - 8192 || dv.fri_lds_bytes > 160 * 1024 - 16384) {
+        (void)hipFree(b->dmem);
+        delete b;
+        return NHIP_ERR_ARG;  // AIR too large for the single-workgroup LDS evaluator
+    }
+    *out = b;
+    return NHIP_OK;
+}
+
+int nhip_batch_run(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* all_ok) {
+    if (!ctx || !b) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
+    (void)hipSetDevice(b->device);
+    hipStream_t st = nhip_internal_stream(ctx);
+    const uint32_t n = b->dev.n_proofs;
+    hipError_t e = hipSuccess;
+    if (n) e = hipMemcpyAsync(b->dev.fail, b->d_fail_init, n * 4, hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) return hipfail(e);
+    if (!b->timed) {
+        for (int i = 0; i < 8; ++i)
+            if (hipEventCreate(&b->tm.ev[i]) != hipSuccess) return NHIP_ERR_HIP;
+        b->timed = true;
+    }
+    e = launch_stark_phases(b->dev, st, &b->tm);
+    if (e != hipSuccess) return hipfail(e);
+    std::vector<uint8_t> v(n);
+    if (n) e = hipMemcpyAsync(v.data(), b->dev.verdicts, n, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hipfail(e);
+    for (int i = 0; i < 7; ++i) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, b->tm.ev[i], b->tm.ev[i + 1]);
+        b->last_ms[i] = ms;
+    }
+    if (verdicts && n) std::memcpy(verdicts, v.data(), n);
+    if (all_ok) {
+        uint8_t a = 1;
+        for (uint32_t i = 0; i < n; ++i) a &= v[i];
+        *all_ok = a;
+    }
+    return NHIP_OK;
+}
+
+int nhip_batch_stats(const nhip_batch* b, nhip_stats* s) {
+    if (!b || !s) return NHIP_ERR_ARG;
+    std::memset(s, 0, sizeof(*s));
+    s->num_proofs = b->dev.n_proofs;
+    s->proof_words = b->H.proof_words;
+    s->ms_decode = b->decode_ms;
+    s->ms_upload = b->upload_ms;
+    s->ms_fiat_shamir = b->last_ms[0];
+    s->ms_row_hash = b->last_ms[1];
+    s->ms_merkle = b->last_ms[2];
+    s->ms_ood_air = b->last_ms[3];
+    s->ms_fri = b->last_ms[4];
+    s->ms_deep = b->last_ms[5];
+    s->ms_device_total = 0;
+    for (int i = 0; i < 7; ++i) s->ms_device_total += b->last_ms[i];
+    s->tip5_perms_static = b->H.perms_static;
+    return NHIP_OK;
+}
+
+int nhip_batch_transcript(nhip_ctx* ctx, const nhip_batch* b, size_t proof, uint64_t* xfe_out, size_t xfe_cap,
+                          uint32_t* idx_out, size_t idx_cap, uint32_t* fail_out, size_t* n_xfe) {
+    if (!ctx || !b || proof >= b->dev.n_proofs) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
+    (void)hipSetDevice(b->device);
+    hipStream_t st = nhip_internal_stream(ctx);
+    const ProofDesc& pd = b->H.desc[proof];
+    const size_t nx = pd.n_xs;
+    if (n_xfe) *n_xfe = nx;
+    std::vector<uint64_t> raw(nx * 3);
+    hipError_t e = hipSuccess;
+    if (nx) e = hipMemcpyAsync(raw.data(), b->dev.xs + pd.xs_off * 3, nx * 24, hipMemcpyDeviceToHost, st);
+    std::vector<uint32_t> ix(b->dev.dims.num_checks);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(ix.data(), b->dev.idx + pd.idx_off, ix.size() * 4, hipMemcpyDeviceToHost, st);
+    uint32_t f = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&f, b->dev.fail + proof, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hipfail(e);
+    if (xfe_out)
+        for (size_t i = 0; i < std::min(nx * 3, xfe_cap * 3); ++i) xfe_out[i] = from_mont(raw[i]);
+    if (idx_out) std::memcpy(idx_out, ix.data(), std::min(ix.size(), idx_cap) * 4);
+    if (fail_out) *fail_out = f;
+    return NHIP_OK;
+}
+
+void nhip_batch_destroy(nhip_batch* b) {
+    if (!b) return;
+    (void)hipSetDevice(b->device);
+    if (b->timed)
+        for (int i = 0; i < 8; ++i) (void)hipEventDestroy(b->tm.ev[i]);
+    if (b->dmem) (void)hipFree(b->dmem);
+    delete b;
+}
+
+int nhip_verify_batch(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
+                      const nhip_proof* proofs, size_t n, uint8_t* verdicts, nhip_stats* stats) {
+    if (!verdicts && n) return NHIP_ERR_ARG;
+    nhip_batch* b = nullptr;
+    int rc = nhip_batch_prepare(ctx, air, sp, claims, proofs, n, &b);
+    if (rc) return rc;
+    rc = nhip_batch_run(ctx, b, verdicts, nullptr);
+    if (!rc && stats) nhip_batch_stats(b, stats);
+    nhip_batch_destroy(b);
+    return rc;
+}
+
+}  // extern "C"

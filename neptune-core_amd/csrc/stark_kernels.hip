@@ -1,0 +1,714 @@
+// Phase kernels of the batched STARK verifier (see stark.hpp for the phase list).
+//
+// Conventions: the batch word buffer holds canonical u64 field elements (proof words and staged
+// claims); every scratch value written by these kernels (samples, row digests, OOD sums) is a raw
+// Montgomery word.  Each failed check ORs a FailBits bit into fail[proof].
+#include "kernels.hpp"
+#include "stark.hpp"
+#include "tip5_device.hpp"
+#include "xfe.hpp"
+
+namespace nhip {
+
+
+__device__ __forceinline__ Xfe ld_xfe_canon(const uint64_t* __restrict__ w, uint64_t off) {
+    return {to_mont(w[off]), to_mont(w[off + 1]), to_mont(w[off + 2])};
+}
+__device__ __forceinline__ Xfe ld_xfe_raw(const uint64_t* __restrict__ w, uint64_t off) {
+    return {w[off], w[off + 1], w[off + 2]};
+}
+__device__ __forceinline__ void st_xfe_raw(uint64_t* __restrict__ w, uint64_t off, Xfe v) {
+    w[off] = v.c0;
+    w[off + 1] = v.c1;
+    w[off + 2] = v.c2;
+}
+__device__ __forceinline__ bool x_is_zero(Xfe a) { return (a.c0 | a.c1 | a.c2) == 0; }
+
+// primitive root of unity of order 2^k (raw Montgomery): 7^((p-1) / 2^k)
+__device__ __forceinline__ uint64_t root_of_unity(uint32_t log2n) {
+    return b_pow(to_mont(7), (GL_P - 1) >> log2n);
+}
+
+// ------------------------------------------------------------------ Fiat-Shamir replay
+// One lane per proof replays the proof's sponge program: pad_and_absorb_all of the claim and of
+// every Fiat-Shamir item, squeezes for sample_scalars, sample_indices (skip BFieldElement::MAX,
+// `value as u32 % bound`).
+__global__ void __launch_bounds__(64) k_fs_replay(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+                                                  const FsOp* __restrict__ ops, uint32_t n_proofs,
+                                                  uint64_t* __restrict__ xs, uint32_t* __restrict__ idx_out,
+                                                  const uint32_t* __restrict__ fail) {
+    __shared__ Tip5Lds lds;
+    tip5_lds_init(lds);
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_proofs || fail[p]) return;
+    const ProofDesc& d = desc[p];
+    uint64_t s[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s[k] = 0;
+    uint64_t xcur = d.xs_off * 3;  // word cursor into xs
+    uint64_t icur = d.idx_off;
+    for (uint32_t o = 0; o < d.fs_op_n; ++o) {
+        const FsOp op = ops[d.fs_op_off + o];
+        if (op.kind == FS_ABSORB) {
+            const uint64_t* __restrict__ src = words + op.arg;
+            const uint32_t len = op.n;
+            uint32_t pos = 0;
+            for (; pos + TIP5_RATE <= len; pos += TIP5_RATE) {
+#pragma unroll
+                for (int k = 0; k < TIP5_RATE; ++k) s[k] = to_mont(src[pos + k]);
+                tip5_permute_raw(s, lds.lut);
+            }
+            const uint32_t rem = len - pos;
+#pragma unroll
+            for (int k = 0; k < TIP5_RATE; ++k) {
+                const uint32_t kk = (uint32_t)k;
+                s[k] = kk < rem ? to_mont(src[pos + kk]) : (kk == rem ? MONT_ONE : 0ull);
+            }
+            tip5_permute_raw(s, lds.lut);
+        } else if (op.kind == FS_SQUEEZE_X) {
+            const uint32_t nwords = 3 * op.n;
+            for (uint32_t f = 0; f < nwords; f += TIP5_RATE) {
+#pragma unroll
+                for (int k = 0; k < TIP5_RATE; ++k)
+                    if (f + (uint32_t)k < nwords) xs[xcur + f + k] = s[k];
+                tip5_permute_raw(s, lds.lut);
+            }
+            xcur += nwords;
+        } else {  // FS_SAMPLE_IDX
+            const uint64_t bound = op.arg;
+            uint32_t got = 0;
+            while (got < op.n) {
+                uint64_t out[TIP5_RATE];
+#pragma unroll
+                for (int k = 0; k < TIP5_RATE; ++k) out[k] = from_mont(s[k]);
+                tip5_permute_raw(s, lds.lut);
+                for (int k = 0; k < TIP5_RATE && got < op.n; ++k) {
+                    if (out[k] != GL_P - 1) idx_out[icur + got++] = (uint32_t)((out[k] & 0xFFFFFFFFull) % bound);
+                }
+            }
+            icur += op.n;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ revealed-row hashing
+// grid.y = 0 main, 1 aux, 2 quotient; one lane per (proof, row).
+__global__ void __launch_bounds__(256) k_hash_rows(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+                                                   uint32_t n_proofs, uint32_t k, StarkDims dims,
+                                                   uint64_t* __restrict__ dig, const uint32_t* __restrict__ fail) {
+    __shared__ Tip5Lds lds;
+    tip5_lds_init(lds);
+    const uint32_t tree = blockIdx.y;
+    const uint32_t width = tree == 0 ? dims.num_main : (tree == 1 ? 3 * dims.num_aux : 3 * dims.num_quot_seg);
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < (uint64_t)n_proofs * k;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = (uint32_t)(t / k), j = (uint32_t)(t % k);
+        if (fail[p]) continue;
+        const ProofDesc& d = desc[p];
+        const uint64_t base = (tree == 0 ? d.main_rows_off : (tree == 1 ? d.aux_rows_off : d.quot_rows_off)) +
+                              (uint64_t)j * width;
+        const uint64_t* __restrict__ row = words + base;
+        uint64_t s[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) s[q] = 0;
+        uint32_t pos = 0;
+        for (; pos + TIP5_RATE <= width; pos += TIP5_RATE) {
+#pragma unroll
+            for (int q = 0; q < TIP5_RATE; ++q) s[q] = to_mont(row[pos + q]);
+            tip5_permute_raw(s, lds.lut);
+        }
+        const uint32_t rem = width - pos;
+#pragma unroll
+        for (int q = 0; q < TIP5_RATE; ++q) {
+            const uint32_t qq = (uint32_t)q;
+            s[q] = qq < rem ? to_mont(row[pos + qq]) : (qq == rem ? MONT_ONE : 0ull);
+        }
+        tip5_permute_raw(s, lds.lut);
+        uint64_t* __restrict__ o = dig + (((uint64_t)p * 3 + tree) * k + j) * 5;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) o[q] = s[q];
+    }
+}
+
+// ------------------------------------------------------------------ workgroup helpers
+// exclusive prefix sum over blockDim.x (<= 256) values; returns the total
+__device__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* sh, uint32_t& excl) {
+    const uint32_t tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (uint32_t off = 1; off < blockDim.x; off <<= 1) {
+        const uint32_t t = tid >= off ? sh[tid - off] : 0u;
+        __syncthreads();
+        sh[tid] += t;
+        __syncthreads();
+    }
+    const uint32_t incl = sh[tid];
+    const uint32_t total = sh[blockDim.x - 1];
+    __syncthreads();
+    excl = incl - v;
+    return total;
+}
+
+__device__ __forceinline__ void hash_pair_raw(const uint64_t* l, const uint64_t* r, uint64_t* out,
+                                              const uint8_t* __restrict__ lut) {
+    uint64_t s[16];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        s[q] = l[q];
+        s[5 + q] = r[q];
+    }
+#pragma unroll
+    for (int q = 10; q < 16; ++q) s[q] = MONT_ONE;
+    tip5_permute_raw(s, lut);
+#pragma unroll
+    for (int q = 0; q < 5; ++q) out[q] = s[q];
+}
+
+// ------------------------------------------------------------------ Merkle multi-proofs
+// twenty-first MerkleTreeInclusionProof::verify: leaves at (index, digest), the authentication
+// structure lists the missing siblings in descending node-index order.  One workgroup (256 lanes)
+// per (proof, tree); tree 0 main, 1 aux, 2 quotient, 3 FRI round-0 a-values, 4 + r FRI round-r
+// b-values.  Nodes of a level are kept sorted by descending node index in LDS, so the siblings
+// that must come from the authentication structure appear exactly in its order.
+struct MpLds {
+    uint32_t key[2][MAX_CHECKS];
+    uint64_t dg[2][MAX_CHECKS][5];
+    uint32_t scan[256];
+    uint32_t flag;
+    Tip5Lds t5;
+};
+
+__global__ void __launch_bounds__(256) k_multiproof(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+                                                    uint32_t n_proofs, uint32_t k, const uint64_t* __restrict__ dig,
+                                                    const uint32_t* __restrict__ idx_all, uint32_t* __restrict__ fail) {
+    __shared__ MpLds L;
+    const uint32_t p = blockIdx.x, tree = blockIdx.y, tid = threadIdx.x;
+    if (p >= n_proofs) return;
+    tip5_lds_init(L.t5);
+    const ProofDesc& d = desc[p];
+    if (fail[p] & FAIL_DECODE) return;
+    if (tree >= 4 + d.R) return;
+    uint32_t h;
+    uint64_t root_off, auth_off;
+    uint32_t auth_n, fail_bit;
+    if (tree < 3) {
+        h = d.log2_N;
+        root_off = tree == 0 ? d.main_root : (tree == 1 ? d.aux_root : d.quot_root);
+        auth_off = tree == 0 ? d.main_auth_off : (tree == 1 ? d.aux_auth_off : d.quot_auth_off);
+        auth_n = tree == 0 ? d.main_auth_n : (tree == 1 ? d.aux_auth_n : d.quot_auth_n);
+        fail_bit = tree == 0 ? FAIL_MERKLE_MAIN : (tree == 1 ? FAIL_MERKLE_AUX : FAIL_MERKLE_QUOT);
+    } else {
+        const uint32_t r = tree == 3 ? 0u : tree - 4;
+        h = d.log2_N - r;
+        root_off = d.fri_root[r];
+        const FriResp& fr = d.fri[tree == 3 ? 0 : 1 + r];
+        auth_off = fr.auth_off;
+        auth_n = fr.auth_n;
+        fail_bit = FAIL_MERKLE_FRI;
+    }
+    const uint32_t* __restrict__ idx = idx_all + d.idx_off;
+    // ---- load leaves
+    uint32_t key = 0u;
+    uint64_t lv[5] = {0, 0, 0, 0, 0};
+    if (tid < k) {
+        const uint64_t nl = 1ull << h;
+        uint64_t li = idx[tid];
+        if (tree == 3) li = li % nl;
+        if (tree >= 4) li = (li + nl / 2) % nl;
+        key = (uint32_t)(li + nl);
+        if (tree < 3) {
+            const uint64_t* s = dig + (((uint64_t)p * 3 + tree) * k + tid) * 5;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) lv[q] = s[q];
+        } else {
+            const uint64_t off = (tree == 3 ? d.fri[0].leaves_off : d.fri[tree - 3].leaves_off) + 3ull * tid;
+            lv[0] = to_mont(words[off]);
+            lv[1] = to_mont(words[off + 1]);
+            lv[2] = to_mont(words[off + 2]);
+        }
+    }
+    L.key[0][tid] = key;
+    if (tid == 0) L.flag = 0;
+    // ---- bitonic sort (descending) of (key, original lane) over 256 slots
+    __shared__ uint32_t order[256];
+    order[tid] = tid;
+    __syncthreads();
+    for (uint32_t size = 2; size <= 256; size <<= 1) {
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            const uint32_t partner = tid ^ stride;
+            if (partner > tid) {
+                const bool desc_dir = (tid & size) == 0;
+                const uint32_t a = L.key[0][tid], b = L.key[0][partner];
+                if ((a < b) == desc_dir) {
+                    L.key[0][tid] = b;
+                    L.key[0][partner] = a;
+                    const uint32_t t = order[tid];
+                    order[tid] = order[partner];
+                    order[partner] = t;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // scatter digests into sorted order (via LDS staging of the unsorted digests)
+    {
+        // stage unsorted leaf digests in dg[1]
+#pragma unroll
+        for (int q = 0; q < 5; ++q) L.dg[1][tid][q] = lv[q];
+    }
+    __syncthreads();
+    const uint32_t skey = L.key[0][tid];
+    uint64_t sd[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) sd[q] = L.dg[1][order[tid]][q];
+    // dedupe: equal keys must carry equal digests
+    bool dup = false;
+    if (skey != 0 && tid > 0 && L.key[0][tid - 1] == skey) {
+        dup = true;
+        bool same = true;
+        const uint32_t o2 = order[tid - 1];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) same &= (L.dg[1][o2][q] == sd[q]);
+        if (!same) atomicOr(&L.flag, 1u);
+    }
+    const uint32_t keep = (skey != 0 && !dup) ? 1u : 0u;
+    uint32_t pos;
+    uint32_t m = block_exclusive_scan(keep, L.scan, pos);
+    __syncthreads();
+    if (keep) {
+        L.key[0][pos] = skey;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) L.dg[0][pos][q] = sd[q];
+    }
+    __syncthreads();
+    // ---- climb
+    const uint64_t* __restrict__ auth = words + auth_off;
+    uint32_t ap = 0;
+    int cur = 0;
+    for (uint32_t lvl = 0; lvl < h; ++lvl) {
+        const uint32_t i = tid;
+        uint32_t ki = 0, unpaired = 0, owner = 0;
+        bool pair_next = false;
+        if (i < m) {
+            ki = L.key[cur][i];
+            const bool pair_prev = i > 0 && L.key[cur][i - 1] == (ki ^ 1u);
+            pair_next = i + 1 < m && L.key[cur][i + 1] == (ki ^ 1u);
+            unpaired = (!pair_prev && !pair_next) ? 1u : 0u;
+            owner = pair_prev ? 0u : 1u;
+        }
+        uint32_t upos, opos;
+        const uint32_t n_unp = block_exclusive_scan(unpaired, L.scan, upos);
+        const uint32_t n_own = block_exclusive_scan(owner, L.scan, opos);
+        if (ap + n_unp > auth_n) {
+            if (tid == 0) L.flag = 1u;
+            __syncthreads();
+            break;
+        }
+        if (owner) {
+            uint64_t left[5], right[5];
+            const uint64_t* mine = L.dg[cur][i];
+            if (pair_next) {  // i holds 2q+1, i+1 holds 2q
+#pragma unroll
+                for (int q = 0; q < 5; ++q) {
+                    right[q] = mine[q];
+                    left[q] = L.dg[cur][i + 1][q];
+                }
+            } else {
+                const uint64_t* a = auth + 5ull * (ap + upos);
+                uint64_t sib[5];
+#pragma unroll
+                for (int q = 0; q < 5; ++q) sib[q] = to_mont(a[q]);
+                const bool odd = (ki & 1u) != 0;
+#pragma unroll
+                for (int q = 0; q < 5; ++q) {
+                    left[q] = odd ? sib[q] : mine[q];
+                    right[q] = odd ? mine[q] : sib[q];
+                }
+            }
+            uint64_t par[5];
+            hash_pair_raw(left, right, par, L.t5.lut);
+            L.key[cur ^ 1][opos] = ki >> 1;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) L.dg[cur ^ 1][opos][q] = par[q];
+        }
+        ap += n_unp;
+        m = n_own;
+        cur ^= 1;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        bool ok = L.flag == 0 && m == 1 && L.key[cur][0] == 1u && ap == auth_n;
+        if (ok) {
+            const uint64_t* rt = words + root_off;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) ok &= (L.dg[cur][0][q] == to_mont(rt[q]));
+        }
+        if (!ok) atomicOr(&fail[p], fail_bit);
+    }
+}
+
+// ------------------------------------------------------------------ XFE block reduction
+__device__ Xfe block_sum_xfe(Xfe v, Xfe* sh) {
+    const uint32_t tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (uint32_t s = blockDim.x >> 1; s > 0; s >>= 1) {
+        if (tid < s) sh[tid] = x_add(sh[tid], sh[tid + s]);
+        __syncthreads();
+    }
+    const Xfe r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+// ------------------------------------------------------------------ OOD: AIR + quotient identity
+// One workgroup per proof.  Circuit nodes are evaluated level by level into LDS (node values are
+// XFE), then sum_i w_i * C_i * Z_type(i)^-1 is compared with sum_k z^k * segment_k(z^4).  Also
+// stores the OOD linear combinations used by DEEP: [sum w*curr row, sum w*next row, sum w*segs].
+__global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+                                                 uint32_t n_proofs, StarkDims dims, const AirNode* __restrict__ nodes,
+                                                 const uint32_t* __restrict__ level_nodes,
+                                                 const uint32_t* __restrict__ level_off, uint32_t n_levels,
+                                                 const uint32_t* __restrict__ cons_nodes, uint4 cons_type_off,
+                                                 const uint64_t* __restrict__ xs, uint64_t* __restrict__ ood_out,
+                                                 uint32_t* __restrict__ fail) {
+    // all LDS in the dynamic region (16-B aligned carve, no static __shared__ in front of it)
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    Xfe* red = reinterpret_cast<Xfe*>(smem);              // 256
+    Xfe* zinv = red + 256;                                 // 4
+    Xfe* chal_derived = zinv + 4;                          // 4 (3 used)
+    uint32_t& zero_flag = *reinterpret_cast<uint32_t*>(chal_derived + 4);
+    Xfe* val = reinterpret_cast<Xfe*>(smem + AIR_LDS_HEADER);
+    const uint32_t p = blockIdx.x, tid = threadIdx.x;
+    if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
+    const ProofDesc& d = desc[p];
+    const SampleLayout sl = SampleLayout::of(dims, d.R);
+    const uint64_t xb = d.xs_off * 3;
+    const Xfe z = ld_xfe_raw(xs, xb + 3ull * sl.z);
+    if (tid == 0) {
+        zero_flag = 0;
+        // zerofier inverses (triton-vm verify: initial, consistency, transition, terminal)
+        const uint64_t w = root_of_unity(d.log2_ph);
+        const uint64_t w_inv = b_inv(w);
+        const Xfe one = x_one();
+        const Xfe zm1 = x_sub(z, one);
+        Xfe zph = z;
+        for (uint32_t q = 0; q < d.log2_ph; ++q) zph = x_mul(zph, zph);
+        const Xfe cons = x_sub(zph, one);
+        const Xfe except_last = x_sub(z, x_lift(w_inv));
+        if (x_is_zero(zm1) || x_is_zero(cons) || x_is_zero(except_last)) zero_flag = 1;
+        zinv[0] = x_inv(zm1);
+        zinv[1] = x_inv(cons);
+        zinv[2] = x_mul(except_last, zinv[1]);
+        zinv[3] = x_inv(except_last);
+    } else if (tid == 64) {
+        // derived challenges: compressed program digest, input / output evaluation arguments
+        const Xfe c0 = ld_xfe_raw(xs, xb + 3ull * (sl.chal + 0));
+        const Xfe c1 = ld_xfe_raw(xs, xb + 3ull * (sl.chal + 1));
+        const Xfe c2 = ld_xfe_raw(xs, xb + 3ull * (sl.chal + 2));
+        Xfe comp = x_zero();
+        for (int q = 0; q < 5; ++q) comp = x_add(x_mul(comp, c0), x_lift(to_mont(words[d.claim_digest_off + q])));
+        Xfe ein = x_one();
+        for (uint32_t q = 0; q < d.claim_in_n; ++q) ein = x_add(x_mul(ein, c1), x_lift(to_mont(words[d.claim_in_off + q])));
+        Xfe eout = x_one();
+        for (uint32_t q = 0; q < d.claim_out_n; ++q)
+            eout = x_add(x_mul(eout, c2), x_lift(to_mont(words[d.claim_out_off + q])));
+        chal_derived[0] = comp;
+        chal_derived[1] = ein;
+        chal_derived[2] = eout;
+    }
+    __syncthreads();
+    // circuit, level by level
+    for (uint32_t lvl = 0; lvl < n_levels; ++lvl) {
+        for (uint32_t q = level_off[lvl] + tid; q < level_off[lvl + 1]; q += blockDim.x) {
+            const uint32_t id = level_nodes[q];
+            const AirNode nd = nodes[id];
+            Xfe v;
+            if (nd.op == AIR_INPUT) {
+                switch (nd.a) {
+                    case IN_MAIN_CURR: v = ld_xfe_canon(words, d.ood_mc + 3ull * nd.b); break;
+                    case IN_AUX_CURR: v = ld_xfe_canon(words, d.ood_ac + 3ull * nd.b); break;
+                    case IN_MAIN_NEXT: v = ld_xfe_canon(words, d.ood_mn + 3ull * nd.b); break;
+                    case IN_AUX_NEXT: v = ld_xfe_canon(words, d.ood_an + 3ull * nd.b); break;
+                    default:
+                        v = nd.b < dims.num_sampled ? ld_xfe_raw(xs, xb + 3ull * (sl.chal + nd.b))
+                                                    : chal_derived[nd.b - dims.num_sampled];
+                }
+            } else if (nd.op == AIR_CONST) {
+                v = {nd.k0, nd.k1, nd.k2};
+            } else if (nd.op == AIR_ADD) {
+                v = x_add(val[nd.a], val[nd.b]);
+            } else if (nd.op == AIR_SUB) {
+                v = x_sub(val[nd.a], val[nd.b]);
+            } else {
+                v = x_mul(val[nd.a], val[nd.b]);
+            }
+            val[id] = v;
+        }
+        __syncthreads();
+    }
+    // weighted quotient sum
+    Xfe acc = x_zero();
+    const uint32_t offs[5] = {0u, cons_type_off.x, cons_type_off.y, cons_type_off.z, cons_type_off.w};
+    for (uint32_t c = tid; c < dims.num_constraints; c += blockDim.x) {
+        uint32_t t = 0;
+        while (t < 3 && c >= offs[t + 1]) ++t;
+        const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.quot_w + c));
+        acc = x_add(acc, x_mul(w, x_mul(val[cons_nodes[c]], zinv[t])));
+    }
+    const Xfe ood_q = block_sum_xfe(acc, red);
+    // OOD linear combinations (DEEP needs them): lin weights = [main | aux | quot segs | deep]
+    const uint32_t M = dims.num_main, A = dims.num_aux, Q = dims.num_quot_seg;
+    Xfe lc = x_zero(), ln = x_zero();
+    for (uint32_t c = tid; c < M + A; c += blockDim.x) {
+        const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + c));
+        const Xfe vc = c < M ? ld_xfe_canon(words, d.ood_mc + 3ull * c) : ld_xfe_canon(words, d.ood_ac + 3ull * (c - M));
+        const Xfe vn = c < M ? ld_xfe_canon(words, d.ood_mn + 3ull * c) : ld_xfe_canon(words, d.ood_an + 3ull * (c - M));
+        lc = x_add(lc, x_mul(w, vc));
+        ln = x_add(ln, x_mul(w, vn));
+    }
+    const Xfe sum_c = block_sum_xfe(lc, red);
+    const Xfe sum_n = block_sum_xfe(ln, red);
+    if (tid == 0) {
+        Xfe seg = x_zero(), zk = x_one(), qlin = x_zero();
+        for (uint32_t q = 0; q < Q; ++q) {
+            const Xfe sq = ld_xfe_canon(words, d.ood_qs + 3ull * q);
+            seg = x_add(seg, x_mul(zk, sq));
+            zk = x_mul(zk, z);
+            qlin = x_add(qlin, x_mul(ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + q)), sq));
+        }
+        uint32_t f = 0;
+        if (zero_flag) f |= FAIL_ZERO_INVERSE;
+        if (!x_eq(seg, ood_q)) f |= FAIL_OOD;
+        if (f) atomicOr(&fail[p], f);
+        uint64_t* o = ood_out + (uint64_t)p * 9;
+        st_xfe_raw(o, 0, sum_c);
+        st_xfe_raw(o, 3, sum_n);
+        st_xfe_raw(o, 6, qlin);
+    }
+}
+
+// ------------------------------------------------------------------ FRI
+// One workgroup per proof.  Lane j follows collinearity check j through all rounds:
+// a_{r+1} = line through (x_a, a_r), (x_b, b_r) evaluated at alpha_r.  Then the last codeword:
+// Merkle root (tree of XFE digests built in LDS), agreement at the a-indices, and
+// Horner(last polynomial, t) == barycentric(last codeword, t).
+__global__ void __launch_bounds__(256) k_fri(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+                                             uint32_t n_proofs, StarkDims dims, const uint64_t* __restrict__ xs,
+                                             const uint32_t* __restrict__ idx_all, uint32_t* __restrict__ fail) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    Xfe* red = reinterpret_cast<Xfe*>(smem);                                   // 256
+    Tip5Lds& t5 = *reinterpret_cast<Tip5Lds*>(smem + 256 * sizeof(Xfe));      // 256 B
+    uint32_t& lflag = *reinterpret_cast<uint32_t*>(smem + 256 * sizeof(Xfe) + 256);
+    uint64_t(*tree)[5] = reinterpret_cast<uint64_t(*)[5]>(smem + FRI_LDS_HEADER);  // last_cw_n digests
+    const uint32_t p = blockIdx.x, tid = threadIdx.x;
+    if (p >= n_proofs) return;
+    tip5_lds_init(t5);
+    if (fail[p] & FAIL_DECODE) return;
+    const ProofDesc& d = desc[p];
+    const SampleLayout sl = SampleLayout::of(dims, d.R);
+    const uint64_t xb = d.xs_off * 3;
+    const uint32_t k = dims.num_checks;
+    const uint32_t* __restrict__ idx = idx_all + d.idx_off;
+    if (tid == 0) lflag = 0;
+    __syncthreads();
+    uint32_t f = 0;
+    if (tid < k) {
+        const uint64_t i0 = idx[tid];
+        Xfe a = ld_xfe_canon(words, d.fri[0].leaves_off + 3ull * tid);
+        const uint64_t g0 = root_of_unity(d.log2_N);
+        uint64_t offset = to_mont(7), gen = g0;
+        for (uint32_t r = 0; r < d.R; ++r) {
+            const uint64_t n = 1ull << (d.log2_N - r);
+            const uint64_t ai = i0 % n, bi = (i0 + n / 2) % n;
+            const Xfe b = ld_xfe_canon(words, d.fri[1 + r].leaves_off + 3ull * tid);
+            const uint64_t ax = mont_mul(offset, b_pow(gen, ai));
+            const uint64_t bx = mont_mul(offset, b_pow(gen, bi));
+            const Xfe alpha = ld_xfe_raw(xs, xb + 3ull * (sl.alpha + r));
+            const uint64_t inv = b_inv(gl_sub(bx, ax));
+            const Xfe slope = x_scale(x_sub(b, a), inv);
+            a = x_add(a, x_mul(slope, x_sub(alpha, x_lift(ax))));
+            offset = mont_mul(offset, offset);
+            gen = mont_mul(gen, gen);
+        }
+        const uint64_t nl = 1ull << (d.log2_N - d.R);
+        const Xfe last = ld_xfe_canon(words, d.last_cw_off + 3ull * (i0 % nl));
+        if (!x_eq(last, a)) f |= FAIL_FRI_LAST_AGREE;
+    }
+    // last codeword Merkle root
+    const uint32_t L = d.last_cw_n;
+    const uint32_t log2L = 31 - __clz(L);
+    for (uint32_t i = tid; i < L; i += blockDim.x) {
+        const uint64_t off = d.last_cw_off + 3ull * i;
+        tree[i][0] = to_mont(words[off]);
+        tree[i][1] = to_mont(words[off + 1]);
+        tree[i][2] = to_mont(words[off + 2]);
+        tree[i][3] = 0;
+        tree[i][4] = 0;
+    }
+    __syncthreads();
+    for (uint32_t lv = 0; lv < log2L; ++lv) {
+        const uint32_t np = L >> (lv + 1);
+        uint64_t par[5];
+        const bool act = tid < np;
+        // parents of this level are written in place at [0, np) after all lanes read their children
+        for (uint32_t base = 0; base < np; base += blockDim.x) {
+            const uint32_t i = base + tid;
+            const bool a2 = i < np;
+            if (a2) hash_pair_raw(tree[2 * i], tree[2 * i + 1], par, t5.lut);
+            __syncthreads();
+            if (a2) {
+#pragma unroll
+                for (int q = 0; q < 5; ++q) tree[i][q] = par[q];
+            }
+            __syncthreads();
+        }
+        (void)act;
+    }
+    if (tid == 0) {
+        bool ok = true;
+        const uint64_t* rt = words + d.fri_root[d.R];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) ok &= (tree[0][q] == to_mont(rt[q]));
+        if (!ok) f |= FAIL_FRI_LAST_ROOT;
+    }
+    // barycentric evaluation of the last codeword at the indeterminate vs Horner of the polynomial
+    const Xfe t = ld_xfe_raw(xs, xb + 3ull * sl.indeterminate);
+    const uint64_t wL = root_of_unity(log2L);
+    Xfe num = x_zero(), den = x_zero();
+    for (uint32_t i = tid; i < L; i += blockDim.x) {
+        const uint64_t wi = b_pow(wL, i);
+        const Xfe diff = x_sub(t, x_lift(wi));
+        if (x_is_zero(diff)) atomicOr(&lflag, 1u);
+        const Xfe q = x_scale(x_inv(diff), wi);
+        num = x_add(num, x_mul(q, ld_xfe_canon(words, d.last_cw_off + 3ull * i)));
+        den = x_add(den, q);
+    }
+    const Xfe snum = block_sum_xfe(num, red);
+    const Xfe sden = block_sum_xfe(den, red);
+    if (tid == 0) {
+        Xfe h = x_zero();
+        for (uint32_t c = d.last_poly_n; c-- > 0;) h = x_add(x_mul(h, t), ld_xfe_canon(words, d.last_poly_off + 3ull * c));
+        if (lflag || x_is_zero(sden)) f |= FAIL_ZERO_INVERSE;
+        else if (!x_eq(h, x_mul(snum, x_inv(sden)))) f |= FAIL_FRI_EVAL;
+        if (!d.last_poly_degree_ok) f |= FAIL_FRI_DEGREE;
+    }
+    if (f) atomicOr(&fail[p], f);
+}
+
+// ------------------------------------------------------------------ DEEP
+// One workgroup per proof; wave w handles revealed rows j = w, w + 4, ...; lanes split the row.
+__global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+                                              uint32_t n_proofs, StarkDims dims, const uint64_t* __restrict__ xs,
+                                              const uint32_t* __restrict__ idx_all, const uint64_t* __restrict__ ood,
+                                              uint32_t* __restrict__ fail) {
+    const uint32_t p = blockIdx.x, tid = threadIdx.x;
+    if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
+    const ProofDesc& d = desc[p];
+    const SampleLayout sl = SampleLayout::of(dims, d.R);
+    const uint64_t xb = d.xs_off * 3;
+    const uint32_t M = dims.num_main, A = dims.num_aux, Q = dims.num_quot_seg, k = dims.num_checks;
+    const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
+    const Xfe z = ld_xfe_raw(xs, xb + 3ull * sl.z);
+    const uint64_t w_tr = root_of_unity(d.log2_ph);
+    const Xfe z_next = x_scale(z, w_tr);
+    Xfe z4 = x_one();
+    for (uint32_t q = 0; q < Q; ++q) z4 = x_mul(z4, z);
+    const Xfe o_curr = ld_xfe_raw(ood, (uint64_t)p * 9 + 0);
+    const Xfe o_next = ld_xfe_raw(ood, (uint64_t)p * 9 + 3);
+    const Xfe o_q = ld_xfe_raw(ood, (uint64_t)p * 9 + 6);
+    const uint64_t gN = root_of_unity(d.log2_N);
+    const uint32_t* __restrict__ idx = idx_all + d.idx_off;
+    uint32_t f = 0;
+    for (uint32_t j = wave; j < k; j += nwaves) {
+        Xfe acc = x_zero();
+        for (uint32_t c = lane; c < M + A; c += 64) {
+            const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + c));
+            if (c < M) {
+                acc = x_add(acc, x_scale(w, to_mont(words[d.main_rows_off + (uint64_t)j * M + c])));
+            } else {
+                acc = x_add(acc, x_mul(w, ld_xfe_canon(words, d.aux_rows_off + (uint64_t)j * 3 * A + 3ull * (c - M))));
+            }
+        }
+        Xfe qv = x_zero();
+        if (lane < Q) {
+            const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + lane));
+            qv = x_mul(w, ld_xfe_canon(words, d.quot_rows_off + (uint64_t)j * 3 * Q + 3ull * lane));
+        }
+        for (int s = 32; s > 0; s >>= 1) {
+            acc.c0 = gl_add(acc.c0, __shfl_xor(acc.c0, s));
+            acc.c1 = gl_add(acc.c1, __shfl_xor(acc.c1, s));
+            acc.c2 = gl_add(acc.c2, __shfl_xor(acc.c2, s));
+            qv.c0 = gl_add(qv.c0, __shfl_xor(qv.c0, s));
+            qv.c1 = gl_add(qv.c1, __shfl_xor(qv.c1, s));
+            qv.c2 = gl_add(qv.c2, __shfl_xor(qv.c2, s));
+        }
+        if (lane == 0) {
+            const uint64_t x = mont_mul(to_mont(7), b_pow(gN, idx[j]));
+            const Xfe d0 = x_sub(x_lift(x), z), d1 = x_sub(x_lift(x), z_next), d2 = x_sub(x_lift(x), z4);
+            if (x_is_zero(d0) || x_is_zero(d1) || x_is_zero(d2)) {
+                f |= FAIL_ZERO_INVERSE;
+            } else {
+                const Xfe t0 = x_mul(x_sub(acc, o_curr), x_inv(d0));
+                const Xfe t1 = x_mul(x_sub(acc, o_next), x_inv(d1));
+                const Xfe t2 = x_mul(x_sub(qv, o_q), x_inv(d2));
+                const Xfe wd0 = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + Q + 0));
+                const Xfe wd1 = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + Q + 1));
+                const Xfe wd2 = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + Q + 2));
+                const Xfe deep = x_add(x_add(x_mul(t0, wd0), x_mul(t1, wd1)), x_mul(t2, wd2));
+                const Xfe fri_v = ld_xfe_canon(words, d.fri[0].leaves_off + 3ull * j);
+                if (!x_eq(deep, fri_v)) f |= FAIL_DEEP;
+            }
+        }
+    }
+    if (f) atomicOr(&fail[p], f);
+}
+
+__global__ void k_verdicts(const uint32_t* __restrict__ fail, uint32_t n, uint8_t* __restrict__ v) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = fail[i] == 0 ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ launchers
+hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, StarkPhaseTimer* tm) {
+    const uint32_t n = b.n_proofs;
+    if (n == 0) return hipSuccess;
+    const uint32_t k = b.dims.num_checks;
+    auto mark = [&](int i) {
+        if (tm && tm->ev[i]) (void)hipEventRecord(tm->ev[i], st);
+    };
+    mark(0);
+    hipLaunchKernelGGL(k_fs_replay, dim3((n + 63) / 64), dim3(64), 0, st, b.words, b.desc, b.ops, n, b.xs, b.idx,
+                       b.fail);
+    mark(1);
+    {
+        uint64_t rows = (uint64_t)n * k;
+        unsigned gx = (unsigned)((rows + 255) / 256);
+        if (gx > 16384) gx = 16384;
+        hipLaunchKernelGGL(k_hash_rows, dim3(gx, 3), dim3(256), 0, st, b.words, b.desc, n, k, b.dims, b.dig, b.fail);
+    }
+    mark(2);
+    hipLaunchKernelGGL(k_multiproof, dim3(n, 4 + b.max_R), dim3(256), 0, st, b.words, b.desc, n, k, b.dig, b.idx,
+                       b.fail);
+    mark(3);
+    hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(256), b.air_lds_bytes, st, b.words, b.desc, n, b.dims, b.air_nodes,
+                       b.air_level_nodes, b.air_level_off, b.air_n_levels, b.air_cons, b.air_cons_off, b.xs, b.ood,
+                       b.fail);
+    mark(4);
+    hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), b.fri_lds_bytes, st, b.words, b.desc, n, b.dims, b.xs, b.idx,
+                       b.fail);
+    mark(5);
+    hipLaunchKernelGGL(k_deep, dim3(n), dim3(256), 0, st, b.words, b.desc, n, b.dims, b.xs, b.idx, b.ood, b.fail);
+    mark(6);
+    hipLaunchKernelGGL(k_verdicts, dim3((n + 255) / 256), dim3(256), 0, st, b.fail, n, b.verdicts);
+    mark(7);
+    return hipGetLastError();
+}
+
+hipError_t stark_set_kernel_attributes() {
+    hipError_t e = hipFuncSetAttribute((const void*)k_ood_air, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)k_fri, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 16384);
+}
+
+}  // namespace nhip

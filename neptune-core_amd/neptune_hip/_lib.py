@@ -23,6 +23,36 @@ _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
 _vp = ctypes.c_void_p
 _sz = ctypes.c_size_t
 
+class StarkParams(ctypes.Structure):
+    _fields_ = [("security_level", ctypes.c_uint32), ("log2_fri_expansion", ctypes.c_uint32),
+                ("num_collinearity_checks", ctypes.c_uint32), ("num_main", ctypes.c_uint32),
+                ("num_aux", ctypes.c_uint32), ("num_quotient_segments", ctypes.c_uint32)]
+
+
+class Claim(ctypes.Structure):
+    _fields_ = [("program_digest", ctypes.c_uint64 * 5), ("version", ctypes.c_uint32),
+                ("input", ctypes.POINTER(ctypes.c_uint64)), ("input_len", ctypes.c_size_t),
+                ("output", ctypes.POINTER(ctypes.c_uint64)), ("output_len", ctypes.c_size_t)]
+
+
+class Proof(ctypes.Structure):
+    _fields_ = [("words", ctypes.POINTER(ctypes.c_uint64)), ("len", ctypes.c_size_t)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("num_proofs", ctypes.c_uint64), ("proof_words", ctypes.c_uint64),
+                ("tip5_perms_static", ctypes.c_uint64), ("ms_decode", ctypes.c_double),
+                ("ms_upload", ctypes.c_double), ("ms_fiat_shamir", ctypes.c_double),
+                ("ms_row_hash", ctypes.c_double), ("ms_merkle", ctypes.c_double),
+                ("ms_ood_air", ctypes.c_double), ("ms_fri", ctypes.c_double), ("ms_deep", ctypes.c_double),
+                ("ms_device_total", ctypes.c_double)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+_pp = ctypes.POINTER(ctypes.c_void_p)
+
 # (name, argtypes) for every symbol of include/neptune_hip.h
 SIGNATURES = {
     "nhip_init": ([ctypes.c_uint32, ctypes.POINTER(_vp)], ctypes.c_int),
@@ -46,6 +76,22 @@ SIGNATURES = {
     "nhip_mtree_build_dev": ([_vp, _vp, _sz, _vp], ctypes.c_int),
     "nhip_mtree_verify_dev": ([_vp, _vp, _sz, _vp, _vp, _vp, ctypes.c_uint32, _sz, _vp], ctypes.c_int),
     "nhip_verdicts_all_dev": ([_vp, _vp, _sz, ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
+    "nhip_stark_params_default": ([ctypes.POINTER(StarkParams)], None),
+    "nhip_air_create": ([_u64p, _sz, _pp], ctypes.c_int),
+    "nhip_air_destroy": ([_vp], None),
+    "nhip_air_info": ([_vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                       ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+    "nhip_proof_decodes": ([_vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof)],
+                           ctypes.c_int),
+    "nhip_verify_batch": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof),
+                           _sz, _u8p, ctypes.POINTER(Stats)], ctypes.c_int),
+    "nhip_batch_prepare": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof),
+                            _sz, _pp], ctypes.c_int),
+    "nhip_batch_run": ([_vp, _vp, _u8p, ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
+    "nhip_batch_stats": ([_vp, ctypes.POINTER(Stats)], ctypes.c_int),
+    "nhip_batch_transcript": ([_vp, _vp, _sz, _u64p, _sz, ctypes.POINTER(ctypes.c_uint32), _sz,
+                               ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "nhip_batch_destroy": ([_vp], None),
     "nhip_timing_enable": ([_vp, ctypes.c_int], ctypes.c_int),
     "nhip_timing_read": ([_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int],
                          ctypes.c_int),

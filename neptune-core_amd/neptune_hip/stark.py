@@ -1,0 +1,170 @@
+"""Host mirror of `triton_vm::verify(stark, claim, proof) -> bool` and its batched form over the
+C ABI (nhip_verify_batch / nhip_batch_*).
+
+Reference call site: neptune-core/src/protocol/proof_abstractions/verifier.rs:60-63
+(`task::spawn_blocking(move || triton_vm::verify(Stark::default(), &claim, &proof))`); batch
+callers that verify sequentially today: proof_collection.rs:342-388, block_program.rs:51-65,
+state/mod.rs:2226-2272.  `Stark` mirrors `Stark::default()` plus the table dimensions, `Claim` the
+triton-vm Claim fields, a proof is the flat `Proof(Vec<BFieldElement>)` word vector.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+
+@dataclass
+class Stark:
+    security_level: int = 160
+    log2_fri_expansion: int = 2
+    num_collinearity_checks: int = 80
+    num_main: int = 379
+    num_aux: int = 88
+    num_quotient_segments: int = 4
+
+    def c(self) -> _lib.StarkParams:
+        return _lib.StarkParams(self.security_level, self.log2_fri_expansion, self.num_collinearity_checks,
+                                self.num_main, self.num_aux, self.num_quotient_segments)
+
+    @classmethod
+    def default(cls) -> "Stark":
+        lib = _lib.load()
+        p = _lib.StarkParams()
+        lib.nhip_stark_params_default(ctypes.byref(p))
+        return cls(p.security_level, p.log2_fri_expansion, p.num_collinearity_checks, p.num_main, p.num_aux,
+                   p.num_quotient_segments)
+
+
+@dataclass
+class Claim:
+    program_digest: Sequence[int]
+    version: int = 0
+    input: Sequence[int] = field(default_factory=list)
+    output: Sequence[int] = field(default_factory=list)
+
+
+class Air:
+    """AIR circuit descriptor (format: DESIGN.md §9)."""
+
+    def __init__(self, words: Sequence[int]):
+        self.lib = _lib.load()
+        w = np.ascontiguousarray(np.asarray(words, dtype=np.uint64))
+        h = ctypes.c_void_p()
+        check(self.lib.nhip_air_create(w, w.size, ctypes.byref(h)), "nhip_air_create")
+        self.handle = h.value
+
+    def info(self):
+        a, b, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        check(self.lib.nhip_air_info(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "air_info")
+        return {"nodes": a.value, "levels": b.value, "constraints": c.value}
+
+    def __del__(self):
+        try:
+            if self.handle:
+                self.lib.nhip_air_destroy(self.handle)
+        except Exception:
+            pass
+
+
+class _Marshal:
+    """Keeps the numpy buffers alive while the C structs point into them."""
+
+    def __init__(self, claims: Sequence[Claim], proofs: Sequence[Sequence[int]]):
+        n = len(claims)
+        self.keep = []
+        self.claims = (_lib.Claim * max(n, 1))()
+        self.proofs = (_lib.Proof * max(n, 1))()
+        u64 = ctypes.POINTER(ctypes.c_uint64)
+        for i, (c, pw) in enumerate(zip(claims, proofs)):
+            inp = np.ascontiguousarray(np.asarray(list(c.input), dtype=np.uint64))
+            out = np.ascontiguousarray(np.asarray(list(c.output), dtype=np.uint64))
+            pa = np.ascontiguousarray(np.asarray(pw, dtype=np.uint64))
+            self.keep += [inp, out, pa]
+            cc = self.claims[i]
+            for k in range(5):
+                cc.program_digest[k] = int(c.program_digest[k])
+            cc.version = int(c.version)
+            cc.input = inp.ctypes.data_as(u64) if inp.size else None
+            cc.input_len = inp.size
+            cc.output = out.ctypes.data_as(u64) if out.size else None
+            cc.output_len = out.size
+            self.proofs[i].words = pa.ctypes.data_as(u64) if pa.size else None
+            self.proofs[i].len = pa.size
+        self.n = n
+
+
+class Batch:
+    """Device-resident batch: decode + upload once, run the device phases any number of times."""
+
+    def __init__(self, ctx, air: Air, stark: Stark, claims: Sequence[Claim], proofs: Sequence[Sequence[int]]):
+        self.ctx, self.air, self.stark = ctx, air, stark
+        m = _Marshal(claims, proofs)
+        self.n = m.n
+        h = ctypes.c_void_p()
+        params = stark.c()
+        check(ctx.lib.nhip_batch_prepare(ctx.handle, air.handle, ctypes.byref(params), m.claims, m.proofs, m.n,
+                                         ctypes.byref(h)), "nhip_batch_prepare")
+        self.handle = h.value
+
+    def run(self) -> Tuple[np.ndarray, bool]:
+        v = np.zeros(max(self.n, 1), dtype=np.uint8)
+        ok = ctypes.c_uint8(0)
+        check(self.ctx.lib.nhip_batch_run(self.ctx.handle, self.handle, v, ctypes.byref(ok)), "nhip_batch_run")
+        return v[:self.n], bool(ok.value)
+
+    def stats(self) -> dict:
+        s = _lib.Stats()
+        check(self.ctx.lib.nhip_batch_stats(self.handle, ctypes.byref(s)), "nhip_batch_stats")
+        return s.as_dict()
+
+    def transcript(self, i: int, max_xfe: int = 1 << 16):
+        xs = np.zeros(3 * max_xfe, dtype=np.uint64)
+        k = self.stark.num_collinearity_checks
+        idx = (ctypes.c_uint32 * k)()
+        fail = ctypes.c_uint32(0)
+        nx = ctypes.c_size_t(0)
+        check(self.ctx.lib.nhip_batch_transcript(self.ctx.handle, self.handle, i, xs, max_xfe, idx, k,
+                                                 ctypes.byref(fail), ctypes.byref(nx)), "nhip_batch_transcript")
+        n = min(nx.value, max_xfe)
+        return [tuple(int(v) for v in xs[3 * j:3 * j + 3]) for j in range(n)], list(idx), fail.value
+
+    def __del__(self):
+        try:
+            if self.handle:
+                self.ctx.lib.nhip_batch_destroy(self.handle)
+        except Exception:
+            pass
+
+
+def verify_batch(ctx, air: Air, stark: Stark, pairs: Sequence[Tuple[Claim, Sequence[int]]]) -> List[bool]:
+    """`verify_batch(&[(Claim, Proof)]) -> Vec<bool>`."""
+    claims = [c for c, _ in pairs]
+    proofs = [p for _, p in pairs]
+    m = _Marshal(claims, proofs)
+    v = np.zeros(max(m.n, 1), dtype=np.uint8)
+    stats = _lib.Stats()
+    params = stark.c()
+    check(ctx.lib.nhip_verify_batch(ctx.handle, air.handle, ctypes.byref(params), m.claims, m.proofs, m.n, v,
+                                    ctypes.byref(stats)), "nhip_verify_batch")
+    return [bool(x) for x in v[:m.n]]
+
+
+def verify(ctx, air: Air, stark: Stark, claim: Claim, proof: Sequence[int]) -> bool:
+    """`triton_vm::verify(stark, &claim, &proof) -> bool`."""
+    return verify_batch(ctx, air, stark, [(claim, proof)])[0]
+
+
+def proof_decodes(air: Air, stark: Stark, claim: Claim, proof: Sequence[int]) -> bool:
+    """Host-only structural decode of the proof stream (no GPU)."""
+    m = _Marshal([claim], [proof])
+    params = stark.c()
+    rc = _lib.load().nhip_proof_decodes(air.handle, ctypes.byref(params), m.claims, m.proofs)
+    if rc < 0:
+        raise _lib.NhipError("nhip_proof_decodes: invalid argument")
+    return rc == 1

@@ -763,3 +763,34 @@ def _verify(params, air, claim, proof_words, transcript):
     if transcript is not None:
         transcript["sponge_samples"] = ps.transcript
         transcript["roots"] = [main_root, aux_root, quot_root]
+
+
+def expected_kinds(R: int) -> List[int]:
+    return ([LOG2_PADDED_HEIGHT, MERKLE_ROOT, MERKLE_ROOT, MERKLE_ROOT, OOD_MAIN_ROW, OOD_AUX_ROW, OOD_MAIN_ROW,
+             OOD_AUX_ROW, OOD_QUOT_SEGMENTS] + [MERKLE_ROOT] * (R + 1) + [FRI_CODEWORD, FRI_POLYNOMIAL] +
+            [FRI_RESPONSE] * (R + 1) + [MAIN_ROWS, AUTH_STRUCTURE, AUX_ROWS, AUTH_STRUCTURE, QUOT_SEGMENTS_ELEMENTS,
+                                        AUTH_STRUCTURE])
+
+
+def structure_ok(params: StarkParams, proof_words: Sequence[int]) -> bool:
+    """Decodes, has the item sequence of Stark::verify and the counts it checks (no arithmetic)."""
+    try:
+        items = decode_proof(proof_words, params)
+    except VerifyError:
+        return False
+    if not items or items[0][0] != LOG2_PADDED_HEIGHT or items[0][1] > 28:
+        return False
+    ph = 1 << items[0][1]
+    N = params.fri_domain(ph).length
+    R = params.fri_num_rounds(N)
+    if [k for k, _ in items] != expected_kinds(R):
+        return False
+    k = params.num_collinearity_checks
+    byk = {}
+    for kind, payload in items:
+        byk.setdefault(kind, []).append(payload)
+    if any(len(leaves) != k for _, leaves in byk[FRI_RESPONSE]):
+        return False
+    if len(byk[MAIN_ROWS][0]) != k or len(byk[AUX_ROWS][0]) != k or len(byk[QUOT_SEGMENTS_ELEMENTS][0]) != k:
+        return False
+    return len(byk[FRI_CODEWORD][0]) == N >> R

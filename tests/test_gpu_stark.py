@@ -1,0 +1,168 @@
+"""GPU parity of the batched STARK verifier (nhip_verify_batch / nhip_batch_*) with the oracle
+(oracle/stark_ref.py): every verdict and every Fiat-Shamir sample (challenges, quotient weights,
+OOD point, linear-combination weights, FRI folding challenges, FRI indices, last indeterminate)
+identical.  Accepting proofs come from the oracle's synthetic prover; rejecting ones from the
+reference's reject cases and from mutations of accepting proofs."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import stark_prover as SP
+import stark_ref as S
+import tip5_ref as T
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "stark_tiny.json")
+
+
+def _ns():
+    import neptune_hip.stark as NS
+    return NS
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    g = json.load(open(GOLD))
+    params = S.StarkParams(**g["params"])
+    air, _ = S.synth_air(params, num_sampled=g["num_sampled"], seed=g["seed"])
+    return g, params, air
+
+
+def _oracle_samples(params, air, claim, proof):
+    tr = {}
+    ok = S.verify(params, air, claim, proof, tr)
+    if not ok:
+        return ok, None, None
+    samples = [tuple(x) for tag, vals in tr["sponge_samples"] if tag != "fri_indices" for x in vals]
+    indices = [v for tag, vals in tr["sponge_samples"] if tag == "fri_indices" for v in vals]
+    return ok, samples, indices
+
+
+def test_tiny_golden_verdicts_and_transcripts(ctx, tiny):
+    NS = _ns()
+    g, params, air = tiny
+    gair = NS.Air([int(w) for w in g["air"]])
+    stark = NS.Stark(num_collinearity_checks=8, num_main=24, num_aux=9)
+    claims, proofs = [], []
+    for c in g["cases"]:
+        cl = c["claim"]
+        claims.append(NS.Claim(cl["digest"], cl["version"], cl["input"], cl["output"]))
+        proofs.append([int(w) for w in c["proof"]])
+    b = NS.Batch(ctx, gair, stark, claims, proofs)
+    v, ok = b.run()
+    assert list(v) == [1, 1, 1] and ok
+    for i, c in enumerate(g["cases"]):
+        xs, idx, fail = b.transcript(i)
+        assert fail == 0
+        assert [[str(x) for x in t] for t in xs] == c["samples"]
+        assert idx == c["fri_indices"]
+
+
+def test_reference_reject_cases_on_gpu(ctx, tiny):
+    NS = _ns()
+    g, params, air = tiny
+    gair = NS.Air([int(w) for w in g["air"]])
+    stark = NS.Stark(num_collinearity_checks=8, num_main=24, num_aux=9)
+    cl = g["cases"][0]["claim"]
+    claim = NS.Claim(cl["digest"], cl["version"], cl["input"], cl["output"])
+    bogus = T.hash_varlen(S.encode_claim(cl["digest"], cl["version"], cl["input"], cl["output"]))
+    good = [int(w) for w in g["cases"][0]["proof"]]
+    pairs = [(claim, p) for p in ([], bogus, [0] * 65, [0], [1], good)]
+    assert NS.verify_batch(ctx, gair, stark, pairs) == [False, False, False, False, False, True]
+    # the claim is bound: other output / input / digest / version -> reject
+    wrong = [NS.Claim(cl["digest"], cl["version"], cl["input"], list(cl["output"]) + [1]),
+             NS.Claim(cl["digest"], cl["version"], [5] + list(cl["input"]), cl["output"]),
+             NS.Claim([1, 1, 1, 1, 1], cl["version"], cl["input"], cl["output"]),
+             NS.Claim(cl["digest"], 1, cl["input"], cl["output"])]
+    assert NS.verify_batch(ctx, gair, stark, [(w, good) for w in wrong]) == [False] * 4
+
+
+def test_tiny_mutations_match_oracle(ctx, tiny):
+    NS = _ns()
+    g, params, air = tiny
+    gair = NS.Air([int(w) for w in g["air"]])
+    stark = NS.Stark(num_collinearity_checks=8, num_main=24, num_aux=9)
+    c = g["cases"][2]
+    cl = c["claim"]
+    claim_t = (cl["digest"], cl["version"], cl["input"], cl["output"])
+    claim = NS.Claim(*claim_t)
+    proof = [int(w) for w in c["proof"]]
+    rng = np.random.default_rng(21)
+    muts = []
+    for pos in sorted(set(rng.integers(0, len(proof), size=70).tolist()) | {0, 1, 2, 3, len(proof) - 1}):
+        m = list(proof)
+        m[pos] = (m[pos] + 1) % S.P
+        muts.append(m)
+    got = NS.verify_batch(ctx, gair, stark, [(claim, m) for m in muts])
+    ref = [S.verify(params, air, claim_t, m) for m in muts]
+    assert got == ref
+    assert not any(ref)  # a single-word change always breaks some check
+
+
+@pytest.fixture(scope="module")
+def full():
+    params = S.StarkParams()
+    air, recipe = S.synth_air(params, seed=1)
+    out = []
+    for lph, claim in [(4, ([11, 22, 33, 44, 55], 0, [1, 2, 3, 4, 5], [])), (6, ([7, 7, 7, 7, 7], 0, [], [9, 8]))]:
+        proof, _ = SP.prove(params, air, recipe, claim, lph, seed=lph)
+        out.append((claim, proof))
+    return params, air, out
+
+
+def test_full_size_params_verdicts_and_transcripts(ctx, full):
+    NS = _ns()
+    params, air, cases = full
+    gair = NS.Air(air.to_words())
+    stark = NS.Stark.default()
+    assert (stark.num_main, stark.num_aux, stark.num_collinearity_checks) == (379, 88, 80)
+    claims = [NS.Claim(*c) for c, _ in cases]
+    b = NS.Batch(ctx, gair, stark, claims, [p for _, p in cases])
+    v, ok = b.run()
+    assert list(v) == [1, 1] and ok
+    for i, (claim, proof) in enumerate(cases):
+        ok_o, samples, indices = _oracle_samples(params, air, claim, proof)
+        assert ok_o
+        xs, idx, fail = b.transcript(i)
+        assert fail == 0 and xs == samples and idx == indices
+    st = b.stats()
+    assert st["num_proofs"] == 2 and st["tip5_perms_static"] > 0
+
+
+def test_full_size_targeted_mutations(ctx, full):
+    """Corrupt one value inside each verifier phase's input; GPU and oracle both reject."""
+    NS = _ns()
+    params, air, cases = full
+    gair = NS.Air(air.to_words())
+    stark = NS.Stark.default()
+    claim, proof = cases[1]
+    items = S.decode_proof(proof, params)
+    # locate item payload starts by re-walking the encoding
+    pos, starts = 2, []
+    for _ in items:
+        ln = proof[pos]
+        starts.append(pos + 1)
+        pos += 1 + ln
+    kinds = [k for k, _ in items]
+    targets = {
+        "ood_main_row": starts[kinds.index(S.OOD_MAIN_ROW)] + 1 + 3 * 17,
+        "ood_quot": starts[kinds.index(S.OOD_QUOT_SEGMENTS)] + 1 + 2,
+        "fri_last_codeword": starts[kinds.index(S.FRI_CODEWORD)] + 3 + 5,
+        "fri_response_leaf": starts[kinds.index(S.FRI_RESPONSE)] + 4 + 7,
+        "main_row_value": starts[kinds.index(S.MAIN_ROWS)] + 3 + 100,
+        "aux_row_value": starts[kinds.index(S.AUX_ROWS)] + 3 + 50,
+        "quot_row_value": starts[kinds.index(S.QUOT_SEGMENTS_ELEMENTS)] + 3 + 4,
+        "main_auth_digest": starts[kinds.index(S.AUTH_STRUCTURE)] + 3 + 2,
+        "fri_root": starts[[i for i, k in enumerate(kinds) if k == S.MERKLE_ROOT][3]] + 1,
+    }
+    muts = []
+    for name, p in targets.items():
+        m = list(proof)
+        m[p] = (m[p] + 12345) % S.P
+        muts.append(m)
+    got = NS.verify_batch(ctx, gair, stark, [(NS.Claim(*claim), m) for m in muts] + [(NS.Claim(*claim), proof)])
+    assert got == [False] * len(muts) + [True], dict(zip(list(targets) + ["clean"], got))
+    for m in muts[:3]:
+        assert S.verify(params, air, claim, m) is False
