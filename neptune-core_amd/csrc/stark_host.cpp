@@ -143,9 +143,14 @@ void decode_proof(HostBatch& B, const nhip_claim& claim, const nhip_proof& proof
     const uint64_t base = B.words.size();
     const uint64_t len = proof.len;
     B.proof_words += len;
-    for (uint64_t i = 0; i < len; ++i) {
-        const uint64_t v = proof.words[i];
-        B.words.push_back(v >= P ? v - P : v);
+    B.words.resize(base + len);
+    {
+        uint64_t* dst = B.words.data() + base;
+        const uint64_t* src = proof.words;
+        for (uint64_t i = 0; i < len; ++i) {
+            const uint64_t v = src[i];
+            dst[i] = v >= P ? v - P : v;
+        }
     }
     // stage the claim encoding (pinned layout): [out_n+1, out_n, out.., in_n+1, in_n, in.., version, digest]
     const uint64_t cbase = B.words.size();
@@ -548,6 +553,11 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     H.D = D;
     H.desc.reserve(n);
     H.fail.reserve(n);
+    {
+        size_t tot = 0;
+        for (size_t i = 0; i < n; ++i) tot += proofs[i].len + claims[i].input_len + claims[i].output_len + 10;
+        H.words.reserve(tot);
+    }
     for (size_t i = 0; i < n; ++i) decode_proof(H, claims[i], proofs[i]);
     auto t1 = std::chrono::steady_clock::now();
     b->decode_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();

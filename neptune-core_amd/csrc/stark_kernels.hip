@@ -91,6 +91,64 @@ __global__ void __launch_bounds__(64) k_fs_replay(const uint64_t* __restrict__ w
     }
 }
 
+// Same program on the 16-lane "wide" Tip5 (one proof per DPP row): ~10x lower latency per
+// permutation, which is what a sequential sponge needs.
+__global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restrict__ words,
+                                                        const ProofDesc* __restrict__ desc,
+                                                        const FsOp* __restrict__ ops, uint32_t n_proofs,
+                                                        uint64_t* __restrict__ xs, uint32_t* __restrict__ idx_out,
+                                                        const uint32_t* __restrict__ fail) {
+    __shared__ Tip5Lds lds;
+    tip5_lds_init(lds);
+    const uint32_t e = threadIdx.x & 15u;
+    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    if (g >= n_proofs || fail[g]) return;  // uniform within the 16-lane row
+    uint64_t rc[TIP5_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < TIP5_ROUNDS; ++r) rc[r] = c_tip5_rc_raw[r * 16 + e];
+    const ProofDesc& d = desc[g];
+    uint64_t s = 0;
+    uint64_t xcur = d.xs_off * 3;
+    uint64_t icur = d.idx_off;
+    const uint32_t row_shift = threadIdx.x & 48u;  // first lane of this row within the wave
+    for (uint32_t o = 0; o < d.fs_op_n; ++o) {
+        const FsOp op = ops[d.fs_op_off + o];
+        if (op.kind == FS_ABSORB) {
+            const uint64_t* __restrict__ src = words + op.arg;
+            const uint32_t len = op.n;
+            uint32_t pos = 0;
+            for (; pos + TIP5_RATE <= len; pos += TIP5_RATE) {
+                if (e < TIP5_RATE) s = to_mont(src[pos + e]);
+                s = tip5_permute_wide(s, e, rc, lds.lut);
+            }
+            const uint32_t rem = len - pos;
+            if (e < TIP5_RATE) s = e < rem ? to_mont(src[pos + e]) : (e == rem ? MONT_ONE : 0ull);
+            s = tip5_permute_wide(s, e, rc, lds.lut);
+        } else if (op.kind == FS_SQUEEZE_X) {
+            const uint32_t nwords = 3 * op.n;
+            for (uint32_t f = 0; f < nwords; f += TIP5_RATE) {
+                if (e < TIP5_RATE && f + e < nwords) xs[xcur + f + e] = s;
+                s = tip5_permute_wide(s, e, rc, lds.lut);
+            }
+            xcur += nwords;
+        } else {  // FS_SAMPLE_IDX
+            const uint64_t bound = op.arg;
+            uint32_t got = 0;
+            while (got < op.n) {
+                const uint64_t v = from_mont(s);
+                s = tip5_permute_wide(s, e, rc, lds.lut);
+                const bool valid = e < TIP5_RATE && v != GL_P - 1;
+                const uint64_t ball = __ballot(valid);
+                const uint32_t bits = (uint32_t)(ball >> row_shift) & 0x3FFu;
+                const uint32_t rank = __popc(bits & ((1u << e) - 1u));
+                if (valid && got + rank < op.n) idx_out[icur + got + rank] = (uint32_t)((v & 0xFFFFFFFFull) % bound);
+                got += __popc(bits);
+            }
+            icur += op.n;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ revealed-row hashing
 // grid.y = 0 main, 1 aux, 2 quotient; one lane per (proof, row).
 __global__ void __launch_bounds__(256) k_hash_rows(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
@@ -678,8 +736,8 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, StarkPhas
         if (tm && tm->ev[i]) (void)hipEventRecord(tm->ev[i], st);
     };
     mark(0);
-    hipLaunchKernelGGL(k_fs_replay, dim3((n + 63) / 64), dim3(64), 0, st, b.words, b.desc, b.ops, n, b.xs, b.idx,
-                       b.fail);
+    hipLaunchKernelGGL(k_fs_replay_wide, dim3((n * 16 + 255) / 256), dim3(256), 0, st, b.words, b.desc, b.ops, n,
+                       b.xs, b.idx, b.fail);
     mark(1);
     {
         uint64_t rows = (uint64_t)n * k;

@@ -162,3 +162,79 @@ __device__ __forceinline__ void tip5_permute_raw(uint64_t s[16], const uint8_t* 
 }
 
 }  // namespace nhip
+
+namespace nhip {
+
+// ---------------------------------------------------------------------------------------------
+// "Wide" Tip5: one state spread over a 16-lane DPP row (lane e of the row holds state[e]).
+// Used where latency, not throughput, matters (the sequential Fiat-Shamir sponge of one proof):
+// a permutation costs ~10x fewer dependent instructions than the lane-per-state form.  The
+// circulant MDS becomes 16 row rotations (`row_ror:k`, DPP) with one uniform coefficient MDS[k]
+// per rotation: lane e receives state[(e - k) & 15] and out[e] = sum_k MDS[k] * state[e - k].
+// ---------------------------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ uint32_t row_ror(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x120 + K, 0xF, 0xF, false);
+}
+
+template <int K>
+__device__ __forceinline__ void mds_term(uint32_t lo, uint32_t hi, uint64_t& al, uint64_t& ah) {
+    const uint64_t c = TIP5_MDS[K];
+    al += c * row_ror<K>(lo);
+    ah += c * row_ror<K>(hi);
+}
+
+// s: this lane's state word (raw Montgomery); e: lane index within the row; rc: this lane's 5
+// round constants (raw).
+__device__ __forceinline__ uint64_t tip5_permute_wide(uint64_t s, uint32_t e, const uint64_t rc[5],
+                                                      const uint8_t* __restrict__ lut) {
+#pragma unroll
+    for (int r = 0; r < TIP5_ROUNDS; ++r) {
+        // S-box: split-and-lookup on lanes 0..3, x^7 elsewhere
+        if (e < 4) {
+            s = split_and_lookup(lut, s);
+        } else {
+            const uint64_t x2 = mont_mul(s, s);
+            const uint64_t x4 = mont_mul(x2, x2);
+            const uint64_t x3 = mont_mul(s, x2);
+            s = mont_mul(x3, x4);
+        }
+        // MDS over the row
+        const uint32_t lo = (uint32_t)s, hi = (uint32_t)(s >> 32);
+        uint64_t al = (uint64_t)TIP5_MDS[0] * lo, ah = (uint64_t)TIP5_MDS[0] * hi;
+        mds_term<1>(lo, hi, al, ah);
+        mds_term<2>(lo, hi, al, ah);
+        mds_term<3>(lo, hi, al, ah);
+        mds_term<4>(lo, hi, al, ah);
+        mds_term<5>(lo, hi, al, ah);
+        mds_term<6>(lo, hi, al, ah);
+        mds_term<7>(lo, hi, al, ah);
+        mds_term<8>(lo, hi, al, ah);
+        mds_term<9>(lo, hi, al, ah);
+        mds_term<10>(lo, hi, al, ah);
+        mds_term<11>(lo, hi, al, ah);
+        mds_term<12>(lo, hi, al, ah);
+        mds_term<13>(lo, hi, al, ah);
+        mds_term<14>(lo, hi, al, ah);
+        mds_term<15>(lo, hi, al, ah);
+        // recombination + ARK, exactly as mds_ark()
+        unsigned int k1, b1, over, c2, bb, ov2;
+        const uint32_t m1 = __builtin_addc((uint32_t)(al >> 32), (uint32_t)ah, 0u, &k1);
+        const uint32_t sh = (uint32_t)(ah >> 32) + k1;
+        const uint32_t tl = __builtin_subc(0u, sh, 0u, &b1);
+        unsigned int dummy;
+        const uint32_t th = __builtin_subc(sh, 0u, b1, &dummy);
+        uint32_t rl = __builtin_addc((uint32_t)al, tl, 0u, &k1);
+        uint32_t rh = __builtin_addc(m1, th, k1, &over);
+        rl = __builtin_addc(rl, 0u - over, 0u, &c2);
+        rh = rh + c2;
+        const uint64_t q = GL_P - rc[r];
+        rl = __builtin_subc(rl, (uint32_t)q, 0u, &bb);
+        rh = __builtin_subc(rh, (uint32_t)(q >> 32), bb, &ov2);
+        rl = __builtin_subc(rl, 0u - ov2, 0u, &bb);
+        s = ((uint64_t)(rh - bb) << 32) | rl;
+    }
+    return s;
+}
+
+}  // namespace nhip
