@@ -131,7 +131,9 @@ typedef struct {
 } nhip_proof;
 
 typedef struct {
-    uint64_t num_proofs, proof_words, tip5_perms_static;
+    uint64_t num_proofs, proof_words;
+    uint64_t tip5_perms_static;  /* Fiat-Shamir + row hashing + last-codeword trees (from the proof shapes) */
+    uint64_t tip5_perms_merkle;  /* authentication-structure hash_pairs actually performed (device-counted) */
     double ms_decode, ms_upload;  /* host */
     double ms_fiat_shamir, ms_row_hash, ms_merkle, ms_ood_air, ms_fri, ms_deep, ms_device_total; /* device */
 } nhip_stats;

@@ -33,6 +33,7 @@ struct StarkBatchDev {
     uint64_t* ood;
     uint32_t* fail;
     uint8_t* verdicts;
+    unsigned long long* perm_counter;  // Merkle hash_pairs performed (device-counted)
     const AirNode* air_nodes;
     const uint32_t* air_level_nodes;
     const uint32_t* air_level_off;

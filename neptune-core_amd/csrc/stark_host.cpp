@@ -366,6 +366,7 @@ struct nhip_batch {
     bool timed = false;
     double last_ms[8] = {};
     double decode_ms = 0, upload_ms = 0;
+    uint64_t merkle_perms = 0;
 };
 
 // ctx internals live in capi.hip; access the stream / device via these helpers
@@ -383,6 +384,7 @@ bool dims_from(const nhip_stark_params* sp, const nhip_air* air, Dims& D) {
     if (sp->log2_fri_expansion < 1 || sp->log2_fri_expansion > 8) return false;
     if (sp->num_main != air->dims_air.num_main || sp->num_aux != air->dims_air.num_aux) return false;
     if (sp->num_quotient_segments < 1 || sp->num_quotient_segments > 64) return false;
+    if (sp->num_main + sp->num_aux > 512) return false;  // DEEP kernel: <= 8 row columns per lane
     StarkDims& d = D.d;
     d.num_main = sp->num_main;
     d.num_aux = sp->num_aux;
@@ -628,6 +630,7 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     b->d_fail_init = (uint32_t*)ptr[8];
     dv.verdicts = (uint8_t*)ptr[9];
     b->d_perm_counter = (uint64_t*)ptr[10];
+    dv.perm_counter = (unsigned long long*)ptr[10];
     dv.air_nodes = air->d_nodes;
     dv.air_level_nodes = air->d_level_nodes;
     dv.air_level_off = air->d_level_off;
@@ -653,6 +656,7 @@ int nhip_batch_run(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* all
     const uint32_t n = b->dev.n_proofs;
     hipError_t e = hipSuccess;
     if (n) e = hipMemcpyAsync(b->dev.fail, b->d_fail_init, n * 4, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipMemsetAsync(b->d_perm_counter, 0, 8, st);
     if (e != hipSuccess) return hipfail(e);
     if (!b->timed) {
         for (int i = 0; i < 8; ++i)
@@ -663,6 +667,7 @@ int nhip_batch_run(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* all
     if (e != hipSuccess) return hipfail(e);
     std::vector<uint8_t> v(n);
     if (n) e = hipMemcpyAsync(v.data(), b->dev.verdicts, n, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&b->merkle_perms, b->d_perm_counter, 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hipfail(e);
     for (int i = 0; i < 7; ++i) {
@@ -695,6 +700,7 @@ int nhip_batch_stats(const nhip_batch* b, nhip_stats* s) {
     s->ms_device_total = 0;
     for (int i = 0; i < 7; ++i) s->ms_device_total += b->last_ms[i];
     s->tip5_perms_static = b->H.perms_static;
+    s->tip5_perms_merkle = b->merkle_perms;
     return NHIP_OK;
 }
 

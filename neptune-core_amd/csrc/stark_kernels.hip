@@ -189,24 +189,6 @@ __global__ void __launch_bounds__(256) k_hash_rows(const uint64_t* __restrict__ 
 }
 
 // ------------------------------------------------------------------ workgroup helpers
-// exclusive prefix sum over blockDim.x (<= 256) values; returns the total
-__device__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* sh, uint32_t& excl) {
-    const uint32_t tid = threadIdx.x;
-    sh[tid] = v;
-    __syncthreads();
-    for (uint32_t off = 1; off < blockDim.x; off <<= 1) {
-        const uint32_t t = tid >= off ? sh[tid - off] : 0u;
-        __syncthreads();
-        sh[tid] += t;
-        __syncthreads();
-    }
-    const uint32_t incl = sh[tid];
-    const uint32_t total = sh[blockDim.x - 1];
-    __syncthreads();
-    excl = incl - v;
-    return total;
-}
-
 __device__ __forceinline__ void hash_pair_raw(const uint64_t* l, const uint64_t* r, uint64_t* out,
                                               const uint8_t* __restrict__ lut) {
     uint64_t s[16];
@@ -224,22 +206,46 @@ __device__ __forceinline__ void hash_pair_raw(const uint64_t* l, const uint64_t*
 
 // ------------------------------------------------------------------ Merkle multi-proofs
 // twenty-first MerkleTreeInclusionProof::verify: leaves at (index, digest), the authentication
-// structure lists the missing siblings in descending node-index order.  One workgroup (256 lanes)
-// per (proof, tree); tree 0 main, 1 aux, 2 quotient, 3 FRI round-0 a-values, 4 + r FRI round-r
-// b-values.  Nodes of a level are kept sorted by descending node index in LDS, so the siblings
-// that must come from the authentication structure appear exactly in its order.
+// structure lists the missing siblings in descending node-index order.  One workgroup of B lanes
+// (B = 128 for up to 128 collinearity checks, else 256) per (proof, tree); tree 0 main, 1 aux,
+// 2 quotient, 3 FRI round-0 a-values, 4 + r FRI round-r b-values.  Nodes of a level are kept
+// sorted by descending node index in LDS, so the siblings that must come from the authentication
+// structure appear exactly in its order; prefix sums are wave ballots.
+
+// exclusive prefix count of `pred` over the workgroup (<= 4 waves); returns the total
+__device__ __forceinline__ uint32_t wg_count_scan(bool pred, uint32_t& excl, uint32_t* sh) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6, nw = blockDim.x >> 6;
+    const uint64_t b = __ballot(pred);
+    const uint32_t in_wave = (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) sh[w] = (uint32_t)__popcll(b);
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+    for (uint32_t q = 0; q < nw; ++q) {
+        const uint32_t c = sh[q];
+        base += q < w ? c : 0u;
+        total += c;
+    }
+    __syncthreads();
+    excl = base + in_wave;
+    return total;
+}
+
+template <int B>
 struct MpLds {
-    uint32_t key[2][MAX_CHECKS];
-    uint64_t dg[2][MAX_CHECKS][5];
-    uint32_t scan[256];
+    uint32_t key[2][B];
+    uint64_t dg[2][B][5];
+    uint32_t order[B];
+    uint32_t scan[4];
     uint32_t flag;
     Tip5Lds t5;
 };
 
-__global__ void __launch_bounds__(256) k_multiproof(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
-                                                    uint32_t n_proofs, uint32_t k, const uint64_t* __restrict__ dig,
-                                                    const uint32_t* __restrict__ idx_all, uint32_t* __restrict__ fail) {
-    __shared__ MpLds L;
+template <int B>
+__global__ void __launch_bounds__(B) k_multiproof(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+                                                  uint32_t n_proofs, uint32_t k, const uint64_t* __restrict__ dig,
+                                                  const uint32_t* __restrict__ idx_all, uint32_t* __restrict__ fail,
+                                                  unsigned long long* __restrict__ perm_counter) {
+    __shared__ MpLds<B> L;
     const uint32_t p = blockIdx.x, tree = blockIdx.y, tid = threadIdx.x;
     if (p >= n_proofs) return;
     tip5_lds_init(L.t5);
@@ -265,7 +271,7 @@ __global__ void __launch_bounds__(256) k_multiproof(const uint64_t* __restrict__
         fail_bit = FAIL_MERKLE_FRI;
     }
     const uint32_t* __restrict__ idx = idx_all + d.idx_off;
-    // ---- load leaves
+    // ---- load leaves (key = node index = leaf index + 2^h; 0 = empty slot)
     uint32_t key = 0u;
     uint64_t lv[5] = {0, 0, 0, 0, 0};
     if (tid < k) {
@@ -286,53 +292,46 @@ __global__ void __launch_bounds__(256) k_multiproof(const uint64_t* __restrict__
         }
     }
     L.key[0][tid] = key;
+    L.order[tid] = tid;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) L.dg[1][tid][q] = lv[q];
     if (tid == 0) L.flag = 0;
-    // ---- bitonic sort (descending) of (key, original lane) over 256 slots
-    __shared__ uint32_t order[256];
-    order[tid] = tid;
     __syncthreads();
-    for (uint32_t size = 2; size <= 256; size <<= 1) {
+    // ---- bitonic sort (descending) of (key, original slot)
+    for (uint32_t size = 2; size <= (uint32_t)B; size <<= 1) {
         for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
             const uint32_t partner = tid ^ stride;
             if (partner > tid) {
                 const bool desc_dir = (tid & size) == 0;
                 const uint32_t a = L.key[0][tid], b = L.key[0][partner];
-                if ((a < b) == desc_dir) {
+                if ((a < b) == desc_dir && a != b) {
                     L.key[0][tid] = b;
                     L.key[0][partner] = a;
-                    const uint32_t t = order[tid];
-                    order[tid] = order[partner];
-                    order[partner] = t;
+                    const uint32_t t = L.order[tid];
+                    L.order[tid] = L.order[partner];
+                    L.order[partner] = t;
                 }
             }
             __syncthreads();
         }
     }
-    // scatter digests into sorted order (via LDS staging of the unsorted digests)
-    {
-        // stage unsorted leaf digests in dg[1]
-#pragma unroll
-        for (int q = 0; q < 5; ++q) L.dg[1][tid][q] = lv[q];
-    }
-    __syncthreads();
     const uint32_t skey = L.key[0][tid];
     uint64_t sd[5];
 #pragma unroll
-    for (int q = 0; q < 5; ++q) sd[q] = L.dg[1][order[tid]][q];
+    for (int q = 0; q < 5; ++q) sd[q] = L.dg[1][L.order[tid]][q];
     // dedupe: equal keys must carry equal digests
     bool dup = false;
     if (skey != 0 && tid > 0 && L.key[0][tid - 1] == skey) {
         dup = true;
         bool same = true;
-        const uint32_t o2 = order[tid - 1];
+        const uint32_t o2 = L.order[tid - 1];
 #pragma unroll
         for (int q = 0; q < 5; ++q) same &= (L.dg[1][o2][q] == sd[q]);
         if (!same) atomicOr(&L.flag, 1u);
     }
-    const uint32_t keep = (skey != 0 && !dup) ? 1u : 0u;
+    const bool keep = skey != 0 && !dup;
     uint32_t pos;
-    uint32_t m = block_exclusive_scan(keep, L.scan, pos);
-    __syncthreads();
+    uint32_t m = wg_count_scan(keep, pos, L.scan);
     if (keep) {
         L.key[0][pos] = skey;
 #pragma unroll
@@ -341,22 +340,22 @@ __global__ void __launch_bounds__(256) k_multiproof(const uint64_t* __restrict__
     __syncthreads();
     // ---- climb
     const uint64_t* __restrict__ auth = words + auth_off;
-    uint32_t ap = 0;
+    uint32_t ap = 0, hashed = 0;
     int cur = 0;
     for (uint32_t lvl = 0; lvl < h; ++lvl) {
         const uint32_t i = tid;
-        uint32_t ki = 0, unpaired = 0, owner = 0;
-        bool pair_next = false;
+        uint32_t ki = 0;
+        bool unpaired = false, owner = false, pair_next = false;
         if (i < m) {
             ki = L.key[cur][i];
             const bool pair_prev = i > 0 && L.key[cur][i - 1] == (ki ^ 1u);
             pair_next = i + 1 < m && L.key[cur][i + 1] == (ki ^ 1u);
-            unpaired = (!pair_prev && !pair_next) ? 1u : 0u;
-            owner = pair_prev ? 0u : 1u;
+            unpaired = !pair_prev && !pair_next;
+            owner = !pair_prev;
         }
         uint32_t upos, opos;
-        const uint32_t n_unp = block_exclusive_scan(unpaired, L.scan, upos);
-        const uint32_t n_own = block_exclusive_scan(owner, L.scan, opos);
+        const uint32_t n_unp = wg_count_scan(unpaired, upos, L.scan);
+        const uint32_t n_own = wg_count_scan(owner, opos, L.scan);
         if (ap + n_unp > auth_n) {
             if (tid == 0) L.flag = 1u;
             __syncthreads();
@@ -391,6 +390,7 @@ __global__ void __launch_bounds__(256) k_multiproof(const uint64_t* __restrict__
         }
         ap += n_unp;
         m = n_own;
+        hashed += n_own;
         cur ^= 1;
         __syncthreads();
     }
@@ -402,6 +402,7 @@ __global__ void __launch_bounds__(256) k_multiproof(const uint64_t* __restrict__
             for (int q = 0; q < 5; ++q) ok &= (L.dg[cur][0][q] == to_mont(rt[q]));
         }
         if (!ok) atomicOr(&fail[p], fail_bit);
+        if (perm_counter) atomicAdd(perm_counter, (unsigned long long)hashed);
     }
 }
 
@@ -655,11 +656,18 @@ __global__ void __launch_bounds__(256) k_fri(const uint64_t* __restrict__ words,
 }
 
 // ------------------------------------------------------------------ DEEP
-// One workgroup per proof; wave w handles revealed rows j = w, w + 4, ...; lanes split the row.
+// One workgroup per proof.  Phase 1: wave w forms the linear combinations of revealed rows
+// j = w, w + 4, ... (lanes split the row; the row weights stay in registers).  Phase 2: the 3k DEEP
+// quotient terms (row j, term t) are independent XFE inversions, one per lane.  Phase 3: lane j sums
+// its row's three terms and compares with the FRI round-0 value.
+static constexpr uint32_t DEEP_MAX_COLS_PER_LANE = 8;  // (M + A) <= 512
+
 __global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                               uint32_t n_proofs, StarkDims dims, const uint64_t* __restrict__ xs,
                                               const uint32_t* __restrict__ idx_all, const uint64_t* __restrict__ ood,
                                               uint32_t* __restrict__ fail) {
+    __shared__ Xfe s_row[MAX_CHECKS], s_quot[MAX_CHECKS], s_term[3 * MAX_CHECKS];
+    __shared__ uint32_t s_flag;
     const uint32_t p = blockIdx.x, tid = threadIdx.x;
     if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
     const ProofDesc& d = desc[p];
@@ -667,32 +675,29 @@ __global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words
     const uint64_t xb = d.xs_off * 3;
     const uint32_t M = dims.num_main, A = dims.num_aux, Q = dims.num_quot_seg, k = dims.num_checks;
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
-    const Xfe z = ld_xfe_raw(xs, xb + 3ull * sl.z);
-    const uint64_t w_tr = root_of_unity(d.log2_ph);
-    const Xfe z_next = x_scale(z, w_tr);
-    Xfe z4 = x_one();
-    for (uint32_t q = 0; q < Q; ++q) z4 = x_mul(z4, z);
-    const Xfe o_curr = ld_xfe_raw(ood, (uint64_t)p * 9 + 0);
-    const Xfe o_next = ld_xfe_raw(ood, (uint64_t)p * 9 + 3);
-    const Xfe o_q = ld_xfe_raw(ood, (uint64_t)p * 9 + 6);
-    const uint64_t gN = root_of_unity(d.log2_N);
-    const uint32_t* __restrict__ idx = idx_all + d.idx_off;
-    uint32_t f = 0;
+    if (tid == 0) s_flag = 0;
+    Xfe wcol[DEEP_MAX_COLS_PER_LANE];
+#pragma unroll
+    for (uint32_t i = 0; i < DEEP_MAX_COLS_PER_LANE; ++i) {
+        const uint32_t c = lane + 64 * i;
+        wcol[i] = c < M + A ? ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + c)) : x_zero();
+    }
+    const Xfe wq = lane < Q ? ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + lane)) : x_zero();
     for (uint32_t j = wave; j < k; j += nwaves) {
         Xfe acc = x_zero();
-        for (uint32_t c = lane; c < M + A; c += 64) {
-            const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + c));
+        const uint64_t* __restrict__ mrow = words + d.main_rows_off + (uint64_t)j * M;
+        const uint64_t arow = d.aux_rows_off + (uint64_t)j * 3 * A;
+#pragma unroll
+        for (uint32_t i = 0; i < DEEP_MAX_COLS_PER_LANE; ++i) {
+            const uint32_t c = lane + 64 * i;
             if (c < M) {
-                acc = x_add(acc, x_scale(w, to_mont(words[d.main_rows_off + (uint64_t)j * M + c])));
-            } else {
-                acc = x_add(acc, x_mul(w, ld_xfe_canon(words, d.aux_rows_off + (uint64_t)j * 3 * A + 3ull * (c - M))));
+                acc = x_add(acc, x_scale(wcol[i], to_mont(mrow[c])));
+            } else if (c < M + A) {
+                acc = x_add(acc, x_mul(wcol[i], ld_xfe_canon(words, arow + 3ull * (c - M))));
             }
         }
         Xfe qv = x_zero();
-        if (lane < Q) {
-            const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + lane));
-            qv = x_mul(w, ld_xfe_canon(words, d.quot_rows_off + (uint64_t)j * 3 * Q + 3ull * lane));
-        }
+        if (lane < Q) qv = x_mul(wq, ld_xfe_canon(words, d.quot_rows_off + (uint64_t)j * 3 * Q + 3ull * lane));
         for (int s = 32; s > 0; s >>= 1) {
             acc.c0 = gl_add(acc.c0, __shfl_xor(acc.c0, s));
             acc.c1 = gl_add(acc.c1, __shfl_xor(acc.c1, s));
@@ -702,22 +707,44 @@ __global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words
             qv.c2 = gl_add(qv.c2, __shfl_xor(qv.c2, s));
         }
         if (lane == 0) {
-            const uint64_t x = mont_mul(to_mont(7), b_pow(gN, idx[j]));
-            const Xfe d0 = x_sub(x_lift(x), z), d1 = x_sub(x_lift(x), z_next), d2 = x_sub(x_lift(x), z4);
-            if (x_is_zero(d0) || x_is_zero(d1) || x_is_zero(d2)) {
-                f |= FAIL_ZERO_INVERSE;
-            } else {
-                const Xfe t0 = x_mul(x_sub(acc, o_curr), x_inv(d0));
-                const Xfe t1 = x_mul(x_sub(acc, o_next), x_inv(d1));
-                const Xfe t2 = x_mul(x_sub(qv, o_q), x_inv(d2));
-                const Xfe wd0 = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + Q + 0));
-                const Xfe wd1 = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + Q + 1));
-                const Xfe wd2 = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + Q + 2));
-                const Xfe deep = x_add(x_add(x_mul(t0, wd0), x_mul(t1, wd1)), x_mul(t2, wd2));
-                const Xfe fri_v = ld_xfe_canon(words, d.fri[0].leaves_off + 3ull * j);
-                if (!x_eq(deep, fri_v)) f |= FAIL_DEEP;
-            }
+            s_row[j] = acc;
+            s_quot[j] = qv;
         }
+    }
+    __syncthreads();
+    const Xfe z = ld_xfe_raw(xs, xb + 3ull * sl.z);
+    const uint64_t gN = root_of_unity(d.log2_N);
+    const uint32_t* __restrict__ idx = idx_all + d.idx_off;
+    for (uint32_t t = tid; t < 3 * k; t += blockDim.x) {
+        const uint32_t j = t / 3, which = t - 3 * j;
+        Xfe at;  // evaluation point of this term: z, z * w_trace, z^Q
+        if (which == 0) {
+            at = z;
+        } else if (which == 1) {
+            at = x_scale(z, root_of_unity(d.log2_ph));
+        } else {
+            at = x_one();
+            for (uint32_t q = 0; q < Q; ++q) at = x_mul(at, z);
+        }
+        const uint64_t x = mont_mul(to_mont(7), b_pow(gN, idx[j]));
+        const Xfe den = x_sub(x_lift(x), at);
+        const Xfe num = which == 2 ? x_sub(s_quot[j], ld_xfe_raw(ood, (uint64_t)p * 9 + 6))
+                                   : x_sub(s_row[j], ld_xfe_raw(ood, (uint64_t)p * 9 + 3 * which));
+        if (x_is_zero(den)) {
+            atomicOr(&s_flag, 1u);
+            s_term[t] = x_zero();
+        } else {
+            const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + Q + which));
+            s_term[t] = x_mul(x_mul(num, x_inv(den)), w);
+        }
+    }
+    __syncthreads();
+    uint32_t f = 0;
+    if (tid == 0 && s_flag) f |= FAIL_ZERO_INVERSE;
+    for (uint32_t j = tid; j < k; j += blockDim.x) {
+        const Xfe deep = x_add(x_add(s_term[3 * j], s_term[3 * j + 1]), s_term[3 * j + 2]);
+        const Xfe fri_v = ld_xfe_canon(words, d.fri[0].leaves_off + 3ull * j);
+        if (!x_eq(deep, fri_v)) f |= FAIL_DEEP;
     }
     if (f) atomicOr(&fail[p], f);
 }
@@ -746,8 +773,12 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, StarkPhas
         hipLaunchKernelGGL(k_hash_rows, dim3(gx, 3), dim3(256), 0, st, b.words, b.desc, n, k, b.dims, b.dig, b.fail);
     }
     mark(2);
-    hipLaunchKernelGGL(k_multiproof, dim3(n, 4 + b.max_R), dim3(256), 0, st, b.words, b.desc, n, k, b.dig, b.idx,
-                       b.fail);
+    if (k <= 128)
+        hipLaunchKernelGGL(k_multiproof<128>, dim3(n, 4 + b.max_R), dim3(128), 0, st, b.words, b.desc, n, k, b.dig,
+                           b.idx, b.fail, b.perm_counter);
+    else
+        hipLaunchKernelGGL(k_multiproof<256>, dim3(n, 4 + b.max_R), dim3(256), 0, st, b.words, b.desc, n, k, b.dig,
+                           b.idx, b.fail, b.perm_counter);
     mark(3);
     hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(256), b.air_lds_bytes, st, b.words, b.desc, n, b.dims, b.air_nodes,
                        b.air_level_nodes, b.air_level_off, b.air_n_levels, b.air_cons, b.air_cons_off, b.xs, b.ood,

@@ -41,7 +41,8 @@ class Proof(ctypes.Structure):
 
 class Stats(ctypes.Structure):
     _fields_ = [("num_proofs", ctypes.c_uint64), ("proof_words", ctypes.c_uint64),
-                ("tip5_perms_static", ctypes.c_uint64), ("ms_decode", ctypes.c_double),
+                ("tip5_perms_static", ctypes.c_uint64), ("tip5_perms_merkle", ctypes.c_uint64),
+                ("ms_decode", ctypes.c_double),
                 ("ms_upload", ctypes.c_double), ("ms_fiat_shamir", ctypes.c_double),
                 ("ms_row_hash", ctypes.c_double), ("ms_merkle", ctypes.c_double),
                 ("ms_ood_air", ctypes.c_double), ("ms_fri", ctypes.c_double), ("ms_deep", ctypes.c_double),
