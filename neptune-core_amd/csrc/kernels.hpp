@@ -21,6 +21,22 @@ hipError_t launch_mtree_verify(const uint64_t* d_roots, int per_path_root, const
 static constexpr uint32_t AIR_LDS_HEADER = (256 + 4 + 4) * 24 + 16;  // red, zinv, derived, flag
 static constexpr uint32_t FRI_LDS_HEADER = 256 * 24 + 256 + 16;      // red, tip5 lut, flag
 
+// Level-synchronous Merkle multiproof plan (see k_mp_plan in stark_kernels.hip)
+struct MpRoot {
+    uint64_t code;  // source code of the tree's final node, ~0 = no check (skipped or already failed)
+    uint64_t root_off;
+    uint32_t fail_bit, pad;
+};
+struct MpPlan {
+    uint64_t* ops;               // 2 source codes per op, level-major: op g at level_base[l] + pos
+    uint64_t* arena;             // parent digest of op g (Montgomery), 5 words
+    const uint64_t* level_base;  // levels entries
+    const uint64_t* cap;         // op capacity per level
+    uint32_t* counter;           // ops appended per level (zeroed per run)
+    MpRoot* roots;               // n_proofs x (4 + max_R)
+    uint32_t levels;
+};
+
 struct StarkBatchDev {
     uint32_t n_proofs, max_R;
     StarkDims dims;
@@ -34,6 +50,8 @@ struct StarkBatchDev {
     uint32_t* fail;
     uint8_t* verdicts;
     unsigned long long* perm_counter;  // Merkle hash_pairs performed (device-counted)
+    MpPlan mp;
+    const uint64_t* mp_cap_host;  // host copy of mp.cap (launch sizes)
     const AirNode* air_nodes;
     const uint32_t* air_level_nodes;
     const uint32_t* air_level_off;

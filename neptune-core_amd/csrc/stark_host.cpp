@@ -367,6 +367,7 @@ struct nhip_batch {
     double last_ms[8] = {};
     double decode_ms = 0, upload_ms = 0;
     uint64_t merkle_perms = 0;
+    std::vector<uint64_t> mp_cap;  // multiproof op capacity per level
 };
 
 // ctx internals live in capi.hip; access the stream / device via these helpers
@@ -577,6 +578,23 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
         attrs = true;
     }
     const uint32_t k = D.d.num_checks;
+    // multiproof op capacity per level: a tree of height h has at most min(k, 2^(h-1-l)) parents at level l
+    const uint32_t tpp = 4 + H.max_R;
+    uint32_t levels = 0;
+    for (size_t i = 0; i < n; ++i)
+        if (!(H.fail[i] & FAIL_DECODE)) levels = std::max(levels, H.desc[i].log2_N);
+    b->mp_cap.assign(levels, 0);
+    for (size_t i = 0; i < n; ++i) {
+        if (H.fail[i] & FAIL_DECODE) continue;
+        const ProofDesc& pd = H.desc[i];
+        for (uint32_t t = 0; t < 4 + pd.R; ++t) {
+            const uint32_t h = t < 4 ? pd.log2_N : pd.log2_N - (t - 4);
+            for (uint32_t l = 0; l < h; ++l) b->mp_cap[l] += std::min<uint64_t>(k, 1ull << std::min(h - 1 - l, 40u));
+        }
+    }
+    std::vector<uint64_t> mp_base(levels + 1, 0);
+    for (uint32_t l = 0; l < levels; ++l) mp_base[l + 1] = mp_base[l] + b->mp_cap[l];
+    const uint64_t mp_total = mp_base[levels];
     const size_t sz[] = {H.words.size() * 8 + 8,
                          std::max<size_t>(1, n) * sizeof(ProofDesc),
                          H.ops.size() * sizeof(FsOp) + 8,
@@ -587,7 +605,14 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
                          std::max<size_t>(1, n) * 4,
                          std::max<size_t>(1, n) * 4,
                          std::max<size_t>(1, n),
-                         8};
+                         8,
+                         mp_total * 16 + 16,
+                         mp_total * 40 + 40,
+                         (size_t)levels * 8 + 8,
+                         (size_t)levels * 8 + 8,
+                         (size_t)levels * 4 + 4,
+                         std::max<size_t>(1, n) * tpp * sizeof(MpRoot)};
+    constexpr int NBUF = sizeof(sz) / sizeof(sz[0]);
     size_t total = 0;
     for (size_t s : sz) total += al(s);
     hipError_t e = hipMalloc(&b->dmem, total);
@@ -596,8 +621,8 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
         return hipfail(e);
     }
     char* p = (char*)b->dmem;
-    void* ptr[11];
-    for (int i = 0; i < 11; ++i) {
+    void* ptr[NBUF];
+    for (int i = 0; i < NBUF; ++i) {
         ptr[i] = p;
         p += al(sz[i]);
     }
@@ -607,6 +632,8 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     if (e == hipSuccess && !H.ops.empty())
         e = hipMemcpyAsync(ptr[2], H.ops.data(), H.ops.size() * sizeof(FsOp), hipMemcpyHostToDevice, st);
     if (e == hipSuccess && n) e = hipMemcpyAsync(ptr[8], H.fail.data(), n * 4, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && levels) e = hipMemcpyAsync(ptr[13], mp_base.data(), levels * 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && levels) e = hipMemcpyAsync(ptr[14], b->mp_cap.data(), levels * 8, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     auto t2 = std::chrono::steady_clock::now();
     b->upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
@@ -631,6 +658,14 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     dv.verdicts = (uint8_t*)ptr[9];
     b->d_perm_counter = (uint64_t*)ptr[10];
     dv.perm_counter = (unsigned long long*)ptr[10];
+    dv.mp.ops = (uint64_t*)ptr[11];
+    dv.mp.arena = (uint64_t*)ptr[12];
+    dv.mp.level_base = (const uint64_t*)ptr[13];
+    dv.mp.cap = (const uint64_t*)ptr[14];
+    dv.mp.counter = (uint32_t*)ptr[15];
+    dv.mp.roots = (MpRoot*)ptr[16];
+    dv.mp.levels = levels;
+    dv.mp_cap_host = b->mp_cap.data();
     dv.air_nodes = air->d_nodes;
     dv.air_level_nodes = air->d_level_nodes;
     dv.air_level_off = air->d_level_off;
@@ -657,6 +692,7 @@ int nhip_batch_run(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* all
     hipError_t e = hipSuccess;
     if (n) e = hipMemcpyAsync(b->dev.fail, b->d_fail_init, n * 4, hipMemcpyDeviceToDevice, st);
     if (e == hipSuccess) e = hipMemsetAsync(b->d_perm_counter, 0, 8, st);
+    if (e == hipSuccess && b->dev.mp.levels) e = hipMemsetAsync(b->dev.mp.counter, 0, b->dev.mp.levels * 4, st);
     if (e != hipSuccess) return hipfail(e);
     if (!b->timed) {
         for (int i = 0; i < 8; ++i)

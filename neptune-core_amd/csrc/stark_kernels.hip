@@ -206,11 +206,38 @@ __device__ __forceinline__ void hash_pair_raw(const uint64_t* l, const uint64_t*
 
 // ------------------------------------------------------------------ Merkle multi-proofs
 // twenty-first MerkleTreeInclusionProof::verify: leaves at (index, digest), the authentication
-// structure lists the missing siblings in descending node-index order.  One workgroup of B lanes
-// (B = 128 for up to 128 collinearity checks, else 256) per (proof, tree); tree 0 main, 1 aux,
-// 2 quotient, 3 FRI round-0 a-values, 4 + r FRI round-r b-values.  Nodes of a level are kept
-// sorted by descending node index in LDS, so the siblings that must come from the authentication
-// structure appear exactly in its order; prefix sums are wave ballots.
+// structure lists the missing siblings in descending node-index order.  Trees per proof: 0 main,
+// 1 aux, 2 quotient, 3 FRI round-0 a-values, 4 + r FRI round-r b-values.
+//
+// Level-synchronous design: which nodes get hashed, and from which children, depends only on the
+// leaf indices and the authentication-structure length.  k_mp_plan (one workgroup per
+// (proof, tree)) sorts and dedupes the leaves and climbs the tree on indices alone, appending one
+// hash op per parent node to a global per-level op list (slot reserved with one atomic per
+// workgroup and level).  k_mp_hash then runs once per level over ALL trees of ALL proofs (one lane
+// per op, full waves regardless of tree shape), and k_mp_roots compares each tree's final node with
+// its committed root.  Child digests are referenced by 64-bit source codes (type in the top 2 bits).
+enum : uint64_t { MPS_ARENA = 0, MPS_AUTH = 1, MPS_DIG = 2, MPS_XFE = 3 };
+static constexpr uint64_t MPS_MASK = (1ull << 62) - 1, MPS_NONE = ~0ull;
+__device__ __forceinline__ uint64_t mps(uint64_t type, uint64_t v) { return (type << 62) | v; }
+
+__device__ __forceinline__ void mp_load(uint64_t code, const uint64_t* __restrict__ words,
+                                        const uint64_t* __restrict__ dig, const uint64_t* __restrict__ arena,
+                                        uint64_t o[5]) {
+    const uint64_t t = code >> 62, v = code & MPS_MASK;
+    if (t == MPS_ARENA || t == MPS_DIG) {
+        const uint64_t* s = (t == MPS_ARENA ? arena : dig) + 5 * v;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) o[q] = s[q];
+    } else if (t == MPS_AUTH) {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) o[q] = to_mont(words[v + q]);
+    } else {  // an XFE leaf of a FRI codeword: digest [c0, c1, c2, 0, 0]
+#pragma unroll
+        for (int q = 0; q < 3; ++q) o[q] = to_mont(words[v + q]);
+        o[3] = 0;
+        o[4] = 0;
+    }
+}
 
 // exclusive prefix count of `pred` over the workgroup (<= 4 waves); returns the total
 __device__ __forceinline__ uint32_t wg_count_scan(bool pred, uint32_t& excl, uint32_t* sh) {
@@ -231,30 +258,30 @@ __device__ __forceinline__ uint32_t wg_count_scan(bool pred, uint32_t& excl, uin
 }
 
 template <int B>
-struct MpLds {
+struct MpPlanLds {
     uint32_t key[2][B];
-    uint64_t dg[2][B][5];
+    uint64_t src[2][B];
     uint32_t order[B];
     uint32_t scan[4];
-    uint32_t flag;
-    Tip5Lds t5;
+    uint32_t flag, base;
 };
 
 template <int B>
-__global__ void __launch_bounds__(B) k_multiproof(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
-                                                  uint32_t n_proofs, uint32_t k, const uint64_t* __restrict__ dig,
-                                                  const uint32_t* __restrict__ idx_all, uint32_t* __restrict__ fail,
-                                                  unsigned long long* __restrict__ perm_counter) {
-    __shared__ MpLds<B> L;
+__global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+                                               uint32_t n_proofs, uint32_t k, uint32_t trees_per_proof,
+                                               const uint64_t* __restrict__ dig, const uint32_t* __restrict__ idx_all,
+                                               MpPlan plan, uint32_t* __restrict__ fail,
+                                               unsigned long long* __restrict__ perm_counter) {
+    __shared__ MpPlanLds<B> L;
     const uint32_t p = blockIdx.x, tree = blockIdx.y, tid = threadIdx.x;
     if (p >= n_proofs) return;
-    tip5_lds_init(L.t5);
+    MpRoot* rec = plan.roots + (uint64_t)p * trees_per_proof + tree;
+    if (tid == 0) rec->code = MPS_NONE;
     const ProofDesc& d = desc[p];
     if (fail[p] & FAIL_DECODE) return;
     if (tree >= 4 + d.R) return;
-    uint32_t h;
+    uint32_t h, auth_n, fail_bit;
     uint64_t root_off, auth_off;
-    uint32_t auth_n, fail_bit;
     if (tree < 3) {
         h = d.log2_N;
         root_off = tree == 0 ? d.main_root : (tree == 1 ? d.aux_root : d.quot_root);
@@ -271,30 +298,21 @@ __global__ void __launch_bounds__(B) k_multiproof(const uint64_t* __restrict__ w
         fail_bit = FAIL_MERKLE_FRI;
     }
     const uint32_t* __restrict__ idx = idx_all + d.idx_off;
-    // ---- load leaves (key = node index = leaf index + 2^h; 0 = empty slot)
+    // ---- leaves (key = node index = leaf index + 2^h; 0 = empty slot)
     uint32_t key = 0u;
-    uint64_t lv[5] = {0, 0, 0, 0, 0};
+    uint64_t code = MPS_NONE;
     if (tid < k) {
         const uint64_t nl = 1ull << h;
         uint64_t li = idx[tid];
         if (tree == 3) li = li % nl;
         if (tree >= 4) li = (li + nl / 2) % nl;
         key = (uint32_t)(li + nl);
-        if (tree < 3) {
-            const uint64_t* s = dig + (((uint64_t)p * 3 + tree) * k + tid) * 5;
-#pragma unroll
-            for (int q = 0; q < 5; ++q) lv[q] = s[q];
-        } else {
-            const uint64_t off = (tree == 3 ? d.fri[0].leaves_off : d.fri[tree - 3].leaves_off) + 3ull * tid;
-            lv[0] = to_mont(words[off]);
-            lv[1] = to_mont(words[off + 1]);
-            lv[2] = to_mont(words[off + 2]);
-        }
+        code = tree < 3 ? mps(MPS_DIG, ((uint64_t)p * 3 + tree) * k + tid)
+                        : mps(MPS_XFE, (tree == 3 ? d.fri[0].leaves_off : d.fri[tree - 3].leaves_off) + 3ull * tid);
     }
     L.key[0][tid] = key;
+    L.src[1][tid] = code;
     L.order[tid] = tid;
-#pragma unroll
-    for (int q = 0; q < 5; ++q) L.dg[1][tid][q] = lv[q];
     if (tid == 0) L.flag = 0;
     __syncthreads();
     // ---- bitonic sort (descending) of (key, original slot)
@@ -316,17 +334,17 @@ __global__ void __launch_bounds__(B) k_multiproof(const uint64_t* __restrict__ w
         }
     }
     const uint32_t skey = L.key[0][tid];
-    uint64_t sd[5];
-#pragma unroll
-    for (int q = 0; q < 5; ++q) sd[q] = L.dg[1][L.order[tid]][q];
+    const uint64_t scode = L.src[1][L.order[tid]];
     // dedupe: equal keys must carry equal digests
     bool dup = false;
     if (skey != 0 && tid > 0 && L.key[0][tid - 1] == skey) {
         dup = true;
+        uint64_t a[5], b[5];
+        mp_load(scode, words, dig, nullptr, a);
+        mp_load(L.src[1][L.order[tid - 1]], words, dig, nullptr, b);
         bool same = true;
-        const uint32_t o2 = L.order[tid - 1];
 #pragma unroll
-        for (int q = 0; q < 5; ++q) same &= (L.dg[1][o2][q] == sd[q]);
+        for (int q = 0; q < 5; ++q) same &= a[q] == b[q];
         if (!same) atomicOr(&L.flag, 1u);
     }
     const bool keep = skey != 0 && !dup;
@@ -334,12 +352,10 @@ __global__ void __launch_bounds__(B) k_multiproof(const uint64_t* __restrict__ w
     uint32_t m = wg_count_scan(keep, pos, L.scan);
     if (keep) {
         L.key[0][pos] = skey;
-#pragma unroll
-        for (int q = 0; q < 5; ++q) L.dg[0][pos][q] = sd[q];
+        L.src[0][pos] = scode;
     }
     __syncthreads();
-    // ---- climb
-    const uint64_t* __restrict__ auth = words + auth_off;
+    // ---- climb on indices; emit one op per parent
     uint32_t ap = 0, hashed = 0;
     int cur = 0;
     for (uint32_t lvl = 0; lvl < h; ++lvl) {
@@ -356,37 +372,30 @@ __global__ void __launch_bounds__(B) k_multiproof(const uint64_t* __restrict__ w
         uint32_t upos, opos;
         const uint32_t n_unp = wg_count_scan(unpaired, upos, L.scan);
         const uint32_t n_own = wg_count_scan(owner, opos, L.scan);
-        if (ap + n_unp > auth_n) {
+        if (tid == 0) L.base = n_own ? atomicAdd(plan.counter + lvl, n_own) : 0u;
+        __syncthreads();
+        const uint32_t base = L.base;
+        if (ap + n_unp > auth_n || lvl >= plan.levels || (uint64_t)base + n_own > plan.cap[lvl]) {
             if (tid == 0) L.flag = 1u;
-            __syncthreads();
-            break;
+            break;  // uniform: every lane takes it
         }
         if (owner) {
-            uint64_t left[5], right[5];
-            const uint64_t* mine = L.dg[cur][i];
+            const uint64_t mine = L.src[cur][i];
+            uint64_t lc, rc;
             if (pair_next) {  // i holds 2q+1, i+1 holds 2q
-#pragma unroll
-                for (int q = 0; q < 5; ++q) {
-                    right[q] = mine[q];
-                    left[q] = L.dg[cur][i + 1][q];
-                }
+                lc = L.src[cur][i + 1];
+                rc = mine;
             } else {
-                const uint64_t* a = auth + 5ull * (ap + upos);
-                uint64_t sib[5];
-#pragma unroll
-                for (int q = 0; q < 5; ++q) sib[q] = to_mont(a[q]);
+                const uint64_t sib = mps(MPS_AUTH, auth_off + 5ull * (ap + upos));
                 const bool odd = (ki & 1u) != 0;
-#pragma unroll
-                for (int q = 0; q < 5; ++q) {
-                    left[q] = odd ? sib[q] : mine[q];
-                    right[q] = odd ? mine[q] : sib[q];
-                }
+                lc = odd ? sib : mine;
+                rc = odd ? mine : sib;
             }
-            uint64_t par[5];
-            hash_pair_raw(left, right, par, L.t5.lut);
+            const uint64_t g = plan.level_base[lvl] + base + opos;
+            plan.ops[2 * g] = lc;
+            plan.ops[2 * g + 1] = rc;
             L.key[cur ^ 1][opos] = ki >> 1;
-#pragma unroll
-            for (int q = 0; q < 5; ++q) L.dg[cur ^ 1][opos][q] = par[q];
+            L.src[cur ^ 1][opos] = mps(MPS_ARENA, g);
         }
         ap += n_unp;
         m = n_own;
@@ -394,16 +403,50 @@ __global__ void __launch_bounds__(B) k_multiproof(const uint64_t* __restrict__ w
         cur ^= 1;
         __syncthreads();
     }
+    __syncthreads();
     if (tid == 0) {
-        bool ok = L.flag == 0 && m == 1 && L.key[cur][0] == 1u && ap == auth_n;
+        const bool ok = L.flag == 0 && m == 1 && L.key[cur][0] == 1u && ap == auth_n;
         if (ok) {
-            const uint64_t* rt = words + root_off;
-#pragma unroll
-            for (int q = 0; q < 5; ++q) ok &= (L.dg[cur][0][q] == to_mont(rt[q]));
+            rec->code = L.src[cur][0];
+            rec->root_off = root_off;
+            rec->fail_bit = fail_bit;
+        } else {
+            atomicOr(&fail[p], fail_bit);
         }
-        if (!ok) atomicOr(&fail[p], fail_bit);
         if (perm_counter) atomicAdd(perm_counter, (unsigned long long)hashed);
     }
+}
+
+__global__ void __launch_bounds__(256) k_mp_hash(const uint64_t* __restrict__ words, const uint64_t* __restrict__ dig,
+                                                 MpPlan plan, uint32_t lvl) {
+    __shared__ Tip5Lds t5;
+    tip5_lds_init(t5);
+    const uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pos >= plan.counter[lvl]) return;
+    const uint64_t g = plan.level_base[lvl] + pos;
+    uint64_t s[16];
+    mp_load(plan.ops[2 * g], words, dig, plan.arena, s);
+    mp_load(plan.ops[2 * g + 1], words, dig, plan.arena, s + 5);
+#pragma unroll
+    for (int q = 10; q < 16; ++q) s[q] = MONT_ONE;
+    tip5_permute_raw(s, t5.lut);
+    uint64_t* o = plan.arena + 5 * g;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) o[q] = s[q];
+}
+
+__global__ void k_mp_roots(const uint64_t* __restrict__ words, const uint64_t* __restrict__ dig, MpPlan plan,
+                           uint32_t n_records, uint32_t trees_per_proof, uint32_t* __restrict__ fail) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_records) return;
+    const MpRoot r = plan.roots[i];
+    if (r.code == MPS_NONE) return;
+    uint64_t v[5];
+    mp_load(r.code, words, dig, plan.arena, v);
+    bool ok = true;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) ok &= v[q] == to_mont(words[r.root_off + q]);
+    if (!ok) atomicOr(&fail[i / trees_per_proof], r.fail_bit);
 }
 
 // ------------------------------------------------------------------ XFE block reduction
@@ -773,12 +816,23 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, StarkPhas
         hipLaunchKernelGGL(k_hash_rows, dim3(gx, 3), dim3(256), 0, st, b.words, b.desc, n, k, b.dims, b.dig, b.fail);
     }
     mark(2);
-    if (k <= 128)
-        hipLaunchKernelGGL(k_multiproof<128>, dim3(n, 4 + b.max_R), dim3(128), 0, st, b.words, b.desc, n, k, b.dig,
-                           b.idx, b.fail, b.perm_counter);
-    else
-        hipLaunchKernelGGL(k_multiproof<256>, dim3(n, 4 + b.max_R), dim3(256), 0, st, b.words, b.desc, n, k, b.dig,
-                           b.idx, b.fail, b.perm_counter);
+    {
+        const uint32_t tpp = 4 + b.max_R;
+        if (k <= 128)
+            hipLaunchKernelGGL(k_mp_plan<128>, dim3(n, tpp), dim3(128), 0, st, b.words, b.desc, n, k, tpp, b.dig, b.idx,
+                               b.mp, b.fail, b.perm_counter);
+        else
+            hipLaunchKernelGGL(k_mp_plan<256>, dim3(n, tpp), dim3(256), 0, st, b.words, b.desc, n, k, tpp, b.dig, b.idx,
+                               b.mp, b.fail, b.perm_counter);
+        for (uint32_t l = 0; l < b.mp.levels; ++l) {
+            const uint64_t cap = b.mp_cap_host[l];
+            if (cap == 0) continue;
+            hipLaunchKernelGGL(k_mp_hash, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, b.words, b.dig, b.mp, l);
+        }
+        const uint32_t nrec = n * tpp;
+        hipLaunchKernelGGL(k_mp_roots, dim3((nrec + 255) / 256), dim3(256), 0, st, b.words, b.dig, b.mp, nrec, tpp,
+                           b.fail);
+    }
     mark(3);
     hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(256), b.air_lds_bytes, st, b.words, b.desc, n, b.dims, b.air_nodes,
                        b.air_level_nodes, b.air_level_off, b.air_n_levels, b.air_cons, b.air_cons_off, b.xs, b.ood,
