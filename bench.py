@@ -1,19 +1,25 @@
 #!/usr/bin/env python3
-"""bench.py — BASELINE.json config 2 on MI355X: synthetic 2^20 Tip5 Merkle authentication
-paths of depth 20 per GPU, verified with MTree::verify semantics
-(neptune-core/src/protocol/consensus/block/pow.rs:162-180) by the hand-written HIP kernel
-behind include/neptune_hip.h.
+"""bench.py — batched STARK verification on MI355X (BASELINE.json metric: STARK proofs verified/s
++ Tip5 permutations/s vs the VALU roofline).
 
-One step = one batch pass of the hot path: verify every resident path
-(nhip_mtree_verify_dev), reduce the per-path verdicts to the batch verdict on the device
-(nhip_verdicts_all_dev) and, for N > 1, AND the batch verdicts of all ranks with one RCCL
-all-reduce(MIN) over xGMI (the path's only exchange step).  Paths are
-sharded by rank (weak scaling: every rank owns its own 2^20-path batch).
+Workload per GPU (BASELINE config 3): 256 synthetic ProofCollections x 8 member proofs with log2
+padded heights {16, 10, 11, 12, 12, 11, 9, 9} = 2,048 STARK verifications with Stark::default()
+parameters (security 160, expansion 4, 80 collinearity checks, 379 main / 88 aux columns, 4
+quotient segments), each through the full verifier: Fiat-Shamir replay, row hashing, Merkle
+multiproofs, out-of-domain AIR evaluation, FRI, DEEP.  5% of the collections carry one flipped word
+(in one member's MainRows payload) and must reject.  The proofs are one accepting synthetic proof per
+padded height from tests/golden/c3_pool.npz (made by tests/golden/make_bench_pool.py), each
+collection member stored separately in HBM.
 
-Inputs are resident in HBM before the timed region.  The rank-0/N=1 CPU baseline is the C
-restatement (oracle/tip5_oracle.c) on the host cores, timed on a bounded sample of the same
-workload (the reference `triton_vm`/twenty-first Rust code cannot be built here: no Rust
-toolchain, crates not vendored — SURVEY.md §8c).
+One step = one nhip_batch_run over the resident batch (every device phase + the verdict copy back)
+and, for N > 1, the batch verdict AND over ranks with one RCCL all-reduce(MIN) — the path's only
+exchange.  Every rank owns its own 2,048-proof batch (weak scaling).  Host decode +
+upload (nhip_batch_prepare) happens before the timed region and is reported separately.
+
+roofline: the dominant kernel, k_mp_hash (the per-level Merkle hash_pair launches), as Tip5
+VALU lane-ops/s against the gfx950 VALU peak; `tip5_paths` adds the config-2 Tip5 path microbench.
+cpu_baseline: the oracle verifier (oracle/stark_ref.py with Tip5 in C, oracle/tip5_oracle.c), one
+proof per process on the host cores, over a bounded sample of this batch's proofs.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -32,14 +38,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
 
 P = (1 << 64) - (1 << 32) + 1
+POOL = os.path.join(ROOT, "tests", "golden", "c3_pool.npz")
+COLLECTION_HEIGHTS = [16, 10, 11, 12, 12, 11, 9, 9]
 # Algorithmic VALU work of one Tip5 permutation in 32-bit VALU lane-ops: a fixed analytic count of
 # a minimal implementation: per round S-box 64 + x^7 672 + MDS 512+160 + ARK 96.
 TIP5_VALU_OPS_PER_PERM = 5 * 1504
 # gfx950: 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz (wave64 VALU issues over 2 cycles on SIMD-32)
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
-# algorithmic HBM bytes per path: leaf (40) + index (8) + depth siblings (40 each) + verdict (1)
-def path_bytes(depth: int) -> int:
-    return 40 + 8 + 40 * depth + 1
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
 
 
 def pmc_traffic(kernel: str):
@@ -60,12 +69,90 @@ def pmc_traffic(kernel: str):
         return None, None
 
 
-def log(*a):
-    print(*a, file=sys.stderr, flush=True)
+# ------------------------------------------------------------------ config 3 batch
+def load_pool():
+    z = np.load(POOL)  # plain arrays, allow_pickle=False
+    meta = json.loads(bytes(z["meta"]).decode())
+    pool = {}
+    for h in meta["heights"]:
+        c = meta["claims"][str(h)]
+        pool[h] = {"claim": (c["digest"], c["version"], c["input"], c["output"]),
+                   "proof": z[f"proof_{h}"], "main_rows": meta["main_rows"][str(h)]}
+    return z["air"], pool
 
 
-def make_batch(rng, log2_leaves: int, ctx, corrupt_frac: float):
-    """Synthetic tree on the device, paths gathered on the host, all uploaded once."""
+def make_batch(pool, collections: int, corrupt_frac: float, seed: int):
+    """(claims, proofs, expected verdicts): collections x 8 members, corrupt_frac of the collections
+    with one flipped word in one member's MainRows payload."""
+    rng = np.random.default_rng(seed)
+    n_bad = int(round(collections * corrupt_frac))
+    bad = set(rng.choice(collections, size=n_bad, replace=False).tolist()) if n_bad else set()
+    claims, proofs, expect = [], [], []
+    for c in range(collections):
+        victim = int(rng.integers(0, len(COLLECTION_HEIGHTS))) if c in bad else -1
+        for m, h in enumerate(COLLECTION_HEIGHTS):
+            e = pool[h]
+            proof = e["proof"]
+            ok = True
+            if m == victim:
+                proof = proof.copy()
+                lo, hi = e["main_rows"]
+                pos = int(rng.integers(lo, hi))
+                proof[pos] = np.uint64((int(proof[pos]) + 1) % P)
+                ok = False
+            claims.append(e["claim"])
+            proofs.append(proof)
+            expect.append(ok)
+    return claims, proofs, np.array(expect, dtype=bool)
+
+
+# ------------------------------------------------------------------ CPU baseline (oracle)
+_CPU = {}
+
+
+def _cpu_init(air_words):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import stark_ref as S  # oracle: CPU baseline leg only
+    import tip5_ref as T
+    T.use_c_backend()
+    _CPU["S"] = S
+    _CPU["params"] = S.StarkParams()
+    _CPU["air"] = S.AirCircuit.from_words([int(w) for w in air_words])
+
+
+def _cpu_verify(args):
+    claim, proof = args
+    S = _CPU["S"]
+    return bool(S.verify(_CPU["params"], _CPU["air"], claim, [int(w) for w in proof]))
+
+
+def cpu_baseline(air_words, claims, proofs, expect, target_s: float, procs: int):
+    """Oracle verifier, one proof per process (fork, before any GPU use), over a bounded prefix of the
+    batch (whole collections, so the padded-height mix is the batch's)."""
+    import multiprocessing as mp
+    ctxm = mp.get_context("fork")
+    with ctxm.Pool(procs, initializer=_cpu_init, initargs=(air_words,)) as pool:
+        # calibrate on one collection per process
+        m = 8 * procs
+        t = time.perf_counter()
+        pool.map(_cpu_verify, list(zip(claims[:m], proofs[:m])), chunksize=1)
+        dt = time.perf_counter() - t
+        m = min(len(proofs), max(m, int(m * target_s / max(dt, 1e-6)) // 8 * 8))
+        t = time.perf_counter()
+        v = pool.map(_cpu_verify, list(zip(claims[:m], proofs[:m])), chunksize=1)
+        dt = time.perf_counter() - t
+    assert list(v) == list(expect[:m]), "CPU baseline verdicts disagree with the expected verdicts"
+    return {"value": m / dt, "unit": "proofs/s", "cores": procs, "kind": "port",
+            "sample": f"the first {m} of this batch's {len(proofs)} proofs ({m // 8} whole collections), oracle "
+                      f"verifier oracle/stark_ref.py with Tip5 in C (oracle/tip5_oracle.c), {procs} processes, "
+                      f"{dt:.1f} s"}
+
+
+# ------------------------------------------------------------------ config 2 Tip5 path microbench
+def tip5_paths(ctx, log2_leaves: int, steps: int):
+    """2^log2_leaves depth-log2_leaves Merkle authentication paths (pow.rs:162-180), 1% corrupted;
+    Tip5 perms/s of k_mtree_verify and its VALU roofline fraction."""
+    rng = np.random.default_rng(0xC2)
     n = 1 << log2_leaves
     depth = log2_leaves
     leafs = rng.integers(0, P, size=(n, 5), dtype=np.uint64)
@@ -73,7 +160,7 @@ def make_batch(rng, log2_leaves: int, ctx, corrupt_frac: float):
     d_nodes = ctx.alloc(n * 40)
     ctx.mtree_build_dev(d_leafs, n, d_nodes)
     nodes = d_nodes.download(np.uint64, (n, 5))
-    idx = rng.permutation(n).astype(np.int64)  # paths in random leaf order
+    idx = rng.permutation(n).astype(np.int64)
     paths = np.empty((n, depth, 5), dtype=np.uint64)
     paths[:, 0] = leafs[idx ^ 1]
     running = idx + n
@@ -82,42 +169,29 @@ def make_batch(rng, log2_leaves: int, ctx, corrupt_frac: float):
         paths[:, k] = nodes[running ^ 1]
     elements = leafs[idx].copy()
     expect = np.ones(n, dtype=np.uint8)
-    n_bad = int(n * corrupt_frac)
-    if n_bad:
-        bad = rng.choice(n, size=n_bad, replace=False)
-        elements[bad, 0] = (elements[bad, 0] + np.uint64(1)) % np.uint64(P)
-        expect[bad] = 0
-    batch = {
-        "n": n, "depth": depth, "root": nodes[1].copy(), "idx": idx.astype(np.uint64),
-        "elements": elements, "paths": paths, "expect": expect,
-        "d_root": ctx.upload(nodes[1]), "d_idx": ctx.upload(idx.astype(np.uint64)),
-        "d_el": ctx.upload(elements), "d_paths": ctx.upload(paths), "d_v": ctx.alloc(n),
-    }
-    d_leafs.free()
-    d_nodes.free()
-    return batch
-
-
-def cpu_baseline(batch, target_s: float, threads: int):
-    """C restatement on the host cores over a bounded sample of the same paths."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import coracle as C  # oracle: CPU baseline leg only
-    depth = batch["depth"]
-    # calibrate on a small slice, then size the sample for ~target_s seconds
-    m = 2048
-    t = time.perf_counter()
-    C.mtree_verify_batch(batch["root"], batch["idx"][:m], batch["elements"][:m], batch["paths"][:m].reshape(-1),
-                         depth, nthreads=threads)
-    dt = time.perf_counter() - t
-    m = int(min(batch["n"], max(m, m * target_s / max(dt, 1e-6))))
-    t = time.perf_counter()
-    v = C.mtree_verify_batch(batch["root"], batch["idx"][:m], batch["elements"][:m],
-                             batch["paths"][:m].reshape(-1), depth, nthreads=threads)
-    dt = time.perf_counter() - t
-    assert (v == batch["expect"][:m]).all(), "CPU baseline verdicts disagree with the expected verdicts"
-    return {"value": m * depth / dt, "unit": "Tip5 perms/s", "cores": threads, "kind": "port",
-            "sample": f"{m} of the {batch['n']} depth-{depth} paths of this batch ({m * depth} permutations), "
-                      f"C restatement oracle/tip5_oracle.c, {threads} POSIX threads, {dt:.1f} s"}
+    bad = rng.choice(n, size=n // 100, replace=False)
+    elements[bad, 0] = (elements[bad, 0] + np.uint64(1)) % np.uint64(P)
+    expect[bad] = 0
+    d = {k: ctx.upload(v) for k, v in (("root", nodes[1]), ("idx", idx.astype(np.uint64)), ("el", elements),
+                                       ("paths", paths))}
+    d_v = ctx.alloc(n)
+    ctx.mtree_verify_dev(d["root"], 1, d["idx"], d["el"], d["paths"], depth, n, d_v)
+    ctx.synchronize()
+    ctx.timing_read(reset=True)
+    ctx.timing(True)
+    for _ in range(steps):
+        ctx.mtree_verify_dev(d["root"], 1, d["idx"], d["el"], d["paths"], depth, n, d_v)
+    ctx.timing(False)
+    ctx.synchronize()
+    kern_ms, launches = ctx.timing_read(reset=True)
+    ok = bool((d_v.download(np.uint8, (n,)) == expect).all())
+    for b in list(d.values()) + [d_leafs, d_nodes, d_v]:
+        b.free()
+    avg_s = kern_ms / max(launches, 1) / 1e3
+    perms_s = n * depth / avg_s
+    return {"workload": f"BASELINE config 2: 2^{log2_leaves} depth-{depth} Merkle auth paths, 1% corrupted",
+            "kernel": "k_mtree_verify", "kernel_avg_ms": avg_s * 1e3, "perms_per_s": perms_s,
+            "valu_frac": perms_s * TIP5_VALU_OPS_PER_PERM / VALU_PEAK_LANE_OPS, "verdicts_correct": ok}
 
 
 def main():
@@ -125,16 +199,27 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--log2-leaves", type=int, default=20)
-    ap.add_argument("--corrupt-frac", type=float, default=0.01)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--collections", type=int, default=256)
+    ap.add_argument("--corrupt-frac", type=float, default=0.05)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    air_words, pool = load_pool()
+    claims, proofs, expect = make_batch(pool, args.collections, args.corrupt_frac, 0xC3 + rank)
+    n = len(proofs)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        t = time.time()
+        cpu = cpu_baseline(air_words, claims, proofs, expect, args.cpu_seconds, args.cpu_procs)
+        log(f"[cpu] {cpu['value']:.1f} proofs/s ({time.time() - t:.1f}s)")
+
     dist = None
     if world > 1:
         import torch
@@ -142,24 +227,20 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")
     import neptune_hip as nh
-
-    ctx = nh.Context(local_rank)
-    rng = np.random.default_rng(0xC2 + rank)
-    t0 = time.time()
-    batch = make_batch(rng, args.log2_leaves, ctx, args.corrupt_frac)
-    n, depth = batch["n"], batch["depth"]
-    log(f"[rank {rank}] batch ready: {n} paths, depth {depth}, {time.time() - t0:.1f}s")
-
+    import neptune_hip.stark as NS
     from neptune_hip import shard
 
-    def step(timed: bool):
-        if timed:
-            ctx.timing(True)
-        ctx.mtree_verify_dev(batch["d_root"], 1, batch["d_idx"], batch["d_el"], batch["d_paths"], depth, n,
-                             batch["d_v"])
-        if timed:
-            ctx.timing(False)
-        ok = ctx.verdicts_all_dev(batch["d_v"], n)
+    ctx = nh.Context(local_rank)
+    t0 = time.time()
+    batch = NS.Batch(ctx, NS.Air([int(w) for w in air_words]), NS.Stark.default(),
+                     [NS.Claim(*c) for c in claims], proofs)
+    prep_s = time.time() - t0
+    st0 = batch.stats()
+    log(f"[rank {rank}] batch ready: {n} proofs, {st0['proof_words']} words, prepare {prep_s:.2f}s "
+        f"(decode {st0['ms_decode']:.0f} ms, upload {st0['ms_upload']:.0f} ms)")
+
+    def step():
+        _, ok = batch.run()
         if dist is not None:
             ok = shard.all_ok(ok, dist)  # the one exchange: RCCL all-reduce(MIN) of the batch verdict
         return ok
@@ -172,20 +253,20 @@ def main():
             dist.barrier()
 
     for _ in range(args.warmup):
-        step(False)
-    ctx.timing_read(reset=True)
+        step()
     barrier_sync()
-    t_start = time.perf_counter()
+    acc = {}
     batch_ok = None
+    t_start = time.perf_counter()
     for _ in range(args.steps):
-        batch_ok = step(True)
+        batch_ok = step()
+        for k, v in batch.stats().items():
+            acc[k] = acc.get(k, 0.0) + v
     barrier_sync()
     elapsed = time.perf_counter() - t_start
-    kern_ms, launches = ctx.timing_read(reset=True)
 
-    # correctness of the measured work: per-path verdicts equal the expected ones
-    v = batch["d_v"].download(np.uint8, (n,))
-    correct = bool((v == batch["expect"]).all())
+    v, _ = batch.run()
+    correct = bool((np.asarray(v, dtype=bool) == expect).all())
     if dist is not None:
         import torch
         t = torch.tensor([elapsed, 0.0 if correct else 1.0], dtype=torch.float64, device="cuda")
@@ -194,42 +275,56 @@ def main():
         correct = any_bad == 0.0
     if not correct:
         log("ERROR: verdicts differ from expected")
-    perms_per_step = world * n * depth
-    value = perms_per_step * args.steps / elapsed
-    kern_avg_s = kern_ms / max(launches, 1) / 1e3
-    achieved = n * depth * TIP5_VALU_OPS_PER_PERM / kern_avg_s
-    traffic, traffic_tag = pmc_traffic("k_mtree_verify")
+    K = args.steps
+    avg = {k: v / K for k, v in acc.items()}
+    perms = avg["tip5_perms_static"] + avg["tip5_perms_merkle"]
+    hash_ms = avg["ms_merkle_hash"]
+    launches = max(avg["merkle_hash_launches"], 1.0)
+    kern_avg_s = hash_ms / launches / 1e3
+    achieved = avg["tip5_perms_merkle"] / launches * TIP5_VALU_OPS_PER_PERM / kern_avg_s
+    traffic, traffic_tag = pmc_traffic("k_mp_hash")
     res = {
-        "metric": "Tip5 permutations/s verifying synthetic Merkle authentication paths (BASELINE config 2)",
-        "value": value,
-        "unit": "Tip5 perms/s",
+        "metric": "STARK proofs verified/s (BASELINE config 3 per GPU) + Tip5 perms/s vs VALU roofline",
+        "value": world * n * K / elapsed,
+        "unit": "proofs/s",
         "n_gpus": world,
-        "steps": args.steps,
+        "steps": K,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": elapsed / K * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u64 (Goldilocks mod p)",
-        "data": "synthetic (seeded uniform canonical leaves, one 2^20-leaf tree per rank, 1% corrupted leaves)",
-        "config": {"workload": f"BASELINE config 2: 2^{args.log2_leaves} Tip5 Merkle auth paths of depth {depth} per GPU "
-                               "(MTree::verify, pow.rs:162-180) + batch verdict AND (+ RCCL MIN all-reduce for N>1)",
-                   "paths_per_gpu": n, "depth": depth, "parallelism": f"path-sharded x{world}"},
-        "paths_per_s": world * n * args.steps / elapsed,
+        "dtype": "u64 (Goldilocks mod p; XFE = cubic extension)",
+        "data": "synthetic: one accepting proof per padded height (tests/golden/c3_pool.npz, synthetic AIR with "
+                "triton-vm column counts), 5% of collections with one flipped MainRows word",
+        "config": {"workload": f"BASELINE config 3: {args.collections} ProofCollections x 8 proofs (log2 padded "
+                               f"heights {COLLECTION_HEIGHTS}) = {n} STARK verifications per GPU, Stark::default()",
+                   "proofs_per_gpu": n, "collections_per_gpu": args.collections,
+                   "parallelism": f"proof-sharded x{world}"},
         "verdicts_correct": correct,
         "batch_verdict": batch_ok,
+        "expected_rejects_per_gpu": int((~expect).sum()),
+        "tip5_perms_per_proof": perms / n,
+        "tip5_perms_per_s": world * perms * K / elapsed,
+        "phase_ms": {k[3:]: round(avg[k], 4) for k in ("ms_fiat_shamir", "ms_row_hash", "ms_merkle",
+                                                        "ms_merkle_hash", "ms_ood_air", "ms_fri", "ms_deep",
+                                                        "ms_device_total")},
+        "host_prepare_ms": {"decode": st0["ms_decode"], "upload": st0["ms_upload"], "total": prep_s * 1e3},
         "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
                      "unit": "T VALU lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS, "traffic": traffic,
                      "traffic_unit": "bytes per launch (FETCH_SIZE+WRITE_SIZE, raw; see DESIGN.md §3)",
-                     "traffic_profile": traffic_tag,
-                     "kernel": "k_mtree_verify", "kernel_avg_ms": kern_avg_s * 1e3,
-                     "valu_ops_per_perm": TIP5_VALU_OPS_PER_PERM,
-                     "hbm_algorithmic_GBps": n * path_bytes(depth) / kern_avg_s / 1e9},
+                     "traffic_profile": traffic_tag, "kernel": "k_mp_hash",
+                     "kernel_avg_ms": kern_avg_s * 1e3, "launches_per_step": launches,
+                     "perms_per_launch": avg["tip5_perms_merkle"] / launches,
+                     "valu_ops_per_perm": TIP5_VALU_OPS_PER_PERM},
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(batch, args.cpu_seconds, args.cpu_threads)
+    if rank == 0 and args.paths_log2 > 0:
+        res["tip5_paths"] = tip5_paths(ctx, args.paths_log2, 5)
+    if cpu is not None:
+        res["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(res), flush=True)
+    batch.close()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

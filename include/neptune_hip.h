@@ -136,6 +136,8 @@ typedef struct {
     uint64_t tip5_perms_merkle;  /* authentication-structure hash_pairs actually performed (device-counted) */
     double ms_decode, ms_upload;  /* host */
     double ms_fiat_shamir, ms_row_hash, ms_merkle, ms_ood_air, ms_fri, ms_deep, ms_device_total; /* device */
+    double ms_merkle_hash;          /* the per-level hash_pair launches inside ms_merkle */
+    uint64_t merkle_hash_launches;  /* number of those launches (one per tree level) */
 } nhip_stats;
 
 typedef struct nhip_air nhip_air;

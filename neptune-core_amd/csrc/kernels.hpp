@@ -21,19 +21,22 @@ hipError_t launch_mtree_verify(const uint64_t* d_roots, int per_path_root, const
 static constexpr uint32_t AIR_LDS_HEADER = (256 + 4 + 4) * 24 + 16;  // red, zinv, derived, flag
 static constexpr uint32_t FRI_LDS_HEADER = 256 * 24 + 256 + 16;      // red, tip5 lut, flag
 
-// Level-synchronous Merkle multiproof plan (see k_mp_plan in stark_kernels.hip)
+// Level-synchronous Merkle multiproof plan (see k_mp_plan in stark_kernels.hip).  Ops of level l
+// live in MP_SHARDS shards (shard = proof index % MP_SHARDS) so the per-level slot reservations of
+// the plan workgroups spread over MP_SHARDS counters instead of contending on one.
+static constexpr uint32_t MP_SHARDS = 16;
 struct MpRoot {
     uint64_t code;  // source code of the tree's final node, ~0 = no check (skipped or already failed)
     uint64_t root_off;
     uint32_t fail_bit, pad;
 };
 struct MpPlan {
-    uint64_t* ops;               // 2 source codes per op, level-major: op g at level_base[l] + pos
-    uint64_t* arena;             // parent digest of op g (Montgomery), 5 words
-    const uint64_t* level_base;  // levels entries
-    const uint64_t* cap;         // op capacity per level
-    uint32_t* counter;           // ops appended per level (zeroed per run)
-    MpRoot* roots;               // n_proofs x (4 + max_R)
+    uint64_t* ops;                // 2 source codes per op
+    uint64_t* arena;              // parent digest of op g (Montgomery), 5 words
+    const uint64_t* shard_base;   // [levels][MP_SHARDS] first op index of the shard
+    const uint64_t* shard_cap;    // [levels][MP_SHARDS] op capacity of the shard
+    uint32_t* counter;            // [levels][MP_SHARDS] ops appended (zeroed per run)
+    MpRoot* roots;                // n_proofs x (4 + max_R)
     uint32_t levels;
 };
 
@@ -51,7 +54,7 @@ struct StarkBatchDev {
     uint8_t* verdicts;
     unsigned long long* perm_counter;  // Merkle hash_pairs performed (device-counted)
     MpPlan mp;
-    const uint64_t* mp_cap_host;  // host copy of mp.cap (launch sizes)
+    const uint64_t* mp_cap_host;  // host: op capacity per level (launch sizes)
     const AirNode* air_nodes;
     const uint32_t* air_level_nodes;
     const uint32_t* air_level_off;
@@ -61,8 +64,11 @@ struct StarkBatchDev {
     size_t air_lds_bytes, fri_lds_bytes;
 };
 
+// events: 0 start | fs | rows | mp plan | mp hash levels | mp roots | ood | fri | deep | 9 verdicts
+static constexpr int STARK_EVENTS = 10;
 struct StarkPhaseTimer {
-    hipEvent_t ev[8];
+    hipEvent_t ev[STARK_EVENTS];
+    uint32_t mp_hash_launches;
 };
 
 hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, StarkPhaseTimer* tm);

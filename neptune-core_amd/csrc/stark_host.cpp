@@ -364,7 +364,7 @@ struct nhip_batch {
     uint64_t* d_perm_counter = nullptr;
     StarkPhaseTimer tm{};
     bool timed = false;
-    double last_ms[8] = {};
+    double last_ms[STARK_EVENTS - 1] = {};
     double decode_ms = 0, upload_ms = 0;
     uint64_t merkle_perms = 0;
     std::vector<uint64_t> mp_cap;  // multiproof op capacity per level
@@ -578,23 +578,31 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
         attrs = true;
     }
     const uint32_t k = D.d.num_checks;
-    // multiproof op capacity per level: a tree of height h has at most min(k, 2^(h-1-l)) parents at level l
+    // multiproof op capacity per (level, shard): a tree of height h has at most min(k, 2^(h-1-l))
+    // parents at level l; shard = proof index % MP_SHARDS
     const uint32_t tpp = 4 + H.max_R;
     uint32_t levels = 0;
     for (size_t i = 0; i < n; ++i)
         if (!(H.fail[i] & FAIL_DECODE)) levels = std::max(levels, H.desc[i].log2_N);
+    std::vector<uint64_t> mp_scap((size_t)levels * MP_SHARDS, 0), mp_sbase((size_t)levels * MP_SHARDS, 0);
     b->mp_cap.assign(levels, 0);
     for (size_t i = 0; i < n; ++i) {
         if (H.fail[i] & FAIL_DECODE) continue;
         const ProofDesc& pd = H.desc[i];
+        const uint32_t sh = (uint32_t)(i % MP_SHARDS);
         for (uint32_t t = 0; t < 4 + pd.R; ++t) {
             const uint32_t h = t < 4 ? pd.log2_N : pd.log2_N - (t - 4);
-            for (uint32_t l = 0; l < h; ++l) b->mp_cap[l] += std::min<uint64_t>(k, 1ull << std::min(h - 1 - l, 40u));
+            for (uint32_t l = 0; l < h; ++l)
+                mp_scap[(size_t)l * MP_SHARDS + sh] += std::min<uint64_t>(k, 1ull << std::min(h - 1 - l, 40u));
         }
     }
-    std::vector<uint64_t> mp_base(levels + 1, 0);
-    for (uint32_t l = 0; l < levels; ++l) mp_base[l + 1] = mp_base[l] + b->mp_cap[l];
-    const uint64_t mp_total = mp_base[levels];
+    uint64_t mp_total = 0;
+    for (uint32_t l = 0; l < levels; ++l)
+        for (uint32_t q = 0; q < MP_SHARDS; ++q) {
+            mp_sbase[(size_t)l * MP_SHARDS + q] = mp_total;
+            mp_total += mp_scap[(size_t)l * MP_SHARDS + q];
+            b->mp_cap[l] += mp_scap[(size_t)l * MP_SHARDS + q];
+        }
     const size_t sz[] = {H.words.size() * 8 + 8,
                          std::max<size_t>(1, n) * sizeof(ProofDesc),
                          H.ops.size() * sizeof(FsOp) + 8,
@@ -608,9 +616,9 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
                          8,
                          mp_total * 16 + 16,
                          mp_total * 40 + 40,
-                         (size_t)levels * 8 + 8,
-                         (size_t)levels * 8 + 8,
-                         (size_t)levels * 4 + 4,
+                         (size_t)levels * MP_SHARDS * 8 + 8,
+                         (size_t)levels * MP_SHARDS * 8 + 8,
+                         (size_t)levels * MP_SHARDS * 4 + 4,
                          std::max<size_t>(1, n) * tpp * sizeof(MpRoot)};
     constexpr int NBUF = sizeof(sz) / sizeof(sz[0]);
     size_t total = 0;
@@ -632,8 +640,10 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     if (e == hipSuccess && !H.ops.empty())
         e = hipMemcpyAsync(ptr[2], H.ops.data(), H.ops.size() * sizeof(FsOp), hipMemcpyHostToDevice, st);
     if (e == hipSuccess && n) e = hipMemcpyAsync(ptr[8], H.fail.data(), n * 4, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess && levels) e = hipMemcpyAsync(ptr[13], mp_base.data(), levels * 8, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess && levels) e = hipMemcpyAsync(ptr[14], b->mp_cap.data(), levels * 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && levels)
+        e = hipMemcpyAsync(ptr[13], mp_sbase.data(), mp_sbase.size() * 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && levels)
+        e = hipMemcpyAsync(ptr[14], mp_scap.data(), mp_scap.size() * 8, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     auto t2 = std::chrono::steady_clock::now();
     b->upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
@@ -660,8 +670,8 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     dv.perm_counter = (unsigned long long*)ptr[10];
     dv.mp.ops = (uint64_t*)ptr[11];
     dv.mp.arena = (uint64_t*)ptr[12];
-    dv.mp.level_base = (const uint64_t*)ptr[13];
-    dv.mp.cap = (const uint64_t*)ptr[14];
+    dv.mp.shard_base = (const uint64_t*)ptr[13];
+    dv.mp.shard_cap = (const uint64_t*)ptr[14];
     dv.mp.counter = (uint32_t*)ptr[15];
     dv.mp.roots = (MpRoot*)ptr[16];
     dv.mp.levels = levels;
@@ -692,10 +702,10 @@ int nhip_batch_run(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* all
     hipError_t e = hipSuccess;
     if (n) e = hipMemcpyAsync(b->dev.fail, b->d_fail_init, n * 4, hipMemcpyDeviceToDevice, st);
     if (e == hipSuccess) e = hipMemsetAsync(b->d_perm_counter, 0, 8, st);
-    if (e == hipSuccess && b->dev.mp.levels) e = hipMemsetAsync(b->dev.mp.counter, 0, b->dev.mp.levels * 4, st);
+    if (e == hipSuccess && b->dev.mp.levels) e = hipMemsetAsync(b->dev.mp.counter, 0, (size_t)b->dev.mp.levels * MP_SHARDS * 4, st);
     if (e != hipSuccess) return hipfail(e);
     if (!b->timed) {
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < STARK_EVENTS; ++i)
             if (hipEventCreate(&b->tm.ev[i]) != hipSuccess) return NHIP_ERR_HIP;
         b->timed = true;
     }
@@ -706,7 +716,7 @@ int nhip_batch_run(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* all
     if (e == hipSuccess) e = hipMemcpyAsync(&b->merkle_perms, b->d_perm_counter, 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hipfail(e);
-    for (int i = 0; i < 7; ++i) {
+    for (int i = 0; i < STARK_EVENTS - 1; ++i) {
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, b->tm.ev[i], b->tm.ev[i + 1]);
         b->last_ms[i] = ms;
@@ -729,12 +739,14 @@ int nhip_batch_stats(const nhip_batch* b, nhip_stats* s) {
     s->ms_upload = b->upload_ms;
     s->ms_fiat_shamir = b->last_ms[0];
     s->ms_row_hash = b->last_ms[1];
-    s->ms_merkle = b->last_ms[2];
-    s->ms_ood_air = b->last_ms[3];
-    s->ms_fri = b->last_ms[4];
-    s->ms_deep = b->last_ms[5];
+    s->ms_merkle = b->last_ms[2] + b->last_ms[3] + b->last_ms[4];
+    s->ms_merkle_hash = b->last_ms[3];
+    s->merkle_hash_launches = b->tm.mp_hash_launches;
+    s->ms_ood_air = b->last_ms[5];
+    s->ms_fri = b->last_ms[6];
+    s->ms_deep = b->last_ms[7];
     s->ms_device_total = 0;
-    for (int i = 0; i < 7; ++i) s->ms_device_total += b->last_ms[i];
+    for (int i = 0; i < STARK_EVENTS - 1; ++i) s->ms_device_total += b->last_ms[i];
     s->tip5_perms_static = b->H.perms_static;
     s->tip5_perms_merkle = b->merkle_perms;
     return NHIP_OK;
@@ -770,7 +782,7 @@ void nhip_batch_destroy(nhip_batch* b) {
     if (!b) return;
     (void)hipSetDevice(b->device);
     if (b->timed)
-        for (int i = 0; i < 8; ++i) (void)hipEventDestroy(b->tm.ev[i]);
+        for (int i = 0; i < STARK_EVENTS; ++i) (void)hipEventDestroy(b->tm.ev[i]);
     if (b->dmem) (void)hipFree(b->dmem);
     delete b;
 }

@@ -210,12 +210,13 @@ __device__ __forceinline__ void hash_pair_raw(const uint64_t* l, const uint64_t*
 // 1 aux, 2 quotient, 3 FRI round-0 a-values, 4 + r FRI round-r b-values.
 //
 // Level-synchronous design: which nodes get hashed, and from which children, depends only on the
-// leaf indices and the authentication-structure length.  k_mp_plan (one workgroup per
-// (proof, tree)) sorts and dedupes the leaves and climbs the tree on indices alone, appending one
-// hash op per parent node to a global per-level op list (slot reserved with one atomic per
-// workgroup and level).  k_mp_hash then runs once per level over ALL trees of ALL proofs (one lane
-// per op, full waves regardless of tree shape), and k_mp_roots compares each tree's final node with
-// its committed root.  Child digests are referenced by 64-bit source codes (type in the top 2 bits).
+// leaf indices and the authentication-structure length.  k_mp_plan sorts and dedupes the leaves
+// and climbs the tree on indices alone, appending one hash op per parent node to a global
+// per-level op list; k_mp_hash then runs once per level over ALL trees of ALL proofs (one lane per
+// op: full waves whatever the tree shapes), and k_mp_roots compares every tree's final node with
+// its committed root.  Trees 0-3 open the same leaf indices at the same height, so one plan
+// workgroup (grid.y = 0) serves all four; grid.y = 1 + r plans FRI b-tree r.  Child digests are
+// referenced by 64-bit source codes (type in the top 2 bits).
 enum : uint64_t { MPS_ARENA = 0, MPS_AUTH = 1, MPS_DIG = 2, MPS_XFE = 3 };
 static constexpr uint64_t MPS_MASK = (1ull << 62) - 1, MPS_NONE = ~0ull;
 __device__ __forceinline__ uint64_t mps(uint64_t type, uint64_t v) { return (type << 62) | v; }
@@ -239,31 +240,40 @@ __device__ __forceinline__ void mp_load(uint64_t code, const uint64_t* __restric
     }
 }
 
-// exclusive prefix count of `pred` over the workgroup (<= 4 waves); returns the total
-__device__ __forceinline__ uint32_t wg_count_scan(bool pred, uint32_t& excl, uint32_t* sh) {
+// exclusive prefix counts of two predicates over the workgroup (<= 4 waves), one barrier pair
+__device__ __forceinline__ void wg_count_scan2(bool p0, bool p1, uint32_t& e0, uint32_t& e1, uint32_t& t0,
+                                               uint32_t& t1, uint32_t* sh) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6, nw = blockDim.x >> 6;
-    const uint64_t b = __ballot(pred);
-    const uint32_t in_wave = (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
-    if (lane == 0) sh[w] = (uint32_t)__popcll(b);
-    __syncthreads();
-    uint32_t base = 0, total = 0;
-    for (uint32_t q = 0; q < nw; ++q) {
-        const uint32_t c = sh[q];
-        base += q < w ? c : 0u;
-        total += c;
+    const uint64_t b0 = __ballot(p0), b1 = __ballot(p1);
+    const uint64_t below = (1ull << lane) - 1ull;
+    if (lane == 0) {
+        sh[w] = (uint32_t)__popcll(b0);
+        sh[4 + w] = (uint32_t)__popcll(b1);
     }
     __syncthreads();
-    excl = base + in_wave;
-    return total;
+    uint32_t s0 = 0, s1 = 0;
+    t0 = 0;
+    t1 = 0;
+    for (uint32_t q = 0; q < nw; ++q) {
+        const uint32_t c0 = sh[q], c1 = sh[4 + q];
+        s0 += q < w ? c0 : 0u;
+        s1 += q < w ? c1 : 0u;
+        t0 += c0;
+        t1 += c1;
+    }
+    __syncthreads();
+    e0 = s0 + (uint32_t)__popcll(b0 & below);
+    e1 = s1 + (uint32_t)__popcll(b1 & below);
 }
 
 template <int B>
 struct MpPlanLds {
     uint32_t key[2][B];
-    uint64_t src[2][B];
+    uint64_t src[2][4][B];
     uint32_t order[B];
-    uint32_t scan[4];
-    uint32_t flag, base;
+    uint32_t scan[8];
+    uint32_t bad;  // bit t: tree t failed (dedupe mismatch, authentication structure too short)
+    uint32_t base;
 };
 
 template <int B>
@@ -273,47 +283,45 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
                                                MpPlan plan, uint32_t* __restrict__ fail,
                                                unsigned long long* __restrict__ perm_counter) {
     __shared__ MpPlanLds<B> L;
-    const uint32_t p = blockIdx.x, tree = blockIdx.y, tid = threadIdx.x;
+    const uint32_t p = blockIdx.x, grp = blockIdx.y, tid = threadIdx.x;
     if (p >= n_proofs) return;
-    MpRoot* rec = plan.roots + (uint64_t)p * trees_per_proof + tree;
-    if (tid == 0) rec->code = MPS_NONE;
     const ProofDesc& d = desc[p];
+    const uint32_t NT = grp == 0 ? 4u : 1u;
+    const uint32_t tree0 = grp == 0 ? 0u : 3u + grp;  // tree id of this group's first tree
+    if (tid < NT) plan.roots[(uint64_t)p * trees_per_proof + tree0 + tid].code = MPS_NONE;
     if (fail[p] & FAIL_DECODE) return;
-    if (tree >= 4 + d.R) return;
-    uint32_t h, auth_n, fail_bit;
-    uint64_t root_off, auth_off;
-    if (tree < 3) {
+    if (grp > d.R) return;
+    uint32_t h, auth_n[4], fail_bit[4];
+    uint64_t root_off[4], auth_off[4];
+    if (grp == 0) {
         h = d.log2_N;
-        root_off = tree == 0 ? d.main_root : (tree == 1 ? d.aux_root : d.quot_root);
-        auth_off = tree == 0 ? d.main_auth_off : (tree == 1 ? d.aux_auth_off : d.quot_auth_off);
-        auth_n = tree == 0 ? d.main_auth_n : (tree == 1 ? d.aux_auth_n : d.quot_auth_n);
-        fail_bit = tree == 0 ? FAIL_MERKLE_MAIN : (tree == 1 ? FAIL_MERKLE_AUX : FAIL_MERKLE_QUOT);
+        root_off[0] = d.main_root, root_off[1] = d.aux_root, root_off[2] = d.quot_root, root_off[3] = d.fri_root[0];
+        auth_off[0] = d.main_auth_off, auth_off[1] = d.aux_auth_off, auth_off[2] = d.quot_auth_off;
+        auth_off[3] = d.fri[0].auth_off;
+        auth_n[0] = d.main_auth_n, auth_n[1] = d.aux_auth_n, auth_n[2] = d.quot_auth_n, auth_n[3] = d.fri[0].auth_n;
+        fail_bit[0] = FAIL_MERKLE_MAIN, fail_bit[1] = FAIL_MERKLE_AUX, fail_bit[2] = FAIL_MERKLE_QUOT;
+        fail_bit[3] = FAIL_MERKLE_FRI;
     } else {
-        const uint32_t r = tree == 3 ? 0u : tree - 4;
+        const uint32_t r = grp - 1;
         h = d.log2_N - r;
-        root_off = d.fri_root[r];
-        const FriResp& fr = d.fri[tree == 3 ? 0 : 1 + r];
-        auth_off = fr.auth_off;
-        auth_n = fr.auth_n;
-        fail_bit = FAIL_MERKLE_FRI;
+        root_off[0] = d.fri_root[r];
+        auth_off[0] = d.fri[1 + r].auth_off;
+        auth_n[0] = d.fri[1 + r].auth_n;
+        fail_bit[0] = FAIL_MERKLE_FRI;
     }
+    const uint32_t shard = p % MP_SHARDS;
     const uint32_t* __restrict__ idx = idx_all + d.idx_off;
     // ---- leaves (key = node index = leaf index + 2^h; 0 = empty slot)
     uint32_t key = 0u;
-    uint64_t code = MPS_NONE;
     if (tid < k) {
         const uint64_t nl = 1ull << h;
-        uint64_t li = idx[tid];
-        if (tree == 3) li = li % nl;
-        if (tree >= 4) li = (li + nl / 2) % nl;
+        uint64_t li = idx[tid] % nl;
+        if (grp > 0) li = (li + nl / 2) % nl;
         key = (uint32_t)(li + nl);
-        code = tree < 3 ? mps(MPS_DIG, ((uint64_t)p * 3 + tree) * k + tid)
-                        : mps(MPS_XFE, (tree == 3 ? d.fri[0].leaves_off : d.fri[tree - 3].leaves_off) + 3ull * tid);
     }
     L.key[0][tid] = key;
-    L.src[1][tid] = code;
     L.order[tid] = tid;
-    if (tid == 0) L.flag = 0;
+    if (tid == 0) L.bad = 0;
     __syncthreads();
     // ---- bitonic sort (descending) of (key, original slot)
     for (uint32_t size = 2; size <= (uint32_t)B; size <<= 1) {
@@ -334,29 +342,44 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
         }
     }
     const uint32_t skey = L.key[0][tid];
-    const uint64_t scode = L.src[1][L.order[tid]];
-    // dedupe: equal keys must carry equal digests
+    const uint32_t slot = L.order[tid];
+    uint64_t scode[4];
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t) {
+        const uint32_t tree = tree0 + t;
+        scode[t] = tree < 3 ? mps(MPS_DIG, ((uint64_t)p * 3 + tree) * k + slot)
+                            : mps(MPS_XFE, d.fri[tree == 3 ? 0 : tree - 3].leaves_off + 3ull * slot);
+    }
+    // dedupe: equal keys must carry equal digests (per tree)
     bool dup = false;
     if (skey != 0 && tid > 0 && L.key[0][tid - 1] == skey) {
         dup = true;
-        uint64_t a[5], b[5];
-        mp_load(scode, words, dig, nullptr, a);
-        mp_load(L.src[1][L.order[tid - 1]], words, dig, nullptr, b);
-        bool same = true;
+        const uint32_t slot2 = L.order[tid - 1];
+        for (uint32_t t = 0; t < NT; ++t) {
+            const uint32_t tree = tree0 + t;
+            const uint64_t c2 = tree < 3 ? mps(MPS_DIG, ((uint64_t)p * 3 + tree) * k + slot2)
+                                         : mps(MPS_XFE, d.fri[tree == 3 ? 0 : tree - 3].leaves_off + 3ull * slot2);
+            uint64_t a[5], b[5];
+            mp_load(scode[t], words, dig, nullptr, a);
+            mp_load(c2, words, dig, nullptr, b);
+            bool same = true;
 #pragma unroll
-        for (int q = 0; q < 5; ++q) same &= a[q] == b[q];
-        if (!same) atomicOr(&L.flag, 1u);
+            for (int q = 0; q < 5; ++q) same &= a[q] == b[q];
+            if (!same) atomicOr(&L.bad, 1u << t);
+        }
     }
     const bool keep = skey != 0 && !dup;
-    uint32_t pos;
-    uint32_t m = wg_count_scan(keep, pos, L.scan);
+    uint32_t pos, unused_e, m, unused_t;
+    wg_count_scan2(keep, false, pos, unused_e, m, unused_t, L.scan);
     if (keep) {
         L.key[0][pos] = skey;
-        L.src[0][pos] = scode;
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) L.src[0][t][pos] = scode[t];
     }
     __syncthreads();
-    // ---- climb on indices; emit one op per parent
-    uint32_t ap = 0, hashed = 0;
+    // ---- climb on indices; emit one op per parent node and tree
+    uint32_t ap = 0;
+    unsigned long long hashed = 0;
     int cur = 0;
     for (uint32_t lvl = 0; lvl < h; ++lvl) {
         const uint32_t i = tid;
@@ -369,64 +392,89 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
             unpaired = !pair_prev && !pair_next;
             owner = !pair_prev;
         }
-        uint32_t upos, opos;
-        const uint32_t n_unp = wg_count_scan(unpaired, upos, L.scan);
-        const uint32_t n_own = wg_count_scan(owner, opos, L.scan);
-        if (tid == 0) L.base = n_own ? atomicAdd(plan.counter + lvl, n_own) : 0u;
+        uint32_t upos, opos, n_unp, n_own;
+        wg_count_scan2(unpaired, owner, upos, opos, n_unp, n_own, L.scan);
+        uint32_t bad = L.bad;
+        for (uint32_t t = 0; t < NT; ++t)
+            if (ap + n_unp > auth_n[t]) bad |= 1u << t;  // authentication structure too short
+        const uint64_t sidx = (uint64_t)lvl * MP_SHARDS + shard;
+        if (tid == 0) L.base = atomicAdd(plan.counter + sidx, NT * n_own);
         __syncthreads();
         const uint32_t base = L.base;
-        if (ap + n_unp > auth_n || lvl >= plan.levels || (uint64_t)base + n_own > plan.cap[lvl]) {
-            if (tid == 0) L.flag = 1u;
-            break;  // uniform: every lane takes it
+        if (lvl >= plan.levels || (uint64_t)base + NT * n_own > plan.shard_cap[sidx]) {
+            bad = 0xFu;  // capacity guard (cannot trigger with the host's bounds)
+            if (tid == 0) L.bad = bad;
+            break;  // uniform
         }
         if (owner) {
-            const uint64_t mine = L.src[cur][i];
-            uint64_t lc, rc;
-            if (pair_next) {  // i holds 2q+1, i+1 holds 2q
-                lc = L.src[cur][i + 1];
-                rc = mine;
-            } else {
-                const uint64_t sib = mps(MPS_AUTH, auth_off + 5ull * (ap + upos));
-                const bool odd = (ki & 1u) != 0;
-                lc = odd ? sib : mine;
-                rc = odd ? mine : sib;
+            const uint64_t g0 = plan.shard_base[sidx] + base + opos;
+            for (uint32_t t = 0; t < NT; ++t) {
+                const uint64_t g = g0 + (uint64_t)t * n_own;
+                uint64_t lc = MPS_NONE, rc = MPS_NONE;
+                if (!((bad >> t) & 1u)) {
+                    const uint64_t mine = L.src[cur][t][i];
+                    if (pair_next) {  // i holds 2q+1, i+1 holds 2q
+                        lc = L.src[cur][t][i + 1];
+                        rc = mine;
+                    } else {
+                        const uint64_t sib = mps(MPS_AUTH, auth_off[t] + 5ull * (ap + upos));
+                        const bool odd = (ki & 1u) != 0;
+                        lc = odd ? sib : mine;
+                        rc = odd ? mine : sib;
+                    }
+                }
+                plan.ops[2 * g] = lc;
+                plan.ops[2 * g + 1] = rc;
+                L.src[cur ^ 1][t][opos] = mps(MPS_ARENA, g);
             }
-            const uint64_t g = plan.level_base[lvl] + base + opos;
-            plan.ops[2 * g] = lc;
-            plan.ops[2 * g + 1] = rc;
             L.key[cur ^ 1][opos] = ki >> 1;
-            L.src[cur ^ 1][opos] = mps(MPS_ARENA, g);
         }
+        for (uint32_t t = 0; t < NT; ++t) hashed += ((bad >> t) & 1u) ? 0u : n_own;
+        if (tid == 0) L.bad = bad;
         ap += n_unp;
         m = n_own;
-        hashed += n_own;
         cur ^= 1;
         __syncthreads();
     }
     __syncthreads();
-    if (tid == 0) {
-        const bool ok = L.flag == 0 && m == 1 && L.key[cur][0] == 1u && ap == auth_n;
+    if (tid < NT) {
+        const uint32_t t = tid;
+        const bool ok = !((L.bad >> t) & 1u) && m == 1 && L.key[cur][0] == 1u && ap == auth_n[t];
+        MpRoot* rec = plan.roots + (uint64_t)p * trees_per_proof + tree0 + t;
         if (ok) {
-            rec->code = L.src[cur][0];
-            rec->root_off = root_off;
-            rec->fail_bit = fail_bit;
+            rec->code = L.src[cur][t][0];
+            rec->root_off = root_off[t];
+            rec->fail_bit = fail_bit[t];
         } else {
-            atomicOr(&fail[p], fail_bit);
+            atomicOr(&fail[p], fail_bit[t]);
         }
-        if (perm_counter) atomicAdd(perm_counter, (unsigned long long)hashed);
     }
+    if (tid == 0 && perm_counter) atomicAdd(perm_counter, hashed);
 }
 
 __global__ void __launch_bounds__(256) k_mp_hash(const uint64_t* __restrict__ words, const uint64_t* __restrict__ dig,
                                                  MpPlan plan, uint32_t lvl) {
     __shared__ Tip5Lds t5;
-    tip5_lds_init(t5);
-    const uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pos >= plan.counter[lvl]) return;
-    const uint64_t g = plan.level_base[lvl] + pos;
+    __shared__ uint64_t s_base[MP_SHARDS + 1];
+    __shared__ uint32_t s_cnt[MP_SHARDS];
+    if (threadIdx.x < MP_SHARDS) {
+        s_base[threadIdx.x] = plan.shard_base[lvl * MP_SHARDS + threadIdx.x];
+        s_cnt[threadIdx.x] = plan.counter[lvl * MP_SHARDS + threadIdx.x];
+    }
+    if (threadIdx.x == 0)
+        s_base[MP_SHARDS] = plan.shard_base[(lvl + 1) * MP_SHARDS - 1] + plan.shard_cap[(lvl + 1) * MP_SHARDS - 1];
+    tip5_lds_init(t5);  // includes the barrier
+    const uint64_t g = s_base[0] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= s_base[MP_SHARDS]) return;
+    uint32_t sh = 0;
+#pragma unroll
+    for (uint32_t q = 1; q < MP_SHARDS; ++q) sh += g >= s_base[q] ? 1u : 0u;
+    if (g - s_base[sh] >= s_cnt[sh]) return;
+    const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
+    if (lc == MPS_NONE) return;  // op of a tree that already failed
     uint64_t s[16];
-    mp_load(plan.ops[2 * g], words, dig, plan.arena, s);
-    mp_load(plan.ops[2 * g + 1], words, dig, plan.arena, s + 5);
+    mp_load(lc, words, dig, plan.arena, s);
+    mp_load(rc, words, dig, plan.arena, s + 5);
 #pragma unroll
     for (int q = 10; q < 16; ++q) s[q] = MONT_ONE;
     tip5_permute_raw(s, t5.lut);
@@ -819,32 +867,37 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, StarkPhas
     {
         const uint32_t tpp = 4 + b.max_R;
         if (k <= 128)
-            hipLaunchKernelGGL(k_mp_plan<128>, dim3(n, tpp), dim3(128), 0, st, b.words, b.desc, n, k, tpp, b.dig, b.idx,
+            hipLaunchKernelGGL(k_mp_plan<128>, dim3(n, 1 + b.max_R), dim3(128), 0, st, b.words, b.desc, n, k, tpp, b.dig, b.idx,
                                b.mp, b.fail, b.perm_counter);
         else
-            hipLaunchKernelGGL(k_mp_plan<256>, dim3(n, tpp), dim3(256), 0, st, b.words, b.desc, n, k, tpp, b.dig, b.idx,
+            hipLaunchKernelGGL(k_mp_plan<256>, dim3(n, 1 + b.max_R), dim3(256), 0, st, b.words, b.desc, n, k, tpp, b.dig, b.idx,
                                b.mp, b.fail, b.perm_counter);
+        mark(3);
+        uint32_t launches = 0;
         for (uint32_t l = 0; l < b.mp.levels; ++l) {
             const uint64_t cap = b.mp_cap_host[l];
             if (cap == 0) continue;
             hipLaunchKernelGGL(k_mp_hash, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, b.words, b.dig, b.mp, l);
+            ++launches;
         }
+        if (tm) tm->mp_hash_launches = launches;
+        mark(4);
         const uint32_t nrec = n * tpp;
         hipLaunchKernelGGL(k_mp_roots, dim3((nrec + 255) / 256), dim3(256), 0, st, b.words, b.dig, b.mp, nrec, tpp,
                            b.fail);
     }
-    mark(3);
+    mark(5);
     hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(256), b.air_lds_bytes, st, b.words, b.desc, n, b.dims, b.air_nodes,
                        b.air_level_nodes, b.air_level_off, b.air_n_levels, b.air_cons, b.air_cons_off, b.xs, b.ood,
                        b.fail);
-    mark(4);
+    mark(6);
     hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), b.fri_lds_bytes, st, b.words, b.desc, n, b.dims, b.xs, b.idx,
                        b.fail);
-    mark(5);
-    hipLaunchKernelGGL(k_deep, dim3(n), dim3(256), 0, st, b.words, b.desc, n, b.dims, b.xs, b.idx, b.ood, b.fail);
-    mark(6);
-    hipLaunchKernelGGL(k_verdicts, dim3((n + 255) / 256), dim3(256), 0, st, b.fail, n, b.verdicts);
     mark(7);
+    hipLaunchKernelGGL(k_deep, dim3(n), dim3(256), 0, st, b.words, b.desc, n, b.dims, b.xs, b.idx, b.ood, b.fail);
+    mark(8);
+    hipLaunchKernelGGL(k_verdicts, dim3((n + 255) / 256), dim3(256), 0, st, b.fail, n, b.verdicts);
+    mark(9);
     return hipGetLastError();
 }
 

@@ -46,7 +46,8 @@ class Stats(ctypes.Structure):
                 ("ms_upload", ctypes.c_double), ("ms_fiat_shamir", ctypes.c_double),
                 ("ms_row_hash", ctypes.c_double), ("ms_merkle", ctypes.c_double),
                 ("ms_ood_air", ctypes.c_double), ("ms_fri", ctypes.c_double), ("ms_deep", ctypes.c_double),
-                ("ms_device_total", ctypes.c_double)]
+                ("ms_device_total", ctypes.c_double), ("ms_merkle_hash", ctypes.c_double),
+                ("merkle_hash_launches", ctypes.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -134,10 +134,14 @@ class Batch:
         n = min(nx.value, max_xfe)
         return [tuple(int(v) for v in xs[3 * j:3 * j + 3]) for j in range(n)], list(idx), fail.value
 
+    def close(self):
+        if self.handle:
+            self.ctx.lib.nhip_batch_destroy(self.handle)
+            self.handle = None
+
     def __del__(self):
         try:
-            if self.handle:
-                self.ctx.lib.nhip_batch_destroy(self.handle)
+            self.close()
         except Exception:
             pass
 

@@ -47,6 +47,23 @@ def lib():
     return L
 
 
+_perm_buf = (ctypes.c_uint64 * 16)()
+_perm_fn = None
+
+
+def permutation_list(state):
+    """One Tip5 permutation of a 16-element list (canonical in / out) through the C restatement;
+    the drop-in for tip5_ref.permutation installed by tip5_ref.use_c_backend()."""
+    global _perm_fn
+    if _perm_fn is None:
+        f = lib().oracle_tip5_permutation
+        _perm_fn = ctypes.CFUNCTYPE(None, ctypes.c_void_p)(ctypes.cast(f, ctypes.c_void_p).value)
+    for i in range(16):
+        _perm_buf[i] = state[i] % 0xFFFFFFFF00000001
+    _perm_fn(ctypes.addressof(_perm_buf))
+    return list(_perm_buf)
+
+
 def permutation_batch(states: np.ndarray) -> np.ndarray:
     L = lib()
     out = np.ascontiguousarray(states, dtype=np.uint64).copy()

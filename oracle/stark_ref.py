@@ -376,6 +376,22 @@ class AirCircuit:
     def num_challenges(self):
         return self.num_sampled + 3
 
+    @classmethod
+    def from_words(cls, w: Sequence[int]) -> "AirCircuit":
+        """Inverse of to_words (the AIR descriptor format)."""
+        assert w[0] == 0x41495231, "bad AIR magic"
+        num_main, num_aux, num_sampled, n_nodes = w[1], w[2], w[3], w[4]
+        counts = w[5:9]
+        pos = 9
+        nodes = [tuple(w[pos + 4 * i:pos + 4 * i + 4]) for i in range(n_nodes)]
+        pos += 4 * n_nodes
+        cons = []
+        for c in counts:
+            cons.append(list(w[pos:pos + c]))
+            pos += c
+        assert pos == len(w), "trailing AIR words"
+        return cls(num_main, num_aux, num_sampled, nodes, cons)
+
     def to_words(self) -> List[int]:
         w = [0x41495231, self.num_main, self.num_aux, self.num_sampled, len(self.nodes)] + \
             [len(c) for c in self.constraints]

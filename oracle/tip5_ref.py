@@ -99,6 +99,15 @@ def permutation(state: Sequence[int]) -> List[int]:
     return s
 
 
+def use_c_backend():
+    """Route every permutation of this module (sponge, hash_pair, hash_varlen) through the C
+    restatement oracle/tip5_oracle.c (itself checked against this file and the KATs in
+    tests/test_oracle_kat.py); used to time the CPU baseline at realistic speed."""
+    global permutation
+    import coracle
+    permutation = coracle.permutation_list
+
+
 # ---------------------------------------------------------------- sponge
 class Tip5:
     """Sponge with the two domains of twenty-first's Tip5."""

@@ -166,3 +166,39 @@ def test_full_size_targeted_mutations(ctx, full):
     assert got == [False] * len(muts) + [True], dict(zip(list(targets) + ["clean"], got))
     for m in muts[:3]:
         assert S.verify(params, air, claim, m) is False
+
+
+def test_bench_pool_heights_9_to_16_match_oracle(ctx):
+    """The BASELINE config-3 proof pool (log2 padded heights 9..12 and 16, Stark::default()):
+    GPU verdicts and full Fiat-Shamir transcripts equal the oracle's; a flipped MainRows word in
+    each rejects on both."""
+    import json as _json
+    T.use_c_backend()
+    NS = _ns()
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "c3_pool.npz"))
+    meta = _json.loads(bytes(z["meta"]).decode())
+    air_w = [int(w) for w in z["air"]]
+    air = S.AirCircuit.from_words(air_w)
+    params = S.StarkParams()
+    gair = NS.Air(air_w)
+    cases, bad = [], []
+    for h in meta["heights"]:
+        c = meta["claims"][str(h)]
+        claim = (c["digest"], c["version"], c["input"], c["output"])
+        proof = [int(w) for w in z[f"proof_{h}"]]
+        cases.append((claim, proof))
+        lo, hi = meta["main_rows"][str(h)]
+        m = list(proof)
+        m[(lo + hi) // 2] = (m[(lo + hi) // 2] + 1) % S.P
+        bad.append((claim, m))
+    b = NS.Batch(ctx, gair, NS.Stark.default(), [NS.Claim(*c) for c, _ in cases + bad], [p for _, p in cases + bad])
+    v, ok = b.run()
+    assert list(v) == [1] * len(cases) + [0] * len(bad) and not ok
+    for i, (claim, proof) in enumerate(cases):
+        ok_o, samples, indices = _oracle_samples(params, air, claim, proof)
+        assert ok_o
+        xs, idx, fail = b.transcript(i)
+        assert fail == 0 and xs == samples and idx == indices
+    for claim, m in bad[:2]:
+        assert S.verify(params, air, claim, m) is False
+    b.close()
