@@ -37,6 +37,8 @@ struct MpPlan {
     const uint64_t* shard_cap;    // [levels][MP_SHARDS] op capacity of the shard
     uint32_t* counter;            // [levels][MP_SHARDS] ops appended (zeroed per run)
     MpRoot* roots;                // n_proofs x (4 + max_R)
+    uint32_t* dups;               // [n_proofs][1 + max_R][k] (slot, earlier slot) pairs of equal leaf indices
+    uint32_t* ndup;               // [n_proofs][1 + max_R]
     uint32_t levels;
 };
 
@@ -71,7 +73,9 @@ struct StarkPhaseTimer {
     uint32_t mp_hash_launches;
 };
 
-hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, StarkPhaseTimer* tm);
+// Phases on two streams: st_aux runs the latency-bound chain (Fiat-Shamir -> Merkle plan -> OOD ->
+// FRI -> DEEP), st the VALU-bound hashing (rows -> per-level Merkle hashes -> roots -> verdicts).
+hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream_t st_aux, StarkPhaseTimer* tm);
 hipError_t stark_set_kernel_attributes();
 
 }  // namespace nhip

@@ -363,8 +363,11 @@ struct nhip_batch {
     uint32_t* d_fail_init = nullptr;
     uint64_t* d_perm_counter = nullptr;
     StarkPhaseTimer tm{};
+    hipStream_t aux = nullptr;  // second stream of the batch (latency-bound phase chain)
     bool timed = false;
-    double last_ms[STARK_EVENTS - 1] = {};
+    struct {
+        double fs, rows, plan, hash, roots, ood, fri, deep, total;
+    } ph{};
     double decode_ms = 0, upload_ms = 0;
     uint64_t merkle_perms = 0;
     std::vector<uint64_t> mp_cap;  // multiproof op capacity per level
@@ -619,7 +622,9 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
                          (size_t)levels * MP_SHARDS * 8 + 8,
                          (size_t)levels * MP_SHARDS * 8 + 8,
                          (size_t)levels * MP_SHARDS * 4 + 4,
-                         std::max<size_t>(1, n) * tpp * sizeof(MpRoot)};
+                         std::max<size_t>(1, n) * tpp * sizeof(MpRoot),
+                         std::max<size_t>(1, n) * (1 + H.max_R) * k * 8,
+                         std::max<size_t>(1, n) * (1 + H.max_R) * 4};
     constexpr int NBUF = sizeof(sz) / sizeof(sz[0]);
     size_t total = 0;
     for (size_t s : sz) total += al(s);
@@ -674,6 +679,8 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     dv.mp.shard_cap = (const uint64_t*)ptr[14];
     dv.mp.counter = (uint32_t*)ptr[15];
     dv.mp.roots = (MpRoot*)ptr[16];
+    dv.mp.dups = (uint32_t*)ptr[17];
+    dv.mp.ndup = (uint32_t*)ptr[18];
     dv.mp.levels = levels;
     dv.mp_cap_host = b->mp_cap.data();
     dv.air_nodes = air->d_nodes;
@@ -707,20 +714,31 @@ int nhip_batch_run(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* all
     if (!b->timed) {
         for (int i = 0; i < STARK_EVENTS; ++i)
             if (hipEventCreate(&b->tm.ev[i]) != hipSuccess) return NHIP_ERR_HIP;
+        if (hipStreamCreateWithFlags(&b->aux, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
         b->timed = true;
     }
-    e = launch_stark_phases(b->dev, st, &b->tm);
+    e = launch_stark_phases(b->dev, st, b->aux, &b->tm);
     if (e != hipSuccess) return hipfail(e);
     std::vector<uint8_t> v(n);
     if (n) e = hipMemcpyAsync(v.data(), b->dev.verdicts, n, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMemcpyAsync(&b->merkle_perms, b->d_perm_counter, 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hipfail(e);
-    for (int i = 0; i < STARK_EVENTS - 1; ++i) {
+    // phases overlap (two streams): each is timed from the event its inputs wait on
+    auto el = [&](int a, int c) {
         float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, b->tm.ev[i], b->tm.ev[i + 1]);
-        b->last_ms[i] = ms;
-    }
+        (void)hipEventElapsedTime(&ms, b->tm.ev[a], b->tm.ev[c]);
+        return (double)ms;
+    };
+    b->ph.fs = el(0, 1);
+    b->ph.rows = el(0, 2);
+    b->ph.plan = el(1, 3);
+    b->ph.hash = std::min(el(2, 4), el(3, 4));
+    b->ph.roots = el(4, 5);
+    b->ph.ood = el(3, 6);
+    b->ph.fri = el(6, 7);
+    b->ph.deep = el(7, 8);
+    b->ph.total = el(0, 9);
     if (verdicts && n) std::memcpy(verdicts, v.data(), n);
     if (all_ok) {
         uint8_t a = 1;
@@ -737,16 +755,16 @@ int nhip_batch_stats(const nhip_batch* b, nhip_stats* s) {
     s->proof_words = b->H.proof_words;
     s->ms_decode = b->decode_ms;
     s->ms_upload = b->upload_ms;
-    s->ms_fiat_shamir = b->last_ms[0];
-    s->ms_row_hash = b->last_ms[1];
-    s->ms_merkle = b->last_ms[2] + b->last_ms[3] + b->last_ms[4];
-    s->ms_merkle_hash = b->last_ms[3];
+    s->ms_fiat_shamir = b->ph.fs;
+    s->ms_row_hash = b->ph.rows;
+    s->ms_merkle = b->ph.plan + b->ph.hash + b->ph.roots;
+    s->ms_merkle_hash = b->ph.hash;
     s->merkle_hash_launches = b->tm.mp_hash_launches;
-    s->ms_ood_air = b->last_ms[5];
-    s->ms_fri = b->last_ms[6];
-    s->ms_deep = b->last_ms[7];
+    s->ms_ood_air = b->ph.ood;
+    s->ms_fri = b->ph.fri;
+    s->ms_deep = b->ph.deep;
     s->ms_device_total = 0;
-    for (int i = 0; i < STARK_EVENTS - 1; ++i) s->ms_device_total += b->last_ms[i];
+    s->ms_device_total = b->ph.total;
     s->tip5_perms_static = b->H.perms_static;
     s->tip5_perms_merkle = b->merkle_perms;
     return NHIP_OK;
@@ -783,6 +801,7 @@ void nhip_batch_destroy(nhip_batch* b) {
     (void)hipSetDevice(b->device);
     if (b->timed)
         for (int i = 0; i < STARK_EVENTS; ++i) (void)hipEventDestroy(b->tm.ev[i]);
+    if (b->aux) (void)hipStreamDestroy(b->aux);
     if (b->dmem) (void)hipFree(b->dmem);
     delete b;
 }

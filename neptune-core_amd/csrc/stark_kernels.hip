@@ -266,14 +266,20 @@ __device__ __forceinline__ void wg_count_scan2(bool p0, bool p1, uint32_t& e0, u
     e1 = s1 + (uint32_t)__popcll(b1 & below);
 }
 
+__device__ __forceinline__ uint64_t mp_leaf_code(const ProofDesc& d, uint32_t p, uint32_t tree, uint32_t k,
+                                                 uint32_t slot) {
+    return tree < 3 ? mps(MPS_DIG, ((uint64_t)p * 3 + tree) * k + slot)
+                    : mps(MPS_XFE, d.fri[tree == 3 ? 0 : tree - 3].leaves_off + 3ull * slot);
+}
+
 template <int B>
 struct MpPlanLds {
     uint32_t key[2][B];
     uint64_t src[2][4][B];
     uint32_t order[B];
     uint32_t scan[8];
-    uint32_t bad;  // bit t: tree t failed (dedupe mismatch, authentication structure too short)
-    uint32_t base;
+    uint32_t bad;  // bit t: tree t failed (authentication structure too short)
+    uint32_t base, ndup;
 };
 
 template <int B>
@@ -289,6 +295,7 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
     const uint32_t NT = grp == 0 ? 4u : 1u;
     const uint32_t tree0 = grp == 0 ? 0u : 3u + grp;  // tree id of this group's first tree
     if (tid < NT) plan.roots[(uint64_t)p * trees_per_proof + tree0 + tid].code = MPS_NONE;
+    if (tid == 0) plan.ndup[(uint64_t)p * (trees_per_proof - 3) + grp] = 0;
     if (fail[p] & FAIL_DECODE) return;
     if (grp > d.R) return;
     uint32_t h, auth_n[4], fail_bit[4];
@@ -321,7 +328,10 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
     }
     L.key[0][tid] = key;
     L.order[tid] = tid;
-    if (tid == 0) L.bad = 0;
+    if (tid == 0) {
+        L.bad = 0;
+        L.ndup = 0;
+    }
     __syncthreads();
     // ---- bitonic sort (descending) of (key, original slot)
     for (uint32_t size = 2; size <= (uint32_t)B; size <<= 1) {
@@ -345,28 +355,16 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
     const uint32_t slot = L.order[tid];
     uint64_t scode[4];
 #pragma unroll
-    for (uint32_t t = 0; t < 4; ++t) {
-        const uint32_t tree = tree0 + t;
-        scode[t] = tree < 3 ? mps(MPS_DIG, ((uint64_t)p * 3 + tree) * k + slot)
-                            : mps(MPS_XFE, d.fri[tree == 3 ? 0 : tree - 3].leaves_off + 3ull * slot);
-    }
-    // dedupe: equal keys must carry equal digests (per tree)
+    for (uint32_t t = 0; t < 4; ++t) scode[t] = t < NT ? mp_leaf_code(d, p, tree0 + t, k, slot) : MPS_NONE;
+    // duplicate leaf indices: kept once; equal digests are checked by k_mp_roots (the leaf digests
+    // are not needed here, so planning does not wait for the row hashes)
+    const uint64_t grp_id = (uint64_t)p * (trees_per_proof - 3) + grp;
     bool dup = false;
     if (skey != 0 && tid > 0 && L.key[0][tid - 1] == skey) {
         dup = true;
-        const uint32_t slot2 = L.order[tid - 1];
-        for (uint32_t t = 0; t < NT; ++t) {
-            const uint32_t tree = tree0 + t;
-            const uint64_t c2 = tree < 3 ? mps(MPS_DIG, ((uint64_t)p * 3 + tree) * k + slot2)
-                                         : mps(MPS_XFE, d.fri[tree == 3 ? 0 : tree - 3].leaves_off + 3ull * slot2);
-            uint64_t a[5], b[5];
-            mp_load(scode[t], words, dig, nullptr, a);
-            mp_load(c2, words, dig, nullptr, b);
-            bool same = true;
-#pragma unroll
-            for (int q = 0; q < 5; ++q) same &= a[q] == b[q];
-            if (!same) atomicOr(&L.bad, 1u << t);
-        }
+        const uint32_t j = atomicAdd(&L.ndup, 1u);
+        plan.dups[(grp_id * k + j) * 2] = slot;
+        plan.dups[(grp_id * k + j) * 2 + 1] = L.order[tid - 1];
     }
     const bool keep = skey != 0 && !dup;
     uint32_t pos, unused_e, m, unused_t;
@@ -376,6 +374,7 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
 #pragma unroll
         for (uint32_t t = 0; t < 4; ++t) L.src[0][t][pos] = scode[t];
     }
+    if (tid == 0) plan.ndup[grp_id] = L.ndup;
     __syncthreads();
     // ---- climb on indices; emit one op per parent node and tree
     uint32_t ap = 0;
@@ -483,18 +482,31 @@ __global__ void __launch_bounds__(256) k_mp_hash(const uint64_t* __restrict__ wo
     for (int q = 0; q < 5; ++q) o[q] = s[q];
 }
 
-__global__ void k_mp_roots(const uint64_t* __restrict__ words, const uint64_t* __restrict__ dig, MpPlan plan,
-                           uint32_t n_records, uint32_t trees_per_proof, uint32_t* __restrict__ fail) {
+// One lane per (proof, tree): duplicate leaf indices carry equal digests, final node == root.
+__global__ void k_mp_roots(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+                           const uint64_t* __restrict__ dig, MpPlan plan, uint32_t n_records, uint32_t trees_per_proof,
+                           uint32_t k, uint32_t* __restrict__ fail) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_records) return;
     const MpRoot r = plan.roots[i];
     if (r.code == MPS_NONE) return;
+    const uint32_t p = i / trees_per_proof, tree = i - p * trees_per_proof;
+    const ProofDesc& d = desc[p];
+    const uint64_t grp_id = (uint64_t)p * (trees_per_proof - 3) + (tree < 4 ? 0u : tree - 3);
+    const uint32_t nd = plan.ndup[grp_id];
+    bool ok = true;
+    for (uint32_t j = 0; j < nd; ++j) {
+        uint64_t a[5], b[5];
+        mp_load(mp_leaf_code(d, p, tree, k, plan.dups[(grp_id * k + j) * 2]), words, dig, nullptr, a);
+        mp_load(mp_leaf_code(d, p, tree, k, plan.dups[(grp_id * k + j) * 2 + 1]), words, dig, nullptr, b);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) ok &= a[q] == b[q];
+    }
     uint64_t v[5];
     mp_load(r.code, words, dig, plan.arena, v);
-    bool ok = true;
 #pragma unroll
     for (int q = 0; q < 5; ++q) ok &= v[q] == to_mont(words[r.root_off + q]);
-    if (!ok) atomicOr(&fail[i / trees_per_proof], r.fail_bit);
+    if (!ok) atomicOr(&fail[p], r.fail_bit);
 }
 
 // ------------------------------------------------------------------ XFE block reduction
@@ -846,58 +858,60 @@ __global__ void k_verdicts(const uint32_t* __restrict__ fail, uint32_t n, uint8_
 }
 
 // ------------------------------------------------------------------ launchers
-hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, StarkPhaseTimer* tm) {
+hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream_t sa, StarkPhaseTimer* tm) {
     const uint32_t n = b.n_proofs;
     if (n == 0) return hipSuccess;
     const uint32_t k = b.dims.num_checks;
-    auto mark = [&](int i) {
-        if (tm && tm->ev[i]) (void)hipEventRecord(tm->ev[i], st);
-    };
-    mark(0);
-    hipLaunchKernelGGL(k_fs_replay_wide, dim3((n * 16 + 255) / 256), dim3(256), 0, st, b.words, b.desc, b.ops, n,
+    const uint32_t tpp = 4 + b.max_R;
+    auto mark = [&](int i, hipStream_t s) { (void)hipEventRecord(tm->ev[i], s); };
+    // fork: the aux stream starts after everything already queued on st (fail-bit reset etc.)
+    mark(0, st);
+    (void)hipStreamWaitEvent(sa, tm->ev[0], 0);
+    // ---- aux stream: latency-bound chain
+    hipLaunchKernelGGL(k_fs_replay_wide, dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words, b.desc, b.ops, n,
                        b.xs, b.idx, b.fail);
-    mark(1);
+    mark(1, sa);
+    if (k <= 128)
+        hipLaunchKernelGGL(k_mp_plan<128>, dim3(n, 1 + b.max_R), dim3(128), 0, sa, b.words, b.desc, n, k, tpp, b.dig,
+                           b.idx, b.mp, b.fail, b.perm_counter);
+    else
+        hipLaunchKernelGGL(k_mp_plan<256>, dim3(n, 1 + b.max_R), dim3(256), 0, sa, b.words, b.desc, n, k, tpp, b.dig,
+                           b.idx, b.mp, b.fail, b.perm_counter);
+    mark(3, sa);
+    hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(256), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims, b.air_nodes,
+                       b.air_level_nodes, b.air_level_off, b.air_n_levels, b.air_cons, b.air_cons_off, b.xs, b.ood,
+                       b.fail);
+    mark(6, sa);
+    hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), b.fri_lds_bytes, sa, b.words, b.desc, n, b.dims, b.xs, b.idx,
+                       b.fail);
+    mark(7, sa);
+    hipLaunchKernelGGL(k_deep, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.ood, b.fail);
+    mark(8, sa);
+    // ---- main stream: VALU-bound hashing
     {
-        uint64_t rows = (uint64_t)n * k;
+        const uint64_t rows = (uint64_t)n * k;
         unsigned gx = (unsigned)((rows + 255) / 256);
         if (gx > 16384) gx = 16384;
         hipLaunchKernelGGL(k_hash_rows, dim3(gx, 3), dim3(256), 0, st, b.words, b.desc, n, k, b.dims, b.dig, b.fail);
     }
-    mark(2);
-    {
-        const uint32_t tpp = 4 + b.max_R;
-        if (k <= 128)
-            hipLaunchKernelGGL(k_mp_plan<128>, dim3(n, 1 + b.max_R), dim3(128), 0, st, b.words, b.desc, n, k, tpp, b.dig, b.idx,
-                               b.mp, b.fail, b.perm_counter);
-        else
-            hipLaunchKernelGGL(k_mp_plan<256>, dim3(n, 1 + b.max_R), dim3(256), 0, st, b.words, b.desc, n, k, tpp, b.dig, b.idx,
-                               b.mp, b.fail, b.perm_counter);
-        mark(3);
-        uint32_t launches = 0;
-        for (uint32_t l = 0; l < b.mp.levels; ++l) {
-            const uint64_t cap = b.mp_cap_host[l];
-            if (cap == 0) continue;
-            hipLaunchKernelGGL(k_mp_hash, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, b.words, b.dig, b.mp, l);
-            ++launches;
-        }
-        if (tm) tm->mp_hash_launches = launches;
-        mark(4);
-        const uint32_t nrec = n * tpp;
-        hipLaunchKernelGGL(k_mp_roots, dim3((nrec + 255) / 256), dim3(256), 0, st, b.words, b.dig, b.mp, nrec, tpp,
-                           b.fail);
+    mark(2, st);
+    (void)hipStreamWaitEvent(st, tm->ev[3], 0);  // plan done
+    uint32_t launches = 0;
+    for (uint32_t l = 0; l < b.mp.levels; ++l) {
+        const uint64_t cap = b.mp_cap_host[l];
+        if (cap == 0) continue;
+        hipLaunchKernelGGL(k_mp_hash, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, b.words, b.dig, b.mp, l);
+        ++launches;
     }
-    mark(5);
-    hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(256), b.air_lds_bytes, st, b.words, b.desc, n, b.dims, b.air_nodes,
-                       b.air_level_nodes, b.air_level_off, b.air_n_levels, b.air_cons, b.air_cons_off, b.xs, b.ood,
-                       b.fail);
-    mark(6);
-    hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), b.fri_lds_bytes, st, b.words, b.desc, n, b.dims, b.xs, b.idx,
-                       b.fail);
-    mark(7);
-    hipLaunchKernelGGL(k_deep, dim3(n), dim3(256), 0, st, b.words, b.desc, n, b.dims, b.xs, b.idx, b.ood, b.fail);
-    mark(8);
+    tm->mp_hash_launches = launches;
+    mark(4, st);
+    const uint32_t nrec = n * tpp;
+    hipLaunchKernelGGL(k_mp_roots, dim3((nrec + 255) / 256), dim3(256), 0, st, b.words, b.desc, b.dig, b.mp, nrec, tpp,
+                       k, b.fail);
+    mark(5, st);
+    (void)hipStreamWaitEvent(st, tm->ev[8], 0);  // join the aux chain
     hipLaunchKernelGGL(k_verdicts, dim3((n + 255) / 256), dim3(256), 0, st, b.fail, n, b.verdicts);
-    mark(9);
+    mark(9, st);
     return hipGetLastError();
 }
 
