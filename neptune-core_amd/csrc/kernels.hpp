@@ -19,7 +19,6 @@ hipError_t launch_mtree_verify(const uint64_t* d_roots, int per_path_root, const
 
 // ---- batched STARK verifier (stark_kernels.hip)
 static constexpr uint32_t AIR_LDS_HEADER = (256 + 4 + 4) * 24 + 16;  // red, zinv, derived, flag
-static constexpr uint32_t FRI_LDS_HEADER = 256 * 24 + 256 + 16;      // red, tip5 lut, flag
 
 // Level-synchronous Merkle multiproof plan (see k_mp_plan in stark_kernels.hip).  Ops of level l
 // live in MP_SHARDS shards (shard = proof index % MP_SHARDS) so the per-level slot reservations of
@@ -52,7 +51,11 @@ struct StarkBatchDev {
     uint32_t* idx;
     uint64_t* dig;
     uint64_t* ood;
+    uint64_t* xdom;        // [n_proofs][k] round-0 FRI domain point of each check (raw), k_fri -> k_deep
+    uint64_t* lcw;         // [n_proofs][max_lcw][5] last-codeword Merkle tree nodes (heap order)
+    uint32_t max_lcw;      // max last-codeword length (power of two)
     uint32_t* fail;
+    const uint32_t* fail_init;  // decode-time failure bits (FAIL_DECODE), constant across runs
     uint8_t* verdicts;
     unsigned long long* perm_counter;  // Merkle hash_pairs performed (device-counted)
     MpPlan mp;
@@ -63,7 +66,7 @@ struct StarkBatchDev {
     uint32_t air_n_levels;
     const uint32_t* air_cons;
     uint4 air_cons_off;
-    size_t air_lds_bytes, fri_lds_bytes;
+    size_t air_lds_bytes;
 };
 
 // events: 0 start | fs | rows | mp plan | mp hash levels | mp roots | ood | fri | deep | 9 verdicts

@@ -128,7 +128,8 @@ struct HostBatch {
     std::vector<uint32_t> fail;
     uint64_t xs_total = 0, idx_total = 0;
     uint32_t max_R = 0, max_last_cw = 1;
-    uint64_t perms_static = 0;  // FS + row hashing + last-codeword trees (Merkle paths counted on device)
+    uint64_t perms_static = 0;  // FS + row hashing (multiproof Merkle hashes are counted on device)
+    uint64_t perms_lcw = 0;     // last-codeword Merkle trees (hashed with the multiproof levels)
     uint64_t proof_words = 0;
 };
 
@@ -316,8 +317,8 @@ void decode_proof(HostBatch& B, const nhip_claim& claim, const nhip_proof& proof
             // rows + last codeword tree
             perms += (uint64_t)k * (absorb_perms(d.num_main) + absorb_perms(3ull * d.num_aux) +
                                     absorb_perms(3ull * d.num_quot_seg));
-            perms += cw->n - 1;
             B.perms_static += perms;
+            B.perms_lcw += cw->n - 1;  // last-codeword tree, hashed by k_mp_hash
         }
     }
     if (!ok) {
@@ -400,8 +401,8 @@ bool dims_from(const nhip_stark_params* sp, const nhip_air* air, Dims& D) {
     d.num_sampled = air->dims_air.num_sampled;
     d.num_constraints = air->dims_air.num_constraints;
     D.expansion = 1u << sp->log2_fri_expansion;
-    // the last FRI codeword (at most 2^(floor(log2 k) + 1 + log2 expansion) XFEs) is rebuilt into a
-    // Merkle tree in one workgroup's LDS
+    // the last FRI codeword has at most 2^(floor(log2 k) + 1 + log2 expansion) XFEs; bound its
+    // Merkle-tree scratch (n x max_len digests)
     if ((1ull << (log2u(d.num_checks) + 1 + d.log2_expansion)) > 4096) return false;
     return true;
 }
@@ -624,7 +625,9 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
                          (size_t)levels * MP_SHARDS * 4 + 4,
                          std::max<size_t>(1, n) * tpp * sizeof(MpRoot),
                          std::max<size_t>(1, n) * (1 + H.max_R) * k * 8,
-                         std::max<size_t>(1, n) * (1 + H.max_R) * 4};
+                         std::max<size_t>(1, n) * (1 + H.max_R) * 4,
+                         std::max<size_t>(1, n) * k * 8,
+                         std::max<size_t>(1, n) * H.max_last_cw * 40};
     constexpr int NBUF = sizeof(sz) / sizeof(sz[0]);
     size_t total = 0;
     for (size_t s : sz) total += al(s);
@@ -682,6 +685,10 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     dv.mp.dups = (uint32_t*)ptr[17];
     dv.mp.ndup = (uint32_t*)ptr[18];
     dv.mp.levels = levels;
+    dv.xdom = (uint64_t*)ptr[19];
+    dv.lcw = (uint64_t*)ptr[20];
+    dv.max_lcw = H.max_last_cw;
+    dv.fail_init = b->d_fail_init;
     dv.mp_cap_host = b->mp_cap.data();
     dv.air_nodes = air->d_nodes;
     dv.air_level_nodes = air->d_level_nodes;
@@ -690,8 +697,7 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     dv.air_cons = air->d_cons;
     dv.air_cons_off = air->cons_off;
     dv.air_lds_bytes = AIR_LDS_HEADER + air->nodes.size() * 24;
-    dv.fri_lds_bytes = FRI_LDS_HEADER + (size_t)H.max_last_cw * 40;
-    if (dv.air_lds_bytes > 160 * 1024 - 8192 || dv.fri_lds_bytes > 160 * 1024 - 16384) {
+    if (dv.air_lds_bytes > 160 * 1024 - 8192) {
         (void)hipFree(b->dmem);
         delete b;
         return NHIP_ERR_ARG;  // AIR too large for the single-workgroup LDS evaluator
@@ -724,6 +730,7 @@ int nhip_batch_run(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* all
     if (e == hipSuccess) e = hipMemcpyAsync(&b->merkle_perms, b->d_perm_counter, 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hipfail(e);
+    b->merkle_perms += b->H.perms_lcw;
     // phases overlap (two streams): each is timed from the event its inputs wait on
     auto el = [&](int a, int c) {
         float ms = 0.f;

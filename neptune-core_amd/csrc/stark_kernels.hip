@@ -451,43 +451,101 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
     if (tid == 0 && perm_counter) atomicAdd(perm_counter, hashed);
 }
 
+// The last FRI codeword's Merkle tree (every node; XFE leaves embedded as [c0, c1, c2, 0, 0]) is
+// hashed by the same launches: blocks past the multiproof ops of level l take the level-l parents
+// of every proof's last-codeword tree, lane q -> (proof q / (maxL >> (l + 1)), parent q % ...).
+// Node v of a proof's tree (heap order, root 1, leaves L..2L-1) lives at lcw[(p * maxL + v) * 5].
+struct LcwTree {
+    uint64_t* nodes;
+    uint32_t max_len;   // max last-codeword length over the batch (power of two)
+};
+
+__device__ __forceinline__ void lcw_node(const uint64_t* __restrict__ words, const ProofDesc& d,
+                                         const uint64_t* __restrict__ mine, uint32_t v, uint32_t L, uint64_t o[5]) {
+    if (v >= L) {
+        const uint64_t off = d.last_cw_off + 3ull * (v - L);
+        o[0] = to_mont(words[off]);
+        o[1] = to_mont(words[off + 1]);
+        o[2] = to_mont(words[off + 2]);
+        o[3] = 0;
+        o[4] = 0;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) o[q] = mine[5ull * v + q];
+    }
+}
+
 __global__ void __launch_bounds__(256) k_mp_hash(const uint64_t* __restrict__ words, const uint64_t* __restrict__ dig,
-                                                 MpPlan plan, uint32_t lvl) {
+                                                 MpPlan plan, uint32_t lvl, uint32_t mp_blocks,
+                                                 const ProofDesc* __restrict__ desc, uint32_t n_proofs,
+                                                 const uint32_t* __restrict__ fail_init, LcwTree lcw) {
     __shared__ Tip5Lds t5;
     __shared__ uint64_t s_base[MP_SHARDS + 1];
     __shared__ uint32_t s_cnt[MP_SHARDS];
-    if (threadIdx.x < MP_SHARDS) {
-        s_base[threadIdx.x] = plan.shard_base[lvl * MP_SHARDS + threadIdx.x];
-        s_cnt[threadIdx.x] = plan.counter[lvl * MP_SHARDS + threadIdx.x];
+    const bool is_lcw = blockIdx.x >= mp_blocks;  // uniform per block
+    if (!is_lcw) {
+        if (threadIdx.x < MP_SHARDS) {
+            s_base[threadIdx.x] = plan.shard_base[lvl * MP_SHARDS + threadIdx.x];
+            s_cnt[threadIdx.x] = plan.counter[lvl * MP_SHARDS + threadIdx.x];
+        }
+        if (threadIdx.x == 0)
+            s_base[MP_SHARDS] = plan.shard_base[(lvl + 1) * MP_SHARDS - 1] + plan.shard_cap[(lvl + 1) * MP_SHARDS - 1];
     }
-    if (threadIdx.x == 0)
-        s_base[MP_SHARDS] = plan.shard_base[(lvl + 1) * MP_SHARDS - 1] + plan.shard_cap[(lvl + 1) * MP_SHARDS - 1];
     tip5_lds_init(t5);  // includes the barrier
-    const uint64_t g = s_base[0] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= s_base[MP_SHARDS]) return;
-    uint32_t sh = 0;
-#pragma unroll
-    for (uint32_t q = 1; q < MP_SHARDS; ++q) sh += g >= s_base[q] ? 1u : 0u;
-    if (g - s_base[sh] >= s_cnt[sh]) return;
-    const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
-    if (lc == MPS_NONE) return;  // op of a tree that already failed
     uint64_t s[16];
-    mp_load(lc, words, dig, plan.arena, s);
-    mp_load(rc, words, dig, plan.arena, s + 5);
+    uint64_t* o;
+    if (is_lcw) {
+        const uint32_t per = lcw.max_len >> (lvl + 1);
+        const uint64_t q = (uint64_t)(blockIdx.x - mp_blocks) * blockDim.x + threadIdx.x;
+        const uint32_t p = (uint32_t)(q / per), i = (uint32_t)(q % per);
+        if (p >= n_proofs || (fail_init[p] & FAIL_DECODE)) return;
+        const ProofDesc& d = desc[p];
+        const uint32_t L = d.last_cw_n;
+        if (i >= (L >> (lvl + 1))) return;
+        const uint32_t v = (L >> (lvl + 1)) + i;
+        uint64_t* mine = lcw.nodes + (uint64_t)p * lcw.max_len * 5;
+        lcw_node(words, d, mine, 2 * v, L, s);
+        lcw_node(words, d, mine, 2 * v + 1, L, s + 5);
+        o = mine + 5ull * v;
+    } else {
+        const uint64_t g = s_base[0] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (g >= s_base[MP_SHARDS]) return;
+        uint32_t sh = 0;
+#pragma unroll
+        for (uint32_t q = 1; q < MP_SHARDS; ++q) sh += g >= s_base[q] ? 1u : 0u;
+        if (g - s_base[sh] >= s_cnt[sh]) return;
+        const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
+        if (lc == MPS_NONE) return;  // op of a tree that already failed
+        mp_load(lc, words, dig, plan.arena, s);
+        mp_load(rc, words, dig, plan.arena, s + 5);
+        o = plan.arena + 5 * g;
+    }
 #pragma unroll
     for (int q = 10; q < 16; ++q) s[q] = MONT_ONE;
     tip5_permute_raw(s, t5.lut);
-    uint64_t* o = plan.arena + 5 * g;
 #pragma unroll
     for (int q = 0; q < 5; ++q) o[q] = s[q];
 }
 
 // One lane per (proof, tree): duplicate leaf indices carry equal digests, final node == root.
+// Lanes n_records.. check the last codeword's Merkle root, one per proof.
 __global__ void k_mp_roots(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                            const uint64_t* __restrict__ dig, MpPlan plan, uint32_t n_records, uint32_t trees_per_proof,
-                           uint32_t k, uint32_t* __restrict__ fail) {
+                           uint32_t k, uint32_t* __restrict__ fail, uint32_t n_proofs,
+                           const uint32_t* __restrict__ fail_init, LcwTree lcw) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_records) return;
+    if (i >= n_records) {
+        const uint32_t p = i - n_records;
+        if (p >= n_proofs || (fail_init[p] & FAIL_DECODE)) return;
+        const ProofDesc& d = desc[p];
+        uint64_t v[5];
+        lcw_node(words, d, lcw.nodes + (uint64_t)p * lcw.max_len * 5, 1, d.last_cw_n, v);
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) ok &= v[q] == to_mont(words[d.fri_root[d.R] + q]);
+        if (!ok) atomicOr(&fail[p], FAIL_FRI_LAST_ROOT);
+        return;
+    }
     const MpRoot r = plan.roots[i];
     if (r.code == MPS_NONE) return;
     const uint32_t p = i / trees_per_proof, tree = i - p * trees_per_proof;
@@ -652,99 +710,78 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
 
 // ------------------------------------------------------------------ FRI
 // One workgroup per proof.  Lane j follows collinearity check j through all rounds:
-// a_{r+1} = line through (x_a, a_r), (x_b, b_r) evaluated at alpha_r.  Then the last codeword:
-// Merkle root (tree of XFE digests built in LDS), agreement at the a-indices, and
-// Horner(last polynomial, t) == barycentric(last codeword, t).
+// a_{r+1} = line through (x_a, a_r), (x_b, b_r) evaluated at alpha_r.  The round-r domain point of
+// check j is x_r = (7 * g^i)^(2^r) and its partner is -x_r (the a/b indices differ by half the
+// round-r domain), so one exponentiation and one inversion per lane serve every round:
+// x_{r+1} = x_r^2, 1/x_{r+1} = (1/x_r)^2, slope = (b - a) * (-1/2) / x_r.  The lane also stores x_0
+// (raw) for DEEP.  Then the last codeword: agreement at the a-indices, and Horner(last polynomial, t)
+// == barycentric(last codeword, t).  The last codeword's Merkle tree is hashed with the multiproof
+// levels (k_mp_hash) and its root checked in k_mp_roots.
+__device__ __forceinline__ uint64_t lds_pow(const uint64_t* __restrict__ sq, uint64_t e) {
+    // sq[b] = g^(2^b); e < 2^32
+    uint64_t r = MONT_ONE;
+    for (uint32_t b = 0; e; ++b, e >>= 1)
+        if (e & 1) r = mont_mul(r, sq[b]);
+    return r;
+}
+
 __global__ void __launch_bounds__(256) k_fri(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                              uint32_t n_proofs, StarkDims dims, const uint64_t* __restrict__ xs,
-                                             const uint32_t* __restrict__ idx_all, uint32_t* __restrict__ fail) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    Xfe* red = reinterpret_cast<Xfe*>(smem);                                   // 256
-    Tip5Lds& t5 = *reinterpret_cast<Tip5Lds*>(smem + 256 * sizeof(Xfe));      // 256 B
-    uint32_t& lflag = *reinterpret_cast<uint32_t*>(smem + 256 * sizeof(Xfe) + 256);
-    uint64_t(*tree)[5] = reinterpret_cast<uint64_t(*)[5]>(smem + FRI_LDS_HEADER);  // last_cw_n digests
+                                             const uint32_t* __restrict__ idx_all, uint64_t* __restrict__ xdom,
+                                             uint32_t* __restrict__ fail) {
+    __shared__ Xfe red[256];
+    __shared__ uint64_t gsq[33], wsq[33];
+    __shared__ uint32_t lflag;
     const uint32_t p = blockIdx.x, tid = threadIdx.x;
-    if (p >= n_proofs) return;
-    tip5_lds_init(t5);
-    if (fail[p] & FAIL_DECODE) return;
+    if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
     const ProofDesc& d = desc[p];
     const SampleLayout sl = SampleLayout::of(dims, d.R);
     const uint64_t xb = d.xs_off * 3;
     const uint32_t k = dims.num_checks;
     const uint32_t* __restrict__ idx = idx_all + d.idx_off;
-    if (tid == 0) lflag = 0;
+    const uint32_t L = d.last_cw_n;
+    const uint32_t log2L = 31 - __clz(L);
+    if (tid == 0) {
+        lflag = 0;
+        uint64_t g = root_of_unity(d.log2_N);
+        for (uint32_t q = 0; q < d.log2_N; ++q, g = mont_mul(g, g)) gsq[q] = g;
+    } else if (tid == 64) {
+        uint64_t w = root_of_unity(log2L);
+        for (uint32_t q = 0; q < log2L; ++q, w = mont_mul(w, w)) wsq[q] = w;
+    }
     __syncthreads();
     uint32_t f = 0;
     if (tid < k) {
-        const uint64_t i0 = idx[tid];
+        const uint32_t i0 = idx[tid];
         Xfe a = ld_xfe_canon(words, d.fri[0].leaves_off + 3ull * tid);
-        const uint64_t g0 = root_of_unity(d.log2_N);
-        uint64_t offset = to_mont(7), gen = g0;
+        uint64_t x = mont_mul(to_mont(7), lds_pow(gsq, i0));
+        xdom[(uint64_t)p * k + tid] = x;
+        uint64_t xinv = b_inv(x);
+        const uint64_t neg_half = to_mont((GL_P - 1) / 2);  // -1/2
         for (uint32_t r = 0; r < d.R; ++r) {
-            const uint64_t n = 1ull << (d.log2_N - r);
-            const uint64_t ai = i0 % n, bi = (i0 + n / 2) % n;
             const Xfe b = ld_xfe_canon(words, d.fri[1 + r].leaves_off + 3ull * tid);
-            const uint64_t ax = mont_mul(offset, b_pow(gen, ai));
-            const uint64_t bx = mont_mul(offset, b_pow(gen, bi));
             const Xfe alpha = ld_xfe_raw(xs, xb + 3ull * (sl.alpha + r));
-            const uint64_t inv = b_inv(gl_sub(bx, ax));
-            const Xfe slope = x_scale(x_sub(b, a), inv);
-            a = x_add(a, x_mul(slope, x_sub(alpha, x_lift(ax))));
-            offset = mont_mul(offset, offset);
-            gen = mont_mul(gen, gen);
+            const Xfe slope = x_scale(x_sub(b, a), mont_mul(neg_half, xinv));
+            a = x_add(a, x_mul(slope, x_sub(alpha, x_lift(x))));
+            x = mont_mul(x, x);
+            xinv = mont_mul(xinv, xinv);
         }
-        const uint64_t nl = 1ull << (d.log2_N - d.R);
-        const Xfe last = ld_xfe_canon(words, d.last_cw_off + 3ull * (i0 % nl));
+        const Xfe last = ld_xfe_canon(words, d.last_cw_off + 3ull * (i0 & (L - 1)));
         if (!x_eq(last, a)) f |= FAIL_FRI_LAST_AGREE;
-    }
-    // last codeword Merkle root
-    const uint32_t L = d.last_cw_n;
-    const uint32_t log2L = 31 - __clz(L);
-    for (uint32_t i = tid; i < L; i += blockDim.x) {
-        const uint64_t off = d.last_cw_off + 3ull * i;
-        tree[i][0] = to_mont(words[off]);
-        tree[i][1] = to_mont(words[off + 1]);
-        tree[i][2] = to_mont(words[off + 2]);
-        tree[i][3] = 0;
-        tree[i][4] = 0;
-    }
-    __syncthreads();
-    for (uint32_t lv = 0; lv < log2L; ++lv) {
-        const uint32_t np = L >> (lv + 1);
-        uint64_t par[5];
-        const bool act = tid < np;
-        // parents of this level are written in place at [0, np) after all lanes read their children
-        for (uint32_t base = 0; base < np; base += blockDim.x) {
-            const uint32_t i = base + tid;
-            const bool a2 = i < np;
-            if (a2) hash_pair_raw(tree[2 * i], tree[2 * i + 1], par, t5.lut);
-            __syncthreads();
-            if (a2) {
-#pragma unroll
-                for (int q = 0; q < 5; ++q) tree[i][q] = par[q];
-            }
-            __syncthreads();
-        }
-        (void)act;
-    }
-    if (tid == 0) {
-        bool ok = true;
-        const uint64_t* rt = words + d.fri_root[d.R];
-#pragma unroll
-        for (int q = 0; q < 5; ++q) ok &= (tree[0][q] == to_mont(rt[q]));
-        if (!ok) f |= FAIL_FRI_LAST_ROOT;
     }
     // barycentric evaluation of the last codeword at the indeterminate vs Horner of the polynomial
     const Xfe t = ld_xfe_raw(xs, xb + 3ull * sl.indeterminate);
-    const uint64_t wL = root_of_unity(log2L);
     Xfe num = x_zero(), den = x_zero();
-    for (uint32_t i = tid; i < L; i += blockDim.x) {
-        const uint64_t wi = b_pow(wL, i);
-        const Xfe diff = x_sub(t, x_lift(wi));
-        if (x_is_zero(diff)) atomicOr(&lflag, 1u);
-        const Xfe q = x_scale(x_inv(diff), wi);
-        num = x_add(num, x_mul(q, ld_xfe_canon(words, d.last_cw_off + 3ull * i)));
-        den = x_add(den, q);
+    if (tid < L) {
+        uint64_t wi = lds_pow(wsq, tid);
+        const uint64_t wstep = blockDim.x < L ? wsq[31 - __clz(blockDim.x)] : MONT_ONE;
+        for (uint32_t i = tid; i < L; i += blockDim.x, wi = mont_mul(wi, wstep)) {
+            const Xfe diff = x_sub(t, x_lift(wi));
+            if (x_is_zero(diff)) atomicOr(&lflag, 1u);
+            const Xfe q = x_scale(x_inv(diff), wi);
+            num = x_add(num, x_mul(q, ld_xfe_canon(words, d.last_cw_off + 3ull * i)));
+            den = x_add(den, q);
+        }
     }
     const Xfe snum = block_sum_xfe(num, red);
     const Xfe sden = block_sum_xfe(den, red);
@@ -760,17 +797,19 @@ __global__ void __launch_bounds__(256) k_fri(const uint64_t* __restrict__ words,
 
 // ------------------------------------------------------------------ DEEP
 // One workgroup per proof.  Phase 1: wave w forms the linear combinations of revealed rows
-// j = w, w + 4, ... (lanes split the row; the row weights stay in registers).  Phase 2: the 3k DEEP
-// quotient terms (row j, term t) are independent XFE inversions, one per lane.  Phase 3: lane j sums
-// its row's three terms and compares with the FRI round-0 value.
+// j = w, w + 4, ... (lanes split the row; the row weights stay in registers).  Proof words are
+// canonical and the weights raw Montgomery, so mont_mul(weight, word) is already the canonical
+// product: the row sums stay canonical and only the final sum is converted.  Phase 2: lane j takes
+// row j's three DEEP terms (x - z, x - z*w_trace, x - z^Q; x from k_fri), inverts their product
+// once (Montgomery's trick) and compares the recombined value with the FRI round-0 leaf.
 static constexpr uint32_t DEEP_MAX_COLS_PER_LANE = 8;  // (M + A) <= 512
 
 __global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                               uint32_t n_proofs, StarkDims dims, const uint64_t* __restrict__ xs,
-                                              const uint32_t* __restrict__ idx_all, const uint64_t* __restrict__ ood,
+                                              const uint64_t* __restrict__ xdom, const uint64_t* __restrict__ ood,
                                               uint32_t* __restrict__ fail) {
-    __shared__ Xfe s_row[MAX_CHECKS], s_quot[MAX_CHECKS], s_term[3 * MAX_CHECKS];
-    __shared__ uint32_t s_flag;
+    __shared__ Xfe s_row[MAX_CHECKS], s_quot[MAX_CHECKS];
+    __shared__ Xfe s_at[3];
     const uint32_t p = blockIdx.x, tid = threadIdx.x;
     if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
     const ProofDesc& d = desc[p];
@@ -778,7 +817,15 @@ __global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words
     const uint64_t xb = d.xs_off * 3;
     const uint32_t M = dims.num_main, A = dims.num_aux, Q = dims.num_quot_seg, k = dims.num_checks;
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
-    if (tid == 0) s_flag = 0;
+    if (tid == 64) {
+        // evaluation points of the three DEEP terms: z, z * w_trace, z^Q
+        const Xfe z = ld_xfe_raw(xs, xb + 3ull * sl.z);
+        s_at[0] = z;
+        s_at[1] = x_scale(z, root_of_unity(d.log2_ph));
+        Xfe zq = x_one();
+        for (uint32_t q = 0; q < Q; ++q) zq = x_mul(zq, z);
+        s_at[2] = zq;
+    }
     Xfe wcol[DEEP_MAX_COLS_PER_LANE];
 #pragma unroll
     for (uint32_t i = 0; i < DEEP_MAX_COLS_PER_LANE; ++i) {
@@ -794,13 +841,13 @@ __global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words
         for (uint32_t i = 0; i < DEEP_MAX_COLS_PER_LANE; ++i) {
             const uint32_t c = lane + 64 * i;
             if (c < M) {
-                acc = x_add(acc, x_scale(wcol[i], to_mont(mrow[c])));
+                acc = x_add(acc, x_scale(wcol[i], mrow[c]));
             } else if (c < M + A) {
-                acc = x_add(acc, x_mul(wcol[i], ld_xfe_canon(words, arow + 3ull * (c - M))));
+                acc = x_add(acc, x_mul(wcol[i], ld_xfe_raw(words, arow + 3ull * (c - M))));
             }
         }
         Xfe qv = x_zero();
-        if (lane < Q) qv = x_mul(wq, ld_xfe_canon(words, d.quot_rows_off + (uint64_t)j * 3 * Q + 3ull * lane));
+        if (lane < Q) qv = x_mul(wq, ld_xfe_raw(words, d.quot_rows_off + (uint64_t)j * 3 * Q + 3ull * lane));
         for (int s = 32; s > 0; s >>= 1) {
             acc.c0 = gl_add(acc.c0, __shfl_xor(acc.c0, s));
             acc.c1 = gl_add(acc.c1, __shfl_xor(acc.c1, s));
@@ -810,42 +857,32 @@ __global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words
             qv.c2 = gl_add(qv.c2, __shfl_xor(qv.c2, s));
         }
         if (lane == 0) {
-            s_row[j] = acc;
-            s_quot[j] = qv;
-        }
-    }
-    __syncthreads();
-    const Xfe z = ld_xfe_raw(xs, xb + 3ull * sl.z);
-    const uint64_t gN = root_of_unity(d.log2_N);
-    const uint32_t* __restrict__ idx = idx_all + d.idx_off;
-    for (uint32_t t = tid; t < 3 * k; t += blockDim.x) {
-        const uint32_t j = t / 3, which = t - 3 * j;
-        Xfe at;  // evaluation point of this term: z, z * w_trace, z^Q
-        if (which == 0) {
-            at = z;
-        } else if (which == 1) {
-            at = x_scale(z, root_of_unity(d.log2_ph));
-        } else {
-            at = x_one();
-            for (uint32_t q = 0; q < Q; ++q) at = x_mul(at, z);
-        }
-        const uint64_t x = mont_mul(to_mont(7), b_pow(gN, idx[j]));
-        const Xfe den = x_sub(x_lift(x), at);
-        const Xfe num = which == 2 ? x_sub(s_quot[j], ld_xfe_raw(ood, (uint64_t)p * 9 + 6))
-                                   : x_sub(s_row[j], ld_xfe_raw(ood, (uint64_t)p * 9 + 3 * which));
-        if (x_is_zero(den)) {
-            atomicOr(&s_flag, 1u);
-            s_term[t] = x_zero();
-        } else {
-            const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + Q + which));
-            s_term[t] = x_mul(x_mul(num, x_inv(den)), w);
+            s_row[j] = {to_mont(acc.c0), to_mont(acc.c1), to_mont(acc.c2)};
+            s_quot[j] = {to_mont(qv.c0), to_mont(qv.c1), to_mont(qv.c2)};
         }
     }
     __syncthreads();
     uint32_t f = 0;
-    if (tid == 0 && s_flag) f |= FAIL_ZERO_INVERSE;
     for (uint32_t j = tid; j < k; j += blockDim.x) {
-        const Xfe deep = x_add(x_add(s_term[3 * j], s_term[3 * j + 1]), s_term[3 * j + 2]);
+        const Xfe x = x_lift(xdom[(uint64_t)p * k + j]);
+        const Xfe d0 = x_sub(x, s_at[0]), d1 = x_sub(x, s_at[1]), d2 = x_sub(x, s_at[2]);
+        const Xfe d01 = x_mul(d0, d1);
+        const Xfe prod = x_mul(d01, d2);
+        if (x_is_zero(prod)) {
+            f |= FAIL_ZERO_INVERSE;
+            continue;
+        }
+        const Xfe inv = x_inv(prod);
+        const Xfe inv2 = x_mul(inv, d01);   // 1 / d2
+        const Xfe inv01 = x_mul(inv, d2);   // 1 / (d0 d1)
+        const Xfe inv0 = x_mul(inv01, d1);  // 1 / d0
+        const Xfe inv1 = x_mul(inv01, d0);  // 1 / d1
+        const uint64_t* __restrict__ oo = ood + (uint64_t)p * 9;
+        const uint64_t wd = xb + 3ull * (sl.lin_w + M + A + Q);
+        const Xfe t0 = x_mul(x_mul(x_sub(s_row[j], ld_xfe_raw(oo, 0)), inv0), ld_xfe_raw(xs, wd));
+        const Xfe t1 = x_mul(x_mul(x_sub(s_row[j], ld_xfe_raw(oo, 3)), inv1), ld_xfe_raw(xs, wd + 3));
+        const Xfe t2 = x_mul(x_mul(x_sub(s_quot[j], ld_xfe_raw(oo, 6)), inv2), ld_xfe_raw(xs, wd + 6));
+        const Xfe deep = x_add(x_add(t0, t1), t2);
         const Xfe fri_v = ld_xfe_canon(words, d.fri[0].leaves_off + 3ull * j);
         if (!x_eq(deep, fri_v)) f |= FAIL_DEEP;
     }
@@ -882,10 +919,9 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
                        b.air_level_nodes, b.air_level_off, b.air_n_levels, b.air_cons, b.air_cons_off, b.xs, b.ood,
                        b.fail);
     mark(6, sa);
-    hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), b.fri_lds_bytes, sa, b.words, b.desc, n, b.dims, b.xs, b.idx,
-                       b.fail);
+    hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
     mark(7, sa);
-    hipLaunchKernelGGL(k_deep, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.ood, b.fail);
+    hipLaunchKernelGGL(k_deep, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.xdom, b.ood, b.fail);
     mark(8, sa);
     // ---- main stream: VALU-bound hashing
     {
@@ -897,17 +933,24 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     mark(2, st);
     (void)hipStreamWaitEvent(st, tm->ev[3], 0);  // plan done
     uint32_t launches = 0;
-    for (uint32_t l = 0; l < b.mp.levels; ++l) {
-        const uint64_t cap = b.mp_cap_host[l];
-        if (cap == 0) continue;
-        hipLaunchKernelGGL(k_mp_hash, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, b.words, b.dig, b.mp, l);
+    const LcwTree lcw{b.lcw, b.max_lcw};
+    const uint32_t log2_lcw = 31 - __builtin_clz(b.max_lcw);
+    const uint32_t hash_levels = b.mp.levels > log2_lcw ? b.mp.levels : log2_lcw;
+    for (uint32_t l = 0; l < hash_levels; ++l) {
+        const uint64_t cap = l < b.mp.levels ? b.mp_cap_host[l] : 0;
+        const uint32_t mp_blocks = (uint32_t)((cap + 255) / 256);
+        const uint64_t per = b.max_lcw >> (l + 1);
+        const uint32_t lcw_blocks = (uint32_t)((per * n + 255) / 256);
+        if (mp_blocks + lcw_blocks == 0) continue;
+        hipLaunchKernelGGL(k_mp_hash, dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, b.words, b.dig, b.mp, l, mp_blocks,
+                           b.desc, n, b.fail_init, lcw);
         ++launches;
     }
     tm->mp_hash_launches = launches;
     mark(4, st);
     const uint32_t nrec = n * tpp;
-    hipLaunchKernelGGL(k_mp_roots, dim3((nrec + 255) / 256), dim3(256), 0, st, b.words, b.desc, b.dig, b.mp, nrec, tpp,
-                       k, b.fail);
+    hipLaunchKernelGGL(k_mp_roots, dim3((nrec + n + 255) / 256), dim3(256), 0, st, b.words, b.desc, b.dig, b.mp, nrec,
+                       tpp, k, b.fail, n, b.fail_init, lcw);
     mark(5, st);
     (void)hipStreamWaitEvent(st, tm->ev[8], 0);  // join the aux chain
     hipLaunchKernelGGL(k_verdicts, dim3((n + 255) / 256), dim3(256), 0, st, b.fail, n, b.verdicts);
@@ -918,7 +961,7 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
 hipError_t stark_set_kernel_attributes() {
     hipError_t e = hipFuncSetAttribute((const void*)k_ood_air, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
     if (e != hipSuccess) return e;
-    return hipFuncSetAttribute((const void*)k_fri, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 16384);
+    return e;
 }
 
 }  // namespace nhip

@@ -36,16 +36,27 @@ __host__ __device__ __forceinline__ Xfe x_mul(Xfe a, Xfe b) {
     return {gl_sub(p00, c3), gl_sub(gl_add(c1, c3), c4), gl_add(c2, c4)};
 }
 
-// base-field inverse a^(p-2) (a != 0), Montgomery in/out
+// x^(2^n) (n successive Montgomery squarings)
+__host__ __device__ __forceinline__ uint64_t b_sqn(uint64_t x, int n) {
+#pragma unroll 1
+    for (int i = 0; i < n; ++i) x = mont_mul(x, x);
+    return x;
+}
+
+// base-field inverse a^(p-2) (a != 0; 0 -> 0), Montgomery in/out.  Addition chain for
+// p - 2 = (2^32 - 2) * 2^32 + (2^32 - 1): 63 squarings + 9 products (square-and-multiply over the
+// 63 one-bits of p - 2 would take 125).
 __host__ __device__ __forceinline__ uint64_t b_inv(uint64_t a) {
-    uint64_t r = MONT_ONE_W, base = a;
-    uint64_t e = GL_P - 2;
-    while (e) {
-        if (e & 1) r = mont_mul(r, base);
-        base = mont_mul(base, base);
-        e >>= 1;
-    }
-    return r;
+    const uint64_t t2 = mont_mul(mont_mul(a, a), a);         // a^(2^2 - 1)
+    const uint64_t t3 = mont_mul(mont_mul(t2, t2), a);       // a^(2^3 - 1)
+    const uint64_t t6 = mont_mul(b_sqn(t3, 3), t3);          // a^(2^6 - 1)
+    const uint64_t t12 = mont_mul(b_sqn(t6, 6), t6);         // a^(2^12 - 1)
+    const uint64_t t15 = mont_mul(b_sqn(t12, 3), t3);        // a^(2^15 - 1)
+    const uint64_t t30 = mont_mul(b_sqn(t15, 15), t15);      // a^(2^30 - 1)
+    const uint64_t t31 = mont_mul(mont_mul(t30, t30), a);    // a^(2^31 - 1)
+    const uint64_t t32m2 = mont_mul(t31, t31);               // a^(2^32 - 2)
+    const uint64_t t32 = mont_mul(t32m2, a);                 // a^(2^32 - 1)
+    return mont_mul(b_sqn(t32m2, 32), t32);                  // a^(p - 2)
 }
 
 __host__ __device__ __forceinline__ uint64_t b_pow(uint64_t a, uint64_t e) {
