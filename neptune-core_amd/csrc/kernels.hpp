@@ -81,4 +81,14 @@ struct StarkPhaseTimer {
 hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream_t st_aux, StarkPhaseTimer* tm);
 hipError_t stark_set_kernel_attributes();
 
+// DEEP row combination: S column chunks per revealed row (S * k threads, <= 256), LDS for the
+// weights (main: 3 words per column, aux: 9 per column) and the S x k chunk sums.
+inline uint32_t deep_chunks(const StarkDims& d) {
+    uint32_t S = 256 / d.num_checks;
+    return S < 1 ? 1 : (S > 8 ? 8 : S);
+}
+inline size_t deep_lds_bytes(const StarkDims& d) {
+    return (size_t)(3 * d.num_main + 9 * d.num_aux) * 8 + (size_t)deep_chunks(d) * d.num_checks * 24;
+}
+
 }  // namespace nhip

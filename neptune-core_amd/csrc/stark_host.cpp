@@ -389,7 +389,8 @@ bool dims_from(const nhip_stark_params* sp, const nhip_air* air, Dims& D) {
     if (sp->log2_fri_expansion < 1 || sp->log2_fri_expansion > 8) return false;
     if (sp->num_main != air->dims_air.num_main || sp->num_aux != air->dims_air.num_aux) return false;
     if (sp->num_quotient_segments < 1 || sp->num_quotient_segments > 64) return false;
-    if (sp->num_main + sp->num_aux > 512) return false;  // DEEP kernel: <= 8 row columns per lane
+    // DEEP kernel: < 2^11 limb products per accumulator (M + 3A terms), weights in LDS
+    if (sp->num_main + 3ull * sp->num_aux >= 2048) return false;
     StarkDims& d = D.d;
     d.num_main = sp->num_main;
     d.num_aux = sp->num_aux;
@@ -401,6 +402,7 @@ bool dims_from(const nhip_stark_params* sp, const nhip_air* air, Dims& D) {
     d.num_sampled = air->dims_air.num_sampled;
     d.num_constraints = air->dims_air.num_constraints;
     D.expansion = 1u << sp->log2_fri_expansion;
+    if (deep_lds_bytes(d) > 160 * 1024 - 8192) return false;
     // the last FRI codeword has at most 2^(floor(log2 k) + 1 + log2 expansion) XFEs; bound its
     // Merkle-tree scratch (n x max_len digests)
     if ((1ull << (log2u(d.num_checks) + 1 + d.log2_expansion)) > 4096) return false;

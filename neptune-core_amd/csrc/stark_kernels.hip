@@ -796,28 +796,76 @@ __global__ void __launch_bounds__(256) k_fri(const uint64_t* __restrict__ words,
 }
 
 // ------------------------------------------------------------------ DEEP
-// One workgroup per proof.  Phase 1: wave w forms the linear combinations of revealed rows
-// j = w, w + 4, ... (lanes split the row; the row weights stay in registers).  Proof words are
-// canonical and the weights raw Montgomery, so mont_mul(weight, word) is already the canonical
-// product: the row sums stay canonical and only the final sum is converted.  Phase 2: lane j takes
-// row j's three DEEP terms (x - z, x - z*w_trace, x - z^Q; x from k_fri), inverts their product
-// once (Montgomery's trick) and compares the recombined value with the FRI round-0 leaf.
-static constexpr uint32_t DEEP_MAX_COLS_PER_LANE = 8;  // (M + A) <= 512
+// One workgroup per proof, thread (s, j) = chunk s of the columns of revealed row j (S chunks per
+// row, S * k <= 256).  Row linear combinations sum_c w_c * row_c are accumulated lazily: the proof
+// words are canonical, the weights raw Montgomery (w R); each weight is split into 32-bit halves and
+// each word into 16-bit limbs, so every partial product is < 2^48 and a 64-bit accumulator per
+// (coefficient, weight half, limb) absorbs up to 2^16 of them without carries (one v_mad_u64_u32
+// per partial product).  The accumulators are folded and reduced once per thread; the result,
+// R * sum w x mod p, is already the raw Montgomery word of the sum.  An XFE product w * x is
+// sum_m x_m * (w X^m) with w X = (-w2, w0 + w2, w1) and w X^2 = (-w1, w1 - w2, w0 + w2) (X^3 = X - 1),
+// precomputed per aux column in LDS.  Then thread j takes row j's three DEEP terms (x - z,
+// x - z w_trace, x - z^Q; x from k_fri), inverts their product once (Montgomery's trick), and
+// compares the recombined value with the FRI round-0 leaf.
+typedef unsigned __int128 u128_t;
+
+// lo + hi * 2^64 mod p for hi < 2^44
+__device__ __forceinline__ uint64_t reduce_u108(u128_t y) {
+    const uint64_t y0 = (uint64_t)y, y1 = (uint64_t)(y >> 64);
+    const uint64_t r = reduce96(y0, (uint32_t)y1);
+    return gl_sub(r, y1 >> 32);  // 2^96 == -1 (mod p)
+}
+
+// (sum_{h<2, q<4} a[h][q] * 2^(32h + 16q)) mod p, a < 2^59
+__device__ __forceinline__ uint64_t limb_reduce(const uint64_t (&a)[8]) {
+    const u128_t U = (u128_t)a[0] + ((u128_t)a[1] << 16) + ((u128_t)a[2] << 32) + ((u128_t)a[3] << 48);
+    const u128_t W = (u128_t)a[4] + ((u128_t)a[5] << 16) + ((u128_t)a[6] << 32) + ((u128_t)a[7] << 48);
+    const uint64_t ur = reduce_u108(U), wr = reduce_u108(W);
+    return gl_add(ur, reduce96(wr << 32, (uint32_t)(wr >> 32)));  // + wr * 2^32
+}
+
+__device__ __forceinline__ void limb_mac(uint64_t (&a)[8], uint64_t w, const uint32_t (&xq)[4]) {
+    const uint32_t w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        a[q] += (uint64_t)w0 * xq[q];
+        a[4 + q] += (uint64_t)w1 * xq[q];
+    }
+}
+
+__device__ __forceinline__ void limbs16(uint64_t x, uint32_t (&xq)[4]) {
+    xq[0] = (uint32_t)x & 0xFFFFu;
+    xq[1] = (uint32_t)x >> 16;
+    xq[2] = (uint32_t)(x >> 32) & 0xFFFFu;
+    xq[3] = (uint32_t)(x >> 48);
+}
 
 __global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
-                                              uint32_t n_proofs, StarkDims dims, const uint64_t* __restrict__ xs,
-                                              const uint64_t* __restrict__ xdom, const uint64_t* __restrict__ ood,
-                                              uint32_t* __restrict__ fail) {
-    __shared__ Xfe s_row[MAX_CHECKS], s_quot[MAX_CHECKS];
+                                              uint32_t n_proofs, StarkDims dims, uint32_t S,
+                                              const uint64_t* __restrict__ xs, const uint64_t* __restrict__ xdom,
+                                              const uint64_t* __restrict__ ood, uint32_t* __restrict__ fail) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t M = dims.num_main, A = dims.num_aux, Q = dims.num_quot_seg, k = dims.num_checks;
+    uint64_t* wm = reinterpret_cast<uint64_t*>(smem);  // [M][3] main weights (raw)
+    uint64_t* wa = wm + 3 * M;                         // [A][3 m][3 coeff] aux weights w X^m (raw)
+    Xfe* part = reinterpret_cast<Xfe*>(wa + 9 * A);    // [S][k] chunk sums (raw)
+    __shared__ Xfe s_quot[MAX_CHECKS];
     __shared__ Xfe s_at[3];
     const uint32_t p = blockIdx.x, tid = threadIdx.x;
     if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
     const ProofDesc& d = desc[p];
     const SampleLayout sl = SampleLayout::of(dims, d.R);
     const uint64_t xb = d.xs_off * 3;
-    const uint32_t M = dims.num_main, A = dims.num_aux, Q = dims.num_quot_seg, k = dims.num_checks;
-    const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
-    if (tid == 64) {
+    const uint64_t* __restrict__ lw = xs + xb + 3ull * sl.lin_w;
+    for (uint32_t i = tid; i < 3 * M; i += blockDim.x) wm[i] = lw[i];
+    for (uint32_t c = tid; c < A; c += blockDim.x) {
+        const uint64_t w0 = lw[3 * (M + c)], w1 = lw[3 * (M + c) + 1], w2 = lw[3 * (M + c) + 2];
+        uint64_t* o = wa + 9 * c;
+        o[0] = w0, o[1] = w1, o[2] = w2;
+        o[3] = gl_sub(0, w2), o[4] = gl_add(w0, w2), o[5] = w1;
+        o[6] = gl_sub(0, w1), o[7] = gl_sub(w1, w2), o[8] = gl_add(w0, w2);
+    }
+    if (tid == blockDim.x - 1) {
         // evaluation points of the three DEEP terms: z, z * w_trace, z^Q
         const Xfe z = ld_xfe_raw(xs, xb + 3ull * sl.z);
         s_at[0] = z;
@@ -826,45 +874,50 @@ __global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words
         for (uint32_t q = 0; q < Q; ++q) zq = x_mul(zq, z);
         s_at[2] = zq;
     }
-    Xfe wcol[DEEP_MAX_COLS_PER_LANE];
+    __syncthreads();
+    const uint32_t s = tid / k, j = tid - s * k;
+    if (s < S) {
+        uint64_t acc[3][8];
 #pragma unroll
-    for (uint32_t i = 0; i < DEEP_MAX_COLS_PER_LANE; ++i) {
-        const uint32_t c = lane + 64 * i;
-        wcol[i] = c < M + A ? ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + c)) : x_zero();
-    }
-    const Xfe wq = lane < Q ? ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + lane)) : x_zero();
-    for (uint32_t j = wave; j < k; j += nwaves) {
-        Xfe acc = x_zero();
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[c][q] = 0;
         const uint64_t* __restrict__ mrow = words + d.main_rows_off + (uint64_t)j * M;
-        const uint64_t arow = d.aux_rows_off + (uint64_t)j * 3 * A;
+        for (uint32_t c = s * M / S, ce = (s + 1) * M / S; c < ce; ++c) {
+            uint32_t xq[4];
+            limbs16(mrow[c], xq);
+            limb_mac(acc[0], wm[3 * c], xq);
+            limb_mac(acc[1], wm[3 * c + 1], xq);
+            limb_mac(acc[2], wm[3 * c + 2], xq);
+        }
+        const uint64_t* __restrict__ arow = words + d.aux_rows_off + (uint64_t)j * 3 * A;
+        for (uint32_t c = s * A / S, ce = (s + 1) * A / S; c < ce; ++c) {
+            const uint64_t* ww = wa + 9 * c;
 #pragma unroll
-        for (uint32_t i = 0; i < DEEP_MAX_COLS_PER_LANE; ++i) {
-            const uint32_t c = lane + 64 * i;
-            if (c < M) {
-                acc = x_add(acc, x_scale(wcol[i], mrow[c]));
-            } else if (c < M + A) {
-                acc = x_add(acc, x_mul(wcol[i], ld_xfe_raw(words, arow + 3ull * (c - M))));
+            for (int m = 0; m < 3; ++m) {
+                uint32_t xq[4];
+                limbs16(arow[3 * c + m], xq);
+                limb_mac(acc[0], ww[3 * m], xq);
+                limb_mac(acc[1], ww[3 * m + 1], xq);
+                limb_mac(acc[2], ww[3 * m + 2], xq);
             }
         }
-        Xfe qv = x_zero();
-        if (lane < Q) qv = x_mul(wq, ld_xfe_raw(words, d.quot_rows_off + (uint64_t)j * 3 * Q + 3ull * lane));
-        for (int s = 32; s > 0; s >>= 1) {
-            acc.c0 = gl_add(acc.c0, __shfl_xor(acc.c0, s));
-            acc.c1 = gl_add(acc.c1, __shfl_xor(acc.c1, s));
-            acc.c2 = gl_add(acc.c2, __shfl_xor(acc.c2, s));
-            qv.c0 = gl_add(qv.c0, __shfl_xor(qv.c0, s));
-            qv.c1 = gl_add(qv.c1, __shfl_xor(qv.c1, s));
-            qv.c2 = gl_add(qv.c2, __shfl_xor(qv.c2, s));
-        }
-        if (lane == 0) {
-            s_row[j] = {to_mont(acc.c0), to_mont(acc.c1), to_mont(acc.c2)};
+        part[s * k + j] = {limb_reduce(acc[0]), limb_reduce(acc[1]), limb_reduce(acc[2])};
+        if (s == S - 1) {
+            // quotient segments: sum_q w_q * seg_q (canonical products of raw weights and words)
+            Xfe qv = x_zero();
+            for (uint32_t q = 0; q < Q; ++q)
+                qv = x_add(qv, x_mul(ld_xfe_raw(lw, 3ull * (M + A + q)),
+                                     ld_xfe_raw(words, d.quot_rows_off + (uint64_t)j * 3 * Q + 3ull * q)));
             s_quot[j] = {to_mont(qv.c0), to_mont(qv.c1), to_mont(qv.c2)};
         }
     }
     __syncthreads();
     uint32_t f = 0;
-    for (uint32_t j = tid; j < k; j += blockDim.x) {
-        const Xfe x = x_lift(xdom[(uint64_t)p * k + j]);
+    for (uint32_t j2 = tid; j2 < k; j2 += blockDim.x) {
+        Xfe row = part[j2];
+        for (uint32_t q = 1; q < S; ++q) row = x_add(row, part[q * k + j2]);
+        const Xfe x = x_lift(xdom[(uint64_t)p * k + j2]);
         const Xfe d0 = x_sub(x, s_at[0]), d1 = x_sub(x, s_at[1]), d2 = x_sub(x, s_at[2]);
         const Xfe d01 = x_mul(d0, d1);
         const Xfe prod = x_mul(d01, d2);
@@ -878,12 +931,12 @@ __global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words
         const Xfe inv0 = x_mul(inv01, d1);  // 1 / d0
         const Xfe inv1 = x_mul(inv01, d0);  // 1 / d1
         const uint64_t* __restrict__ oo = ood + (uint64_t)p * 9;
-        const uint64_t wd = xb + 3ull * (sl.lin_w + M + A + Q);
-        const Xfe t0 = x_mul(x_mul(x_sub(s_row[j], ld_xfe_raw(oo, 0)), inv0), ld_xfe_raw(xs, wd));
-        const Xfe t1 = x_mul(x_mul(x_sub(s_row[j], ld_xfe_raw(oo, 3)), inv1), ld_xfe_raw(xs, wd + 3));
-        const Xfe t2 = x_mul(x_mul(x_sub(s_quot[j], ld_xfe_raw(oo, 6)), inv2), ld_xfe_raw(xs, wd + 6));
+        const uint64_t* __restrict__ wd = lw + 3ull * (M + A + Q);
+        const Xfe t0 = x_mul(x_mul(x_sub(row, ld_xfe_raw(oo, 0)), inv0), ld_xfe_raw(wd, 0));
+        const Xfe t1 = x_mul(x_mul(x_sub(row, ld_xfe_raw(oo, 3)), inv1), ld_xfe_raw(wd, 3));
+        const Xfe t2 = x_mul(x_mul(x_sub(s_quot[j2], ld_xfe_raw(oo, 6)), inv2), ld_xfe_raw(wd, 6));
         const Xfe deep = x_add(x_add(t0, t1), t2);
-        const Xfe fri_v = ld_xfe_canon(words, d.fri[0].leaves_off + 3ull * j);
+        const Xfe fri_v = ld_xfe_canon(words, d.fri[0].leaves_off + 3ull * j2);
         if (!x_eq(deep, fri_v)) f |= FAIL_DEEP;
     }
     if (f) atomicOr(&fail[p], f);
@@ -921,7 +974,11 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     mark(6, sa);
     hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
     mark(7, sa);
-    hipLaunchKernelGGL(k_deep, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.xdom, b.ood, b.fail);
+    {
+        const uint32_t S = deep_chunks(b.dims);
+        hipLaunchKernelGGL(k_deep, dim3(n), dim3(S * k), deep_lds_bytes(b.dims), sa, b.words, b.desc, n, b.dims, S,
+                           b.xs, b.xdom, b.ood, b.fail);
+    }
     mark(8, sa);
     // ---- main stream: VALU-bound hashing
     {
@@ -960,6 +1017,8 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
 
 hipError_t stark_set_kernel_attributes() {
     hipError_t e = hipFuncSetAttribute((const void*)k_ood_air, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void*)k_deep, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
     if (e != hipSuccess) return e;
     return e;
 }
