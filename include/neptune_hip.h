@@ -132,8 +132,8 @@ typedef struct {
 
 typedef struct {
     uint64_t num_proofs, proof_words;
-    uint64_t tip5_perms_static;  /* Fiat-Shamir + row hashing + last-codeword trees (from the proof shapes) */
-    uint64_t tip5_perms_merkle;  /* authentication-structure hash_pairs actually performed (device-counted) */
+    uint64_t tip5_perms_static;  /* Fiat-Shamir + row hashing (from the proof shapes) */
+    uint64_t tip5_perms_merkle;  /* authentication-structure hash_pairs performed (device-counted) + last-codeword trees */
     double ms_decode, ms_upload;  /* host */
     double ms_fiat_shamir, ms_row_hash, ms_merkle, ms_ood_air, ms_fri, ms_deep, ms_device_total; /* device */
     double ms_merkle_hash;          /* the per-level hash_pair launches inside ms_merkle */
