@@ -158,6 +158,11 @@ int nhip_verify_batch(nhip_ctx *ctx, nhip_air *air, const nhip_stark_params *par
 int nhip_batch_prepare(nhip_ctx *ctx, nhip_air *air, const nhip_stark_params *params, const nhip_claim *claims,
                        const nhip_proof *proofs, size_t n, nhip_batch **out);
 int nhip_batch_run(nhip_ctx *ctx, nhip_batch *batch, uint8_t *verdicts, uint8_t *all_ok);
+/* Asynchronous form of nhip_batch_run: launch enqueues every phase on the batch's own streams and
+ * returns; wait blocks until that batch is done.  Batches launched back to back run concurrently
+ * (e.g. two half-batches overlap each other's latency-bound tails). */
+int nhip_batch_launch(nhip_ctx *ctx, nhip_batch *batch);
+int nhip_batch_wait(nhip_ctx *ctx, nhip_batch *batch, uint8_t *verdicts, uint8_t *all_ok);
 int nhip_batch_stats(const nhip_batch *batch, nhip_stats *stats);
 /* Samples squeezed for proof `proof` in squeeze order (challenges, quotient weights, z, linear-
  * combination weights, FRI folding challenges, last-round indeterminate) as canonical XFE

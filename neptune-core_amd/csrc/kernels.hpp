@@ -24,6 +24,8 @@ static constexpr uint32_t AIR_LDS_HEADER = (256 + 4 + 4) * 24 + 16;  // red, zin
 // live in MP_SHARDS shards (shard = proof index % MP_SHARDS) so the per-level slot reservations of
 // the plan workgroups spread over MP_SHARDS counters instead of contending on one.
 static constexpr uint32_t MP_SHARDS = 16;
+// levels with at most this many hash ops run the 16-lane-row Tip5 (latency-bound regime)
+static constexpr uint64_t MP_WIDE_MAX_OPS = 48 * 1024;
 struct MpRoot {
     uint64_t code;  // source code of the tree's final node, ~0 = no check (skipped or already failed)
     uint64_t root_off;

@@ -364,8 +364,10 @@ struct nhip_batch {
     uint32_t* d_fail_init = nullptr;
     uint64_t* d_perm_counter = nullptr;
     StarkPhaseTimer tm{};
-    hipStream_t aux = nullptr;  // second stream of the batch (latency-bound phase chain)
-    bool timed = false;
+    hipStream_t main = nullptr;  // hashing chain (rows -> Merkle levels -> roots -> verdicts)
+    hipStream_t aux = nullptr;   // latency-bound chain (Fiat-Shamir -> plan -> OOD -> FRI -> DEEP)
+    uint8_t* h_out = nullptr;    // pinned: [perm counter (8 B) | verdicts (n B)]
+    bool timed = false, in_flight = false;
     struct {
         double fs, rows, plan, hash, roots, ood, fri, deep, total;
     } ph{};
@@ -708,30 +710,48 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     return NHIP_OK;
 }
 
-int nhip_batch_run(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* all_ok) {
+// Enqueue every device phase of the batch on the batch's own two streams (no host wait).  Batches
+// launched back to back run concurrently on the device.
+int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
     if (!ctx || !b) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
     (void)hipSetDevice(b->device);
-    hipStream_t st = nhip_internal_stream(ctx);
+    if (b->in_flight) return NHIP_ERR_ARG;
+    if (!b->timed) {
+        for (int i = 0; i < STARK_EVENTS; ++i)
+            if (hipEventCreate(&b->tm.ev[i]) != hipSuccess) return NHIP_ERR_HIP;
+        if (hipStreamCreateWithFlags(&b->main, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
+        if (hipStreamCreateWithFlags(&b->aux, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
+        if (hipHostMalloc((void**)&b->h_out, (size_t)b->dev.n_proofs + 16, hipHostMallocDefault) != hipSuccess)
+            return NHIP_ERR_OOM;
+        b->timed = true;
+    }
+    hipStream_t st = b->main;
     const uint32_t n = b->dev.n_proofs;
     hipError_t e = hipSuccess;
     if (n) e = hipMemcpyAsync(b->dev.fail, b->d_fail_init, n * 4, hipMemcpyDeviceToDevice, st);
     if (e == hipSuccess) e = hipMemsetAsync(b->d_perm_counter, 0, 8, st);
     if (e == hipSuccess && b->dev.mp.levels) e = hipMemsetAsync(b->dev.mp.counter, 0, (size_t)b->dev.mp.levels * MP_SHARDS * 4, st);
     if (e != hipSuccess) return hipfail(e);
-    if (!b->timed) {
-        for (int i = 0; i < STARK_EVENTS; ++i)
-            if (hipEventCreate(&b->tm.ev[i]) != hipSuccess) return NHIP_ERR_HIP;
-        if (hipStreamCreateWithFlags(&b->aux, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
-        b->timed = true;
-    }
     e = launch_stark_phases(b->dev, st, b->aux, &b->tm);
     if (e != hipSuccess) return hipfail(e);
-    std::vector<uint8_t> v(n);
-    if (n) e = hipMemcpyAsync(v.data(), b->dev.verdicts, n, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(&b->merkle_perms, b->d_perm_counter, 8, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipMemcpyAsync(b->h_out, b->d_perm_counter, 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && n) e = hipMemcpyAsync(b->h_out + 8, b->dev.verdicts, n, hipMemcpyDeviceToHost, st);
     if (e != hipSuccess) return hipfail(e);
+    b->in_flight = true;
+    return NHIP_OK;
+}
+
+// Wait for a launched batch; verdicts (n bytes, nullable) and the batch AND (nullable).
+int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* all_ok) {
+    if (!ctx || !b) return NHIP_ERR_ARG;
+    if (!b->in_flight) return NHIP_ERR_ARG;
+    (void)hipSetDevice(b->device);
+    hipError_t e = hipStreamSynchronize(b->main);
+    b->in_flight = false;
+    if (e != hipSuccess) return hipfail(e);
+    const uint32_t n = b->dev.n_proofs;
+    std::memcpy(&b->merkle_perms, b->h_out, 8);
     b->merkle_perms += b->H.perms_lcw;
     // phases overlap (two streams): each is timed from the event its inputs wait on
     auto el = [&](int a, int c) {
@@ -739,22 +759,31 @@ int nhip_batch_run(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* all
         (void)hipEventElapsedTime(&ms, b->tm.ev[a], b->tm.ev[c]);
         return (double)ms;
     };
-    b->ph.fs = el(0, 1);
-    b->ph.rows = el(0, 2);
-    b->ph.plan = el(1, 3);
-    b->ph.hash = std::min(el(2, 4), el(3, 4));
-    b->ph.roots = el(4, 5);
-    b->ph.ood = el(3, 6);
-    b->ph.fri = el(6, 7);
-    b->ph.deep = el(7, 8);
-    b->ph.total = el(0, 9);
-    if (verdicts && n) std::memcpy(verdicts, v.data(), n);
+    if (n) {
+        b->ph.fs = el(0, 1);
+        b->ph.rows = el(0, 2);
+        b->ph.plan = el(1, 3);
+        b->ph.hash = std::min(el(2, 4), el(3, 4));
+        b->ph.roots = el(4, 5);
+        b->ph.ood = el(3, 6);
+        b->ph.fri = el(6, 7);
+        b->ph.deep = el(7, 8);
+        b->ph.total = el(0, 9);
+    }
+    const uint8_t* v = b->h_out + 8;
+    if (verdicts && n) std::memcpy(verdicts, v, n);
     if (all_ok) {
         uint8_t a = 1;
         for (uint32_t i = 0; i < n; ++i) a &= v[i];
         *all_ok = a;
     }
     return NHIP_OK;
+}
+
+int nhip_batch_run(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* all_ok) {
+    const int rc = nhip_batch_launch(ctx, b);
+    if (rc) return rc;
+    return nhip_batch_wait(ctx, b, verdicts, all_ok);
 }
 
 int nhip_batch_stats(const nhip_batch* b, nhip_stats* s) {
@@ -781,7 +810,7 @@ int nhip_batch_stats(const nhip_batch* b, nhip_stats* s) {
 
 int nhip_batch_transcript(nhip_ctx* ctx, const nhip_batch* b, size_t proof, uint64_t* xfe_out, size_t xfe_cap,
                           uint32_t* idx_out, size_t idx_cap, uint32_t* fail_out, size_t* n_xfe) {
-    if (!ctx || !b || proof >= b->dev.n_proofs) return NHIP_ERR_ARG;
+    if (!ctx || !b || proof >= b->dev.n_proofs || b->in_flight) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
     (void)hipSetDevice(b->device);
     hipStream_t st = nhip_internal_stream(ctx);
@@ -810,7 +839,10 @@ void nhip_batch_destroy(nhip_batch* b) {
     (void)hipSetDevice(b->device);
     if (b->timed)
         for (int i = 0; i < STARK_EVENTS; ++i) (void)hipEventDestroy(b->tm.ev[i]);
+    if (b->in_flight && b->main) (void)hipStreamSynchronize(b->main);
+    if (b->main) (void)hipStreamDestroy(b->main);
     if (b->aux) (void)hipStreamDestroy(b->aux);
+    if (b->h_out) (void)hipHostFree(b->h_out);
     if (b->dmem) (void)hipFree(b->dmem);
     delete b;
 }

@@ -527,6 +527,50 @@ __global__ void __launch_bounds__(256) k_mp_hash(const uint64_t* __restrict__ wo
     for (int q = 0; q < 5; ++q) o[q] = s[q];
 }
 
+// Small levels (the last levels of the tallest trees): a lane-per-op permutation is a ~20 us
+// dependent instruction chain however few ops there are, so these levels use the 16-lane row
+// Tip5 (one op per DPP row, ~8x shorter chain) instead.
+__device__ __forceinline__ uint64_t mp_load_word(uint64_t code, uint32_t e, const uint64_t* __restrict__ words,
+                                                 const uint64_t* __restrict__ dig, const uint64_t* __restrict__ arena) {
+    const uint64_t t = code >> 62, v = code & MPS_MASK;
+    if (t == MPS_ARENA) return arena[5 * v + e];
+    if (t == MPS_DIG) return dig[5 * v + e];
+    if (t == MPS_AUTH) return to_mont(words[v + e]);
+    return e < 3 ? to_mont(words[v + e]) : 0ull;  // XFE leaf [c0, c1, c2, 0, 0]
+}
+
+__global__ void __launch_bounds__(256) k_mp_hash_wide(const uint64_t* __restrict__ words,
+                                                      const uint64_t* __restrict__ dig, MpPlan plan, uint32_t lvl) {
+    __shared__ Tip5Lds t5;
+    __shared__ uint64_t s_base[MP_SHARDS + 1];
+    __shared__ uint32_t s_cnt[MP_SHARDS];
+    if (threadIdx.x < MP_SHARDS) {
+        s_base[threadIdx.x] = plan.shard_base[lvl * MP_SHARDS + threadIdx.x];
+        s_cnt[threadIdx.x] = plan.counter[lvl * MP_SHARDS + threadIdx.x];
+    }
+    if (threadIdx.x == 0)
+        s_base[MP_SHARDS] = plan.shard_base[(lvl + 1) * MP_SHARDS - 1] + plan.shard_cap[(lvl + 1) * MP_SHARDS - 1];
+    tip5_lds_init(t5);  // includes the barrier
+    const uint32_t e = threadIdx.x & 15u;
+    const uint64_t g = s_base[0] + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4);
+    // every test below is uniform within the 16-lane row (one op per row)
+    if (g >= s_base[MP_SHARDS]) return;
+    uint32_t sh = 0;
+#pragma unroll
+    for (uint32_t q = 1; q < MP_SHARDS; ++q) sh += g >= s_base[q] ? 1u : 0u;
+    if (g - s_base[sh] >= s_cnt[sh]) return;
+    const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
+    if (lc == MPS_NONE) return;
+    uint64_t rcs[TIP5_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < TIP5_ROUNDS; ++r) rcs[r] = c_tip5_rc_raw[r * 16 + e];
+    uint64_t s = MONT_ONE;
+    if (e < 5) s = mp_load_word(lc, e, words, dig, plan.arena);
+    else if (e < 10) s = mp_load_word(rc, e - 5, words, dig, plan.arena);
+    s = tip5_permute_wide(s, e, rcs, t5.lut);
+    if (e < 5) plan.arena[5 * g + e] = s;
+}
+
 // One lane per (proof, tree): duplicate leaf indices carry equal digests, final node == root.
 // Lanes n_records.. check the last codeword's Merkle root, one per proof.
 __global__ void k_mp_roots(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
@@ -999,8 +1043,12 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         const uint64_t per = b.max_lcw >> (l + 1);
         const uint32_t lcw_blocks = (uint32_t)((per * n + 255) / 256);
         if (mp_blocks + lcw_blocks == 0) continue;
-        hipLaunchKernelGGL(k_mp_hash, dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, b.words, b.dig, b.mp, l, mp_blocks,
-                           b.desc, n, b.fail_init, lcw);
+        if (lcw_blocks == 0 && cap <= MP_WIDE_MAX_OPS)
+            hipLaunchKernelGGL(k_mp_hash_wide, dim3((unsigned)((cap * 16 + 255) / 256)), dim3(256), 0, st, b.words,
+                               b.dig, b.mp, l);
+        else
+            hipLaunchKernelGGL(k_mp_hash, dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, b.words, b.dig, b.mp, l,
+                               mp_blocks, b.desc, n, b.fail_init, lcw);
         ++launches;
     }
     tm->mp_hash_launches = launches;

@@ -90,6 +90,8 @@ SIGNATURES = {
     "nhip_batch_prepare": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof),
                             _sz, _pp], ctypes.c_int),
     "nhip_batch_run": ([_vp, _vp, _u8p, ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
+    "nhip_batch_launch": ([_vp, _vp], ctypes.c_int),
+    "nhip_batch_wait": ([_vp, _vp, _u8p, ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
     "nhip_batch_stats": ([_vp, ctypes.POINTER(Stats)], ctypes.c_int),
     "nhip_batch_transcript": ([_vp, _vp, _sz, _u64p, _sz, ctypes.POINTER(ctypes.c_uint32), _sz,
                                ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),

@@ -118,6 +118,16 @@ class Batch:
         check(self.ctx.lib.nhip_batch_run(self.ctx.handle, self.handle, v, ctypes.byref(ok)), "nhip_batch_run")
         return v[:self.n], bool(ok.value)
 
+    def launch(self) -> None:
+        """Enqueue the device phases on the batch's own streams (returns immediately)."""
+        check(self.ctx.lib.nhip_batch_launch(self.ctx.handle, self.handle), "nhip_batch_launch")
+
+    def wait(self) -> Tuple[np.ndarray, bool]:
+        v = np.zeros(max(self.n, 1), dtype=np.uint8)
+        ok = ctypes.c_uint8(0)
+        check(self.ctx.lib.nhip_batch_wait(self.ctx.handle, self.handle, v, ctypes.byref(ok)), "nhip_batch_wait")
+        return v[:self.n], bool(ok.value)
+
     def stats(self) -> dict:
         s = _lib.Stats()
         check(self.ctx.lib.nhip_batch_stats(self.handle, ctypes.byref(s)), "nhip_batch_stats")
