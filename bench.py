@@ -208,7 +208,7 @@ def main():
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="split the per-GPU batch into this many sub-batches (whole collections) launched "
-                         "back to back on their own streams (measured slower: 2 -> 9.7 ms vs 6.6 ms, the 4 HW "
+                         "back to back on their own streams (measured slower: 2 -> 9.7 ms vs 6.6 ms, probably because the 4 HW "
                          "queues per process serialize the extra streams; DESIGN.md §3)")
     args = ap.parse_args()
 

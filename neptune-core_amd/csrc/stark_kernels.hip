@@ -852,6 +852,7 @@ __global__ void __launch_bounds__(256) k_fri(const uint64_t* __restrict__ words,
 // x - z w_trace, x - z^Q; x from k_fri), inverts their product once (Montgomery's trick), and
 // compares the recombined value with the FRI round-0 leaf.
 typedef unsigned __int128 u128_t;
+static constexpr uint32_t DEEP_UNROLL = 8;
 
 // lo + hi * 2^64 mod p for hi < 2^44
 __device__ __forceinline__ uint64_t reduce_u108(u128_t y) {
@@ -926,8 +927,25 @@ __global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words
         for (int c = 0; c < 3; ++c)
 #pragma unroll
             for (int q = 0; q < 8; ++q) acc[c][q] = 0;
+        // the row words are read DEEP_UNROLL at a time so that many loads are in flight per lane
+        // (the lanes of a wave read different rows: the kernel is load-latency-bound otherwise)
         const uint64_t* __restrict__ mrow = words + d.main_rows_off + (uint64_t)j * M;
-        for (uint32_t c = s * M / S, ce = (s + 1) * M / S; c < ce; ++c) {
+        uint32_t c = s * M / S;
+        const uint32_t ce = (s + 1) * M / S;
+        for (; c + DEEP_UNROLL <= ce; c += DEEP_UNROLL) {
+            uint64_t xv[DEEP_UNROLL];
+#pragma unroll
+            for (uint32_t u = 0; u < DEEP_UNROLL; ++u) xv[u] = mrow[c + u];
+#pragma unroll
+            for (uint32_t u = 0; u < DEEP_UNROLL; ++u) {
+                uint32_t xq[4];
+                limbs16(xv[u], xq);
+                limb_mac(acc[0], wm[3 * (c + u)], xq);
+                limb_mac(acc[1], wm[3 * (c + u) + 1], xq);
+                limb_mac(acc[2], wm[3 * (c + u) + 2], xq);
+            }
+        }
+        for (; c < ce; ++c) {
             uint32_t xq[4];
             limbs16(mrow[c], xq);
             limb_mac(acc[0], wm[3 * c], xq);
@@ -935,15 +953,25 @@ __global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words
             limb_mac(acc[2], wm[3 * c + 2], xq);
         }
         const uint64_t* __restrict__ arow = words + d.aux_rows_off + (uint64_t)j * 3 * A;
-        for (uint32_t c = s * A / S, ce = (s + 1) * A / S; c < ce; ++c) {
-            const uint64_t* ww = wa + 9 * c;
+        uint32_t ca = s * A / S;
+        const uint32_t cae = (s + 1) * A / S;
+        for (; ca < cae; ca += DEEP_UNROLL / 2) {
+            const uint32_t nc = cae - ca < DEEP_UNROLL / 2 ? cae - ca : DEEP_UNROLL / 2;
+            uint64_t xv[3 * (DEEP_UNROLL / 2)];
 #pragma unroll
-            for (int m = 0; m < 3; ++m) {
-                uint32_t xq[4];
-                limbs16(arow[3 * c + m], xq);
-                limb_mac(acc[0], ww[3 * m], xq);
-                limb_mac(acc[1], ww[3 * m + 1], xq);
-                limb_mac(acc[2], ww[3 * m + 2], xq);
+            for (uint32_t u = 0; u < 3 * (DEEP_UNROLL / 2); ++u) xv[u] = u < 3 * nc ? arow[3 * ca + u] : 0ull;
+#pragma unroll
+            for (uint32_t u = 0; u < DEEP_UNROLL / 2; ++u) {
+                if (u >= nc) break;
+                const uint64_t* ww = wa + 9 * (ca + u);
+#pragma unroll
+                for (int m = 0; m < 3; ++m) {
+                    uint32_t xq[4];
+                    limbs16(xv[3 * u + m], xq);
+                    limb_mac(acc[0], ww[3 * m], xq);
+                    limb_mac(acc[1], ww[3 * m + 1], xq);
+                    limb_mac(acc[2], ww[3 * m + 2], xq);
+                }
             }
         }
         part[s * k + j] = {limb_reduce(acc[0]), limb_reduce(acc[1]), limb_reduce(acc[2])};
