@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "stark.hpp"
+#include "xfe.hpp"
 
 namespace nhip {
 
@@ -18,7 +19,7 @@ hipError_t launch_mtree_verify(const uint64_t* d_roots, int per_path_root, const
                                uint8_t* d_verdicts, hipStream_t st);
 
 // ---- batched STARK verifier (stark_kernels.hip)
-static constexpr uint32_t AIR_LDS_HEADER = (256 + 4 + 4) * 24 + 16;  // red, zinv, derived, flag
+static constexpr uint32_t AIR_LDS_HEADER = (256 + 4 + 4 + 4) * 24 + 16;  // red, zinv, derived, misc, flag
 
 // Level-synchronous Merkle multiproof plan (see k_mp_plan in stark_kernels.hip).  Ops of level l
 // live in MP_SHARDS shards (shard = proof index % MP_SHARDS) so the per-level slot reservations of
@@ -62,12 +63,11 @@ struct StarkBatchDev {
     unsigned long long* perm_counter;  // Merkle hash_pairs performed (device-counted)
     MpPlan mp;
     const uint64_t* mp_cap_host;  // host: op capacity per level (launch sizes)
-    const AirNode* air_nodes;
-    const uint32_t* air_level_nodes;
-    const uint32_t* air_level_off;
+    const OodIns* air_prog;        // compiled AIR (OodIns per level)
+    const uint32_t* air_prog_off;  // [n_levels + 1]
     uint32_t air_n_levels;
-    const uint32_t* air_cons;
-    uint4 air_cons_off;
+    const Xfe* air_consts;         // constant table (raw Montgomery)
+    uint4 air_cons_off;            // constraint-type boundaries
     size_t air_lds_bytes;
 };
 

@@ -346,12 +346,18 @@ void decode_proof(HostBatch& B, const nhip_claim& claim, const nhip_proof& proof
 struct nhip_air {
     StarkDims dims_air{};  // num_main, num_aux, num_sampled, num_constraints filled
     std::vector<AirNode> nodes;
-    std::vector<uint32_t> level_nodes, level_off, cons;
+    std::vector<uint32_t> level_off;  // node-level histogram (nhip_air_info)
     uint4 cons_off{};
+    // compiled program (see OodIns in stark.hpp)
+    std::vector<OodIns> prog;
+    std::vector<uint32_t> prog_off;
+    std::vector<Xfe> consts;
+    uint32_t slots = 0;
     // device copies per context (one context per process in practice)
     nhip_ctx* dev_ctx = nullptr;
-    AirNode* d_nodes = nullptr;
-    uint32_t *d_level_nodes = nullptr, *d_level_off = nullptr, *d_cons = nullptr;
+    OodIns* d_prog = nullptr;
+    uint32_t* d_prog_off = nullptr;
+    Xfe* d_consts = nullptr;
 };
 
 struct nhip_batch {
@@ -413,17 +419,77 @@ bool dims_from(const nhip_stark_params* sp, const nhip_air* air, Dims& D) {
 
 int air_upload(nhip_ctx* ctx, nhip_air* a) {
     if (a->dev_ctx == ctx) return NHIP_OK;
-    hipError_t e = hipMalloc(&a->d_nodes, a->nodes.size() * sizeof(AirNode));
-    if (e == hipSuccess) e = hipMalloc(&a->d_level_nodes, a->level_nodes.size() * 4 + 4);
-    if (e == hipSuccess) e = hipMalloc(&a->d_level_off, a->level_off.size() * 4 + 4);
-    if (e == hipSuccess) e = hipMalloc(&a->d_cons, a->cons.size() * 4 + 4);
-    if (e == hipSuccess) e = hipMemcpy(a->d_nodes, a->nodes.data(), a->nodes.size() * sizeof(AirNode), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(a->d_level_nodes, a->level_nodes.data(), a->level_nodes.size() * 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(a->d_level_off, a->level_off.data(), a->level_off.size() * 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(a->d_cons, a->cons.data(), a->cons.size() * 4, hipMemcpyHostToDevice);
+    hipError_t e = hipMalloc(&a->d_prog, a->prog.size() * sizeof(OodIns) + 16);
+    if (e == hipSuccess) e = hipMalloc(&a->d_prog_off, a->prog_off.size() * 4 + 4);
+    if (e == hipSuccess) e = hipMalloc(&a->d_consts, a->consts.size() * sizeof(Xfe) + 24);
+    if (e == hipSuccess && !a->prog.empty())
+        e = hipMemcpy(a->d_prog, a->prog.data(), a->prog.size() * sizeof(OodIns), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(a->d_prog_off, a->prog_off.data(), a->prog_off.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess && !a->consts.empty())
+        e = hipMemcpy(a->d_consts, a->consts.data(), a->consts.size() * sizeof(Xfe), hipMemcpyHostToDevice);
     if (e != hipSuccess) return hipfail(e);
     a->dev_ctx = ctx;
     return NHIP_OK;
+}
+
+// Compile the levelized circuit into the slot program of k_ood_air (OodIns, stark.hpp).
+void air_compile(nhip_air* a, const std::vector<uint32_t>& level, uint32_t max_level,
+                 const std::vector<uint32_t>& cons) {
+    const size_t NN = a->nodes.size();
+    const uint32_t n_lv = max_level + 2;  // + one level for the accumulation of top-level constraints
+    std::vector<int64_t> last(NN, -1);
+    for (size_t i = 0; i < NN; ++i) {
+        const AirNode& nd = a->nodes[i];
+        if (nd.op == AIR_ADD || nd.op == AIR_SUB || nd.op == AIR_MUL) {
+            last[nd.a] = std::max<int64_t>(last[nd.a], level[i]);
+            last[nd.b] = std::max<int64_t>(last[nd.b], level[i]);
+        }
+    }
+    for (uint32_t c : cons) last[c] = std::max<int64_t>(last[c], (int64_t)level[c] + 1);
+    std::vector<std::vector<uint32_t>> by_level(n_lv), release(n_lv + 1);
+    for (size_t i = 0; i < NN; ++i) by_level[level[i]].push_back((uint32_t)i);
+    std::vector<uint32_t> ref(NN, 0), free_slots;
+    std::vector<std::vector<OodIns>> lv_prog(n_lv);
+    uint32_t next_slot = 0;
+    auto alloc = [&](uint32_t i) {
+        uint32_t sl;
+        if (!free_slots.empty()) {
+            sl = free_slots.back();
+            free_slots.pop_back();
+        } else {
+            sl = next_slot++;
+        }
+        ref[i] = OOD_REF_SLOT | sl;
+        release[last[i] + 1].push_back(sl);
+        return sl;
+    };
+    for (uint32_t l = 0; l < n_lv; ++l) {
+        for (uint32_t sl : release[l]) free_slots.push_back(sl);
+        for (uint32_t i : by_level[l]) {
+            const AirNode& nd = a->nodes[i];
+            if (nd.op == AIR_CONST) {
+                ref[i] = OOD_REF_CONST | (uint32_t)a->consts.size();
+                a->consts.push_back(Xfe{nd.k0, nd.k1, nd.k2});
+            } else if (nd.op == AIR_INPUT) {
+                if (last[i] < 0) continue;
+                const uint32_t sl = alloc(i);
+                lv_prog[l].push_back(OodIns{OOD_LOAD, OOD_REF_INPUT | (nd.a << 27) | nd.b, 0, sl});
+            } else {
+                if (last[i] < 0) continue;  // dead node
+                const uint32_t ra = ref[nd.a], rb = ref[nd.b];
+                const uint32_t sl = alloc(i);
+                lv_prog[l].push_back(OodIns{nd.op, ra, rb, sl});
+            }
+        }
+    }
+    for (size_t c = 0; c < cons.size(); ++c)
+        lv_prog[level[cons[c]] + 1].push_back(OodIns{OOD_ACC, ref[cons[c]], (uint32_t)c, 0});
+    a->prog_off.assign(1, 0);
+    for (uint32_t l = 0; l < n_lv; ++l) {
+        a->prog.insert(a->prog.end(), lv_prog[l].begin(), lv_prog[l].end());
+        a->prog_off.push_back((uint32_t)a->prog.size());
+    }
+    a->slots = next_slot;
 }
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -494,19 +560,17 @@ int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
     a->level_off.assign(max_level + 2, 0);
     for (uint64_t i = 0; i < NN; ++i) a->level_off[level[i] + 1]++;
     for (uint32_t l = 0; l <= max_level; ++l) a->level_off[l + 1] += a->level_off[l];
-    a->level_nodes.resize(NN);
-    std::vector<uint32_t> fillp(a->level_off.begin(), a->level_off.end() - 1);
-    for (uint64_t i = 0; i < NN; ++i) a->level_nodes[fillp[level[i]]++] = (uint32_t)i;
     const uint64_t* cw = nw + 4 * NN;
-    a->cons.resize(C);
+    std::vector<uint32_t> cons(C);
     for (uint64_t i = 0; i < C; ++i) {
         if (cw[i] >= NN) {
             delete a;
             return NHIP_ERR_ARG;
         }
-        a->cons[i] = (uint32_t)cw[i];
+        cons[i] = (uint32_t)cw[i];
     }
     a->cons_off = make_uint4((uint32_t)nc[0], (uint32_t)(nc[0] + nc[1]), (uint32_t)(nc[0] + nc[1] + nc[2]), (uint32_t)C);
+    air_compile(a, level, max_level, cons);
     *out = a;
     return NHIP_OK;
 }
@@ -514,10 +578,9 @@ int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
 void nhip_air_destroy(nhip_air* a) {
     if (!a) return;
     if (a->dev_ctx) {
-        (void)hipFree(a->d_nodes);
-        (void)hipFree(a->d_level_nodes);
-        (void)hipFree(a->d_level_off);
-        (void)hipFree(a->d_cons);
+        (void)hipFree(a->d_prog);
+        (void)hipFree(a->d_prog_off);
+        (void)hipFree(a->d_consts);
     }
     delete a;
 }
@@ -694,13 +757,12 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     dv.max_lcw = H.max_last_cw;
     dv.fail_init = b->d_fail_init;
     dv.mp_cap_host = b->mp_cap.data();
-    dv.air_nodes = air->d_nodes;
-    dv.air_level_nodes = air->d_level_nodes;
-    dv.air_level_off = air->d_level_off;
-    dv.air_n_levels = (uint32_t)air->level_off.size() - 1;
-    dv.air_cons = air->d_cons;
+    dv.air_prog = air->d_prog;
+    dv.air_prog_off = air->d_prog_off;
+    dv.air_n_levels = (uint32_t)air->prog_off.size() - 1;
+    dv.air_consts = air->d_consts;
     dv.air_cons_off = air->cons_off;
-    dv.air_lds_bytes = AIR_LDS_HEADER + air->nodes.size() * 24;
+    dv.air_lds_bytes = AIR_LDS_HEADER + (size_t)air->slots * 24;
     if (dv.air_lds_bytes > 160 * 1024 - 8192) {
         (void)hipFree(b->dmem);
         delete b;

@@ -626,14 +626,15 @@ __device__ Xfe block_sum_xfe(Xfe v, Xfe* sh) {
 }
 
 // ------------------------------------------------------------------ OOD: AIR + quotient identity
-// One workgroup per proof.  Circuit nodes are evaluated level by level into LDS (node values are
-// XFE), then sum_i w_i * C_i * Z_type(i)^-1 is compared with sum_k z^k * segment_k(z^4).  Also
+// One workgroup per proof.  The compiled AIR program (OodIns, stark.hpp) runs level by level:
+// OOD-row inputs are loaded into LDS slots, each ADD/SUB/MUL writes its value (XFE) to a reusable
+// slot, and each constraint is folded into this thread's share of sum_i w_i * C_i * Z_type(i)^-1
+// one level after it is produced.  The sum is then compared with sum_k z^k * segment_k(z^4).  Also
 // stores the OOD linear combinations used by DEEP: [sum w*curr row, sum w*next row, sum w*segs].
 __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
-                                                 uint32_t n_proofs, StarkDims dims, const AirNode* __restrict__ nodes,
-                                                 const uint32_t* __restrict__ level_nodes,
-                                                 const uint32_t* __restrict__ level_off, uint32_t n_levels,
-                                                 const uint32_t* __restrict__ cons_nodes, uint4 cons_type_off,
+                                                 uint32_t n_proofs, StarkDims dims, const OodIns* __restrict__ prog,
+                                                 const uint32_t* __restrict__ prog_off, uint32_t n_levels,
+                                                 const Xfe* __restrict__ consts, uint4 cons_type_off,
                                                  const uint64_t* __restrict__ xs, uint64_t* __restrict__ ood_out,
                                                  uint32_t* __restrict__ fail) {
     // all LDS in the dynamic region (16-B aligned carve, no static __shared__ in front of it)
@@ -641,7 +642,8 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
     Xfe* red = reinterpret_cast<Xfe*>(smem);              // 256
     Xfe* zinv = red + 256;                                 // 4
     Xfe* chal_derived = zinv + 4;                          // 4 (3 used)
-    uint32_t& zero_flag = *reinterpret_cast<uint32_t*>(chal_derived + 4);
+    Xfe* misc = chal_derived + 4;                          // 4 (1 used: z - w^-1)
+    uint32_t& zero_flag = *reinterpret_cast<uint32_t*>(misc + 4);
     Xfe* val = reinterpret_cast<Xfe*>(smem + AIR_LDS_HEADER);
     const uint32_t p = blockIdx.x, tid = threadIdx.x;
     if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
@@ -649,23 +651,27 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
     const SampleLayout sl = SampleLayout::of(dims, d.R);
     const uint64_t xb = d.xs_off * 3;
     const Xfe z = ld_xfe_raw(xs, xb + 3ull * sl.z);
+    if (tid == 0) zero_flag = 0;
+    __syncthreads();
+    // zerofier inverses (triton-vm verify: initial, consistency, transition, terminal), one
+    // inversion per wave, and the derived challenges
     if (tid == 0) {
-        zero_flag = 0;
-        // zerofier inverses (triton-vm verify: initial, consistency, transition, terminal)
-        const uint64_t w = root_of_unity(d.log2_ph);
-        const uint64_t w_inv = b_inv(w);
-        const Xfe one = x_one();
-        const Xfe zm1 = x_sub(z, one);
-        Xfe zph = z;
-        for (uint32_t q = 0; q < d.log2_ph; ++q) zph = x_mul(zph, zph);
-        const Xfe cons = x_sub(zph, one);
+        const uint64_t w_inv = b_inv(root_of_unity(d.log2_ph));
         const Xfe except_last = x_sub(z, x_lift(w_inv));
-        if (x_is_zero(zm1) || x_is_zero(cons) || x_is_zero(except_last)) zero_flag = 1;
-        zinv[0] = x_inv(zm1);
-        zinv[1] = x_inv(cons);
-        zinv[2] = x_mul(except_last, zinv[1]);
+        if (x_is_zero(except_last)) atomicOr(&zero_flag, 1u);
+        misc[0] = except_last;
         zinv[3] = x_inv(except_last);
     } else if (tid == 64) {
+        const Xfe zm1 = x_sub(z, x_one());
+        if (x_is_zero(zm1)) atomicOr(&zero_flag, 1u);
+        zinv[0] = x_inv(zm1);
+    } else if (tid == 128) {
+        Xfe zph = z;
+        for (uint32_t q = 0; q < d.log2_ph; ++q) zph = x_mul(zph, zph);
+        const Xfe cons = x_sub(zph, x_one());
+        if (x_is_zero(cons)) atomicOr(&zero_flag, 1u);
+        zinv[1] = x_inv(cons);
+    } else if (tid == 192) {
         // derived challenges: compressed program digest, input / output evaluation arguments
         const Xfe c0 = ld_xfe_raw(xs, xb + 3ull * (sl.chal + 0));
         const Xfe c1 = ld_xfe_raw(xs, xb + 3ull * (sl.chal + 1));
@@ -682,43 +688,41 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
         chal_derived[2] = eout;
     }
     __syncthreads();
-    // circuit, level by level
+    if (tid == 0) zinv[2] = x_mul(misc[0], zinv[1]);
+    __syncthreads();
+    const uint32_t offs[5] = {0u, cons_type_off.x, cons_type_off.y, cons_type_off.z, cons_type_off.w};
+    auto fetch = [&](uint32_t ref) -> Xfe {
+        const uint32_t t = ref >> 30;
+        if (t == 0) return val[ref];
+        if (t == 1) return consts[ref & 0x3FFFFFFFu];
+        const uint32_t kind = (ref >> 27) & 7u, i = ref & 0x7FFFFFFu;
+        switch (kind) {
+            case IN_MAIN_CURR: return ld_xfe_canon(words, d.ood_mc + 3ull * i);
+            case IN_AUX_CURR: return ld_xfe_canon(words, d.ood_ac + 3ull * i);
+            case IN_MAIN_NEXT: return ld_xfe_canon(words, d.ood_mn + 3ull * i);
+            case IN_AUX_NEXT: return ld_xfe_canon(words, d.ood_an + 3ull * i);
+            default:
+                return i < dims.num_sampled ? ld_xfe_raw(xs, xb + 3ull * (sl.chal + i)) : chal_derived[i - dims.num_sampled];
+        }
+    };
+    Xfe acc = x_zero();
     for (uint32_t lvl = 0; lvl < n_levels; ++lvl) {
-        for (uint32_t q = level_off[lvl] + tid; q < level_off[lvl + 1]; q += blockDim.x) {
-            const uint32_t id = level_nodes[q];
-            const AirNode nd = nodes[id];
-            Xfe v;
-            if (nd.op == AIR_INPUT) {
-                switch (nd.a) {
-                    case IN_MAIN_CURR: v = ld_xfe_canon(words, d.ood_mc + 3ull * nd.b); break;
-                    case IN_AUX_CURR: v = ld_xfe_canon(words, d.ood_ac + 3ull * nd.b); break;
-                    case IN_MAIN_NEXT: v = ld_xfe_canon(words, d.ood_mn + 3ull * nd.b); break;
-                    case IN_AUX_NEXT: v = ld_xfe_canon(words, d.ood_an + 3ull * nd.b); break;
-                    default:
-                        v = nd.b < dims.num_sampled ? ld_xfe_raw(xs, xb + 3ull * (sl.chal + nd.b))
-                                                    : chal_derived[nd.b - dims.num_sampled];
-                }
-            } else if (nd.op == AIR_CONST) {
-                v = {nd.k0, nd.k1, nd.k2};
-            } else if (nd.op == AIR_ADD) {
-                v = x_add(val[nd.a], val[nd.b]);
-            } else if (nd.op == AIR_SUB) {
-                v = x_sub(val[nd.a], val[nd.b]);
+        for (uint32_t q = prog_off[lvl] + tid; q < prog_off[lvl + 1]; q += blockDim.x) {
+            const OodIns ins = prog[q];
+            if (ins.op == OOD_ACC) {
+                const uint32_t c = ins.b;
+                uint32_t t = 0;
+                while (t < 3 && c >= offs[t + 1]) ++t;
+                const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.quot_w + c));
+                acc = x_add(acc, x_mul(w, x_mul(fetch(ins.a), zinv[t])));
+            } else if (ins.op == OOD_LOAD) {
+                val[ins.dst] = fetch(ins.a);
             } else {
-                v = x_mul(val[nd.a], val[nd.b]);
+                const Xfe x = fetch(ins.a), y = fetch(ins.b);
+                val[ins.dst] = ins.op == OOD_ADD ? x_add(x, y) : (ins.op == OOD_SUB ? x_sub(x, y) : x_mul(x, y));
             }
-            val[id] = v;
         }
         __syncthreads();
-    }
-    // weighted quotient sum
-    Xfe acc = x_zero();
-    const uint32_t offs[5] = {0u, cons_type_off.x, cons_type_off.y, cons_type_off.z, cons_type_off.w};
-    for (uint32_t c = tid; c < dims.num_constraints; c += blockDim.x) {
-        uint32_t t = 0;
-        while (t < 3 && c >= offs[t + 1]) ++t;
-        const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.quot_w + c));
-        acc = x_add(acc, x_mul(w, x_mul(val[cons_nodes[c]], zinv[t])));
     }
     const Xfe ood_q = block_sum_xfe(acc, red);
     // OOD linear combinations (DEEP needs them): lin weights = [main | aux | quot segs | deep]
@@ -1040,9 +1044,8 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         hipLaunchKernelGGL(k_mp_plan<256>, dim3(n, 1 + b.max_R), dim3(256), 0, sa, b.words, b.desc, n, k, tpp, b.dig,
                            b.idx, b.mp, b.fail, b.perm_counter);
     mark(3, sa);
-    hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(256), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims, b.air_nodes,
-                       b.air_level_nodes, b.air_level_off, b.air_n_levels, b.air_cons, b.air_cons_off, b.xs, b.ood,
-                       b.fail);
+    hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(256), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims, b.air_prog,
+                       b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs, b.ood, b.fail);
     mark(6, sa);
     hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
     mark(7, sa);
