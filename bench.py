@@ -19,8 +19,8 @@ upload (nhip_batch_prepare) happens before the timed region and is reported sepa
 
 roofline: the dominant kernel, k_mp_hash (the per-level Merkle hash_pair launches), as Tip5
 VALU lane-ops/s against the gfx950 VALU peak; `tip5_paths` adds the config-2 Tip5 path microbench.
-cpu_baseline: the oracle verifier (oracle/stark_ref.py with Tip5 in C, oracle/tip5_oracle.c), one
-proof per process on the host cores, over a bounded sample of this batch's proofs.
+cpu_baseline: the C restatement of the verifier (oracle/stark_oracle.c), one proof per host thread,
+over a bounded sample of this batch's proofs (the reference, Rust triton-vm, cannot be built here).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -108,45 +108,26 @@ def make_batch(pool, collections: int, corrupt_frac: float, seed: int):
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle)
-_CPU = {}
-
-
-def _cpu_init(air_words):
+def cpu_baseline(air_words, claims, proofs, expect, target_s: float, threads: int):
+    """The C restatement of the verifier (oracle/stark_oracle.c), one proof per host thread, over a
+    bounded prefix of the batch (whole collections, so the padded-height mix is the batch's)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import stark_ref as S  # oracle: CPU baseline leg only
-    import tip5_ref as T
-    T.use_c_backend()
-    _CPU["S"] = S
-    _CPU["params"] = S.StarkParams()
-    _CPU["air"] = S.AirCircuit.from_words([int(w) for w in air_words])
-
-
-def _cpu_verify(args):
-    claim, proof = args
-    S = _CPU["S"]
-    return bool(S.verify(_CPU["params"], _CPU["air"], claim, [int(w) for w in proof]))
-
-
-def cpu_baseline(air_words, claims, proofs, expect, target_s: float, procs: int):
-    """Oracle verifier, one proof per process (fork, before any GPU use), over a bounded prefix of the
-    batch (whole collections, so the padded-height mix is the batch's)."""
-    import multiprocessing as mp
-    ctxm = mp.get_context("fork")
-    with ctxm.Pool(procs, initializer=_cpu_init, initargs=(air_words,)) as pool:
-        # calibrate on one collection per process
-        m = 8 * procs
-        t = time.perf_counter()
-        pool.map(_cpu_verify, list(zip(claims[:m], proofs[:m])), chunksize=1)
-        dt = time.perf_counter() - t
-        m = min(len(proofs), max(m, int(m * target_s / max(dt, 1e-6)) // 8 * 8))
-        t = time.perf_counter()
-        v = pool.map(_cpu_verify, list(zip(claims[:m], proofs[:m])), chunksize=1)
-        dt = time.perf_counter() - t
-    assert list(v) == list(expect[:m]), "CPU baseline verdicts disagree with the expected verdicts"
-    return {"value": m / dt, "unit": "proofs/s", "cores": procs, "kind": "port",
-            "sample": f"the first {m} of this batch's {len(proofs)} proofs ({m // 8} whole collections), oracle "
-                      f"verifier oracle/stark_ref.py with Tip5 in C (oracle/tip5_oracle.c), {procs} processes, "
-                      f"{dt:.1f} s"}
+    import coracle as C  # oracle: CPU baseline leg only
+    import stark_ref as S
+    params = S.StarkParams()
+    m = min(len(proofs), 8 * threads)
+    t = time.perf_counter()
+    C.stark_verify_batch(air_words, params, claims[:m], proofs[:m], threads)
+    dt = time.perf_counter() - t
+    m = min(len(proofs), max(m, int(m * target_s / max(dt, 1e-6)) // 8 * 8))
+    t = time.perf_counter()
+    v = C.stark_verify_batch(air_words, params, claims[:m], proofs[:m], threads)
+    dt = time.perf_counter() - t
+    assert [bool(x) for x in v] == list(expect[:m]), "CPU baseline verdicts disagree with the expected verdicts"
+    return {"value": m / dt, "unit": "proofs/s", "cores": threads, "kind": "port",
+            "sample": f"the first {m} of this batch's {len(proofs)} proofs ({m // 8} whole collections), C "
+                      f"restatement of the verifier (oracle/stark_oracle.c, Tip5 oracle/tip5_oracle.c), {threads} "
+                      f"threads, {dt:.1f} s"}
 
 
 # ------------------------------------------------------------------ config 2 Tip5 path microbench
@@ -203,7 +184,7 @@ def main():
     ap.add_argument("--collections", type=int, default=256)
     ap.add_argument("--corrupt-frac", type=float, default=0.05)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
-    ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
     ap.add_argument("--pipeline", type=int, default=1,
@@ -222,7 +203,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         t = time.time()
-        cpu = cpu_baseline(air_words, claims, proofs, expect, args.cpu_seconds, args.cpu_procs)
+        cpu = cpu_baseline(air_words, claims, proofs, expect, args.cpu_seconds, args.cpu_threads)
         log(f"[cpu] {cpu['value']:.1f} proofs/s ({time.time() - t:.1f}s)")
 
     dist = None

@@ -109,3 +109,61 @@ def mtree_verify_batch(roots, indices, leaves, paths, depth: int, nthreads: int 
                                     np.ascontiguousarray(leaves, dtype=np.uint64).reshape(-1) if n else np.zeros(1, np.uint64),
                                     paths, depth, n, verdicts, nthreads)
     return verdicts[:n]
+
+
+def permutation_raw_pair(states_raw: np.ndarray):
+    """(reference-form perm_raw, twenty-first-MDS perm_raw_fast) of raw Montgomery states, for the
+    cross-check of the two C permutations."""
+    L = lib()
+    for fn in ("oracle_tip5_permutation_raw", "oracle_tip5_permutation_raw_fast"):
+        getattr(L, fn).argtypes = [_u64p]
+    a = np.ascontiguousarray(states_raw, dtype=np.uint64).copy()
+    b = a.copy()
+    for i in range(a.shape[0]):
+        ra, rb = np.ascontiguousarray(a[i]), np.ascontiguousarray(b[i])
+        L.oracle_tip5_permutation_raw(ra)
+        L.oracle_tip5_permutation_raw_fast(rb)
+        a[i], b[i] = ra, rb
+    return a, b
+
+
+def stark_verify_batch(air_words, params, claims, proofs, threads: int = 1) -> np.ndarray:
+    """C restatement of the verifier (oracle/stark_oracle.c) over (claim, proof) pairs.
+    params: oracle StarkParams; claims: (digest, version, input, output) tuples; proofs: word lists."""
+    L = lib()
+    fn = L.oracle_stark_verify_batch
+    fn.argtypes = [_u64p, ctypes.c_size_t, np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS"),
+                   _u64p, np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS"), _u64p, _u64p, _u64p,
+                   _u64p, _u64p, _u64p, ctypes.c_size_t, _u8p, ctypes.c_int]
+    fn.restype = ctypes.c_int
+    n = len(proofs)
+    air = np.ascontiguousarray(np.asarray(air_words, dtype=np.uint64))
+    import math
+    pw = np.array([int(math.log2(params.fri_expansion_factor)), params.num_collinearity_checks, params.num_main,
+                   params.num_aux, params.num_quotient_segments], dtype=np.uint32)
+    dig = np.array([[int(x) % (2 ** 64) for x in c[0]] for c in claims] or [[0] * 5], dtype=np.uint64).reshape(-1)
+    ver = np.array([int(c[1]) for c in claims] or [0], dtype=np.uint32)
+
+    def flat(lists):
+        if lists and all(isinstance(l, np.ndarray) for l in lists):
+            off = np.zeros(len(lists) + 1, dtype=np.uint64)
+            off[1:] = np.cumsum([l.size for l in lists])
+            data = np.concatenate([np.asarray(l, dtype=np.uint64).reshape(-1) for l in lists] + [np.zeros(1, np.uint64)])
+            return np.ascontiguousarray(data), off
+        off = np.zeros(len(lists) + 1, dtype=np.uint64)
+        for i, l in enumerate(lists):
+            off[i + 1] = off[i] + len(l)
+        data = np.zeros(max(int(off[-1]), 1), dtype=np.uint64)
+        for i, l in enumerate(lists):
+            if len(l):
+                data[int(off[i]):int(off[i + 1])] = np.asarray(l, dtype=np.uint64)
+        return data, off
+
+    ind, ino = flat([list(map(int, c[2])) for c in claims])
+    outd, outo = flat([list(map(int, c[3])) for c in claims])
+    prd, pro = flat(proofs)
+    v = np.zeros(max(n, 1), dtype=np.uint8)
+    rc = fn(air, air.size, pw, dig, ver, ind, ino, outd, outo, prd, pro, n, v, threads)
+    if rc != 0:
+        raise ValueError("oracle_stark_verify_batch: malformed AIR or parameters")
+    return v[:n]

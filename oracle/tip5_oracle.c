@@ -90,6 +90,50 @@ static void perm_raw(uint64_t s[16]) {
     }
 }
 
+/* The same permutation with twenty-first's MDS arithmetic (split into 32-bit halves, 64-bit
+ * accumulation, s = lo + hi * 2^32 reduced as s_lo + s_hi * (2^32 - 1) with the overflow fix, then
+ * BFieldElement addition of the round constant), used by the STARK oracle (stark_oracle.c) where
+ * speed matters; tests/test_stark_oracle_c.py checks it against perm_raw. */
+void oracle_tip5_permutation_raw_fast(uint64_t s[16]) {
+    for (int r = 0; r < 5; ++r) {
+        for (int i = 0; i < 4; ++i) {
+            uint64_t v = s[i], o = 0;
+            for (int k = 0; k < 8; ++k) o |= (uint64_t)LUT[(v >> (8 * k)) & 0xFF] << (8 * k);
+            s[i] = o;
+        }
+        for (int i = 4; i < 16; ++i) {
+            uint64_t x = s[i], x2 = mmul(x, x), x4 = mmul(x2, x2);
+            s[i] = mmul(mmul(x, x2), x4);
+        }
+        uint64_t lo[16], hi[16];
+        for (int j = 0; j < 16; ++j) {
+            lo[j] = s[j] & 0xFFFFFFFFull;
+            hi[j] = s[j] >> 32;
+        }
+        for (int i = 0; i < 16; ++i) {
+            uint64_t al = 0, ah = 0;
+            for (int j = 0; j < 16; ++j) {
+                al += MDS[(i - j) & 15] * lo[j];
+                ah += MDS[(i - j) & 15] * hi[j];
+            }
+            const u128 sum = (u128)al + ((u128)ah << 32);
+            const uint64_t s_lo = (uint64_t)sum, s_hi = (uint64_t)(sum >> 64);
+            uint64_t res = s_lo + s_hi * 0xFFFFFFFFull;
+            if (res < s_lo) res += 0xFFFFFFFFull;
+            s[i] = res;
+        }
+        for (int i = 0; i < 16; ++i) {
+            const uint64_t q = P - RC_RAW[r * 16 + i];
+            uint64_t x1 = s[i] - q;
+            if (s[i] < q) x1 -= 0xFFFFFFFFull;  /* BFieldElement add: borrow -> + p (mod 2^64) */
+            s[i] = x1;
+        }
+    }
+}
+uint64_t oracle_to_mont(uint64_t x) { return to_mont(x % P); }
+uint64_t oracle_from_mont(uint64_t r) { return from_mont(r); }
+void oracle_tip5_permutation_raw(uint64_t s[16]) { perm_raw(s); }
+
 /* canonical in / canonical out */
 void oracle_tip5_permutation(uint64_t s[16]) {
     for (int i = 0; i < 16; ++i) s[i] = to_mont(s[i] % P);
