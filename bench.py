@@ -281,10 +281,14 @@ def main():
     K = args.steps
     avg = {k: v / K for k, v in acc.items()}
     perms = avg["tip5_perms_static"] + avg["tip5_perms_merkle"]
-    hash_ms = avg["ms_merkle_hash"]
-    launches = max(avg["merkle_hash_launches"], 1.0)
-    kern_avg_s = hash_ms / launches / 1e3
-    achieved = avg["tip5_perms_merkle"] / launches * TIP5_VALU_OPS_PER_PERM / kern_avg_s
+    # the Merkle hash launches (k_mp_hash, and k_mp_hash_wide for levels of <= 48K ops) run back to
+    # back on the batch's main stream between two HIP events: their summed duration / launch count is
+    # the average launch duration (rocprofv3 cross-check: profiles/<tag>/SUMMARY.md, "Merkle hash
+    # launches" line)
+    launches = max(avg["mp_hash_kernel_launches"], 1.0)
+    kern_avg_s = avg["ms_mp_hash_kernel"] / launches / 1e3
+    perms_per_launch = avg["mp_hash_kernel_perms"] / launches
+    achieved = perms_per_launch * TIP5_VALU_OPS_PER_PERM / kern_avg_s if kern_avg_s > 0 else 0.0
     traffic, traffic_tag = pmc_traffic("k_mp_hash")
     res = {
         "metric": "STARK proofs verified/s (BASELINE config 3 per GPU) + Tip5 perms/s vs VALU roofline",
@@ -319,9 +323,9 @@ def main():
         "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
                      "unit": "T VALU lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS, "traffic": traffic,
                      "traffic_unit": "bytes per launch (FETCH_SIZE+WRITE_SIZE, raw; see DESIGN.md §3)",
-                     "traffic_profile": traffic_tag, "kernel": "k_mp_hash",
+                     "traffic_profile": traffic_tag, "kernel": "k_mp_hash (+ k_mp_hash_wide on the smallest levels)",
                      "kernel_avg_ms": kern_avg_s * 1e3, "launches_per_step": launches,
-                     "perms_per_launch": avg["tip5_perms_merkle"] / launches,
+                     "perms_per_launch": perms_per_launch,
                      "valu_ops_per_perm": TIP5_VALU_OPS_PER_PERM},
     }
     if rank == 0 and args.paths_log2 > 0:

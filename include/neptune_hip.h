@@ -138,6 +138,10 @@ typedef struct {
     double ms_fiat_shamir, ms_row_hash, ms_merkle, ms_ood_air, ms_fri, ms_deep, ms_device_total; /* device */
     double ms_merkle_hash;          /* the per-level hash_pair launches inside ms_merkle */
     uint64_t merkle_hash_launches;  /* number of those launches (one per tree level) */
+    /* the lane-per-op k_mp_hash launches only (HIP events around each launch; the small levels
+     * run k_mp_hash_wide): summed kernel time, launch count, permutations they performed */
+    double ms_mp_hash_kernel;
+    uint64_t mp_hash_kernel_launches, mp_hash_kernel_perms;
 } nhip_stats;
 
 typedef struct nhip_air nhip_air;

@@ -129,7 +129,7 @@ bool is_pow2(size_t n) { return n >= 2 && (n & (n - 1)) == 0; }
 
 extern "C" {
 
-int nhip_abi_version(void) { return 1000; }
+int nhip_abi_version(void) { return 1001; }
 
 const char* nhip_strerror(int code) {
     switch (code) {

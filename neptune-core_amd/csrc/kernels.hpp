@@ -60,7 +60,7 @@ struct StarkBatchDev {
     uint32_t* fail;
     const uint32_t* fail_init;  // decode-time failure bits (FAIL_DECODE), constant across runs
     uint8_t* verdicts;
-    unsigned long long* perm_counter;  // Merkle hash_pairs performed (device-counted)
+    unsigned long long* perm_counter;  // multiproof hash ops skipped (trees whose authentication structure failed)
     MpPlan mp;
     const uint64_t* mp_cap_host;  // host: op capacity per level (launch sizes)
     const OodIns* air_prog;        // compiled AIR (OodIns per level)

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -27,6 +28,7 @@ using namespace nhip;
 namespace {
 
 constexpr uint64_t P = GL_P;
+constexpr size_t OUT_HDR = 16;  // pinned readback: [skipped ops u64 | pad | plan counters | verdicts]
 
 enum ItemKind : uint32_t {
     MERKLE_ROOT = 0, OOD_MAIN_ROW, OOD_AUX_ROW, OOD_QUOT_SEGMENTS, AUTH_STRUCTURE, MAIN_ROWS, AUX_ROWS,
@@ -784,7 +786,8 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
             if (hipEventCreate(&b->tm.ev[i]) != hipSuccess) return NHIP_ERR_HIP;
         if (hipStreamCreateWithFlags(&b->main, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
         if (hipStreamCreateWithFlags(&b->aux, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
-        if (hipHostMalloc((void**)&b->h_out, (size_t)b->dev.n_proofs + 16, hipHostMallocDefault) != hipSuccess)
+        if (hipHostMalloc((void**)&b->h_out, OUT_HDR + (size_t)b->dev.mp.levels * MP_SHARDS * 4 + b->dev.n_proofs + 16,
+                          hipHostMallocDefault) != hipSuccess)
             return NHIP_ERR_OOM;
         b->timed = true;
     }
@@ -792,13 +795,15 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
     const uint32_t n = b->dev.n_proofs;
     hipError_t e = hipSuccess;
     if (n) e = hipMemcpyAsync(b->dev.fail, b->d_fail_init, n * 4, hipMemcpyDeviceToDevice, st);
+    const size_t cnt_bytes = (size_t)b->dev.mp.levels * MP_SHARDS * 4;
     if (e == hipSuccess) e = hipMemsetAsync(b->d_perm_counter, 0, 8, st);
-    if (e == hipSuccess && b->dev.mp.levels) e = hipMemsetAsync(b->dev.mp.counter, 0, (size_t)b->dev.mp.levels * MP_SHARDS * 4, st);
+    if (e == hipSuccess && cnt_bytes) e = hipMemsetAsync(b->dev.mp.counter, 0, cnt_bytes, st);
     if (e != hipSuccess) return hipfail(e);
     e = launch_stark_phases(b->dev, st, b->aux, &b->tm);
     if (e != hipSuccess) return hipfail(e);
     if (e == hipSuccess) e = hipMemcpyAsync(b->h_out, b->d_perm_counter, 8, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess && n) e = hipMemcpyAsync(b->h_out + 8, b->dev.verdicts, n, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && cnt_bytes) e = hipMemcpyAsync(b->h_out + OUT_HDR, b->dev.mp.counter, cnt_bytes, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && n) e = hipMemcpyAsync(b->h_out + OUT_HDR + cnt_bytes, b->dev.verdicts, n, hipMemcpyDeviceToHost, st);
     if (e != hipSuccess) return hipfail(e);
     b->in_flight = true;
     return NHIP_OK;
@@ -813,8 +818,17 @@ int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* al
     b->in_flight = false;
     if (e != hipSuccess) return hipfail(e);
     const uint32_t n = b->dev.n_proofs;
-    std::memcpy(&b->merkle_perms, b->h_out, 8);
-    b->merkle_perms += b->H.perms_lcw;
+    // Merkle permutations: multiproof ops reserved by the plan (per level and shard) minus the ops of
+    // trees whose authentication structure failed, plus the last-codeword trees
+    const size_t cnt_n = (size_t)b->dev.mp.levels * MP_SHARDS;
+    uint64_t skipped = 0, reserved = 0;
+    std::memcpy(&skipped, b->h_out, 8);
+    for (size_t i = 0; i < cnt_n; ++i) {
+        uint32_t c;
+        std::memcpy(&c, b->h_out + OUT_HDR + 4 * i, 4);
+        reserved += c;
+    }
+    b->merkle_perms = reserved - skipped + b->H.perms_lcw;
     // phases overlap (two streams): each is timed from the event its inputs wait on
     auto el = [&](int a, int c) {
         float ms = 0.f;
@@ -832,7 +846,7 @@ int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* al
         b->ph.deep = el(7, 8);
         b->ph.total = el(0, 9);
     }
-    const uint8_t* v = b->h_out + 8;
+    const uint8_t* v = b->h_out + OUT_HDR + cnt_n * 4;
     if (verdicts && n) std::memcpy(verdicts, v, n);
     if (all_ok) {
         uint8_t a = 1;
@@ -867,6 +881,11 @@ int nhip_batch_stats(const nhip_batch* b, nhip_stats* s) {
     s->ms_device_total = b->ph.total;
     s->tip5_perms_static = b->H.perms_static;
     s->tip5_perms_merkle = b->merkle_perms;
+    // every Merkle hash launch (k_mp_hash + the 16-lane-row k_mp_hash_wide): back to back on the
+    // batch's main stream, so the phase span is their summed duration
+    s->ms_mp_hash_kernel = b->ph.hash;
+    s->mp_hash_kernel_launches = b->tm.mp_hash_launches;
+    s->mp_hash_kernel_perms = b->merkle_perms;
     return NHIP_OK;
 }
 

@@ -378,7 +378,6 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
     __syncthreads();
     // ---- climb on indices; emit one op per parent node and tree
     uint32_t ap = 0;
-    unsigned long long hashed = 0;
     int cur = 0;
     for (uint32_t lvl = 0; lvl < h; ++lvl) {
         const uint32_t i = tid;
@@ -428,8 +427,12 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
             }
             L.key[cur ^ 1][opos] = ki >> 1;
         }
-        for (uint32_t t = 0; t < NT; ++t) hashed += ((bad >> t) & 1u) ? 0u : n_own;
-        if (tid == 0) L.bad = bad;
+        if (tid == 0) {
+            L.bad = bad;
+            uint32_t skipped = 0;
+            for (uint32_t t = 0; t < NT; ++t) skipped += ((bad >> t) & 1u) ? n_own : 0u;
+            if (skipped && perm_counter) atomicAdd(perm_counter, (unsigned long long)skipped);
+        }
         ap += n_unp;
         m = n_own;
         cur ^= 1;
@@ -448,7 +451,6 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
             atomicOr(&fail[p], fail_bit[t]);
         }
     }
-    if (tid == 0 && perm_counter) atomicAdd(perm_counter, hashed);
 }
 
 // The last FRI codeword's Merkle tree (every node; XFE leaves embedded as [c0, c1, c2, 0, 0]) is
@@ -493,33 +495,43 @@ __global__ void __launch_bounds__(256) k_mp_hash(const uint64_t* __restrict__ wo
     }
     tip5_lds_init(t5);  // includes the barrier
     uint64_t s[16];
-    uint64_t* o;
+    uint64_t* o = nullptr;
+    bool work = false;
     if (is_lcw) {
         const uint32_t per = lcw.max_len >> (lvl + 1);
         const uint64_t q = (uint64_t)(blockIdx.x - mp_blocks) * blockDim.x + threadIdx.x;
         const uint32_t p = (uint32_t)(q / per), i = (uint32_t)(q % per);
-        if (p >= n_proofs || (fail_init[p] & FAIL_DECODE)) return;
-        const ProofDesc& d = desc[p];
-        const uint32_t L = d.last_cw_n;
-        if (i >= (L >> (lvl + 1))) return;
-        const uint32_t v = (L >> (lvl + 1)) + i;
-        uint64_t* mine = lcw.nodes + (uint64_t)p * lcw.max_len * 5;
-        lcw_node(words, d, mine, 2 * v, L, s);
-        lcw_node(words, d, mine, 2 * v + 1, L, s + 5);
-        o = mine + 5ull * v;
+        if (p < n_proofs && !(fail_init[p] & FAIL_DECODE)) {
+            const ProofDesc& d = desc[p];
+            const uint32_t L = d.last_cw_n;
+            if (i < (L >> (lvl + 1))) {
+                const uint32_t v = (L >> (lvl + 1)) + i;
+                uint64_t* mine = lcw.nodes + (uint64_t)p * lcw.max_len * 5;
+                lcw_node(words, d, mine, 2 * v, L, s);
+                lcw_node(words, d, mine, 2 * v + 1, L, s + 5);
+                o = mine + 5ull * v;
+                work = true;
+            }
+        }
     } else {
         const uint64_t g = s_base[0] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-        if (g >= s_base[MP_SHARDS]) return;
-        uint32_t sh = 0;
+        if (g < s_base[MP_SHARDS]) {
+            uint32_t sh = 0;
 #pragma unroll
-        for (uint32_t q = 1; q < MP_SHARDS; ++q) sh += g >= s_base[q] ? 1u : 0u;
-        if (g - s_base[sh] >= s_cnt[sh]) return;
-        const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
-        if (lc == MPS_NONE) return;  // op of a tree that already failed
-        mp_load(lc, words, dig, plan.arena, s);
-        mp_load(rc, words, dig, plan.arena, s + 5);
-        o = plan.arena + 5 * g;
+            for (uint32_t q = 1; q < MP_SHARDS; ++q) sh += g >= s_base[q] ? 1u : 0u;
+            if (g - s_base[sh] < s_cnt[sh]) {
+                const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
+                if (lc != MPS_NONE) {  // else: op of a tree that already failed
+                    mp_load(lc, words, dig, plan.arena, s);
+                    mp_load(rc, words, dig, plan.arena, s + 5);
+                    o = plan.arena + 5 * g;
+                    work = true;
+                }
+            }
+        }
     }
+    // permutations performed, one atomic per wave (bench / stats: perms per launch)
+    if (!work) return;
 #pragma unroll
     for (int q = 10; q < 16; ++q) s[q] = MONT_ONE;
     tip5_permute_raw(s, t5.lut);
@@ -554,13 +566,19 @@ __global__ void __launch_bounds__(256) k_mp_hash_wide(const uint64_t* __restrict
     const uint32_t e = threadIdx.x & 15u;
     const uint64_t g = s_base[0] + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4);
     // every test below is uniform within the 16-lane row (one op per row)
-    if (g >= s_base[MP_SHARDS]) return;
-    uint32_t sh = 0;
+    bool work = false;
+    uint64_t lc = MPS_NONE, rc = MPS_NONE;
+    if (g < s_base[MP_SHARDS]) {
+        uint32_t sh = 0;
 #pragma unroll
-    for (uint32_t q = 1; q < MP_SHARDS; ++q) sh += g >= s_base[q] ? 1u : 0u;
-    if (g - s_base[sh] >= s_cnt[sh]) return;
-    const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
-    if (lc == MPS_NONE) return;
+        for (uint32_t q = 1; q < MP_SHARDS; ++q) sh += g >= s_base[q] ? 1u : 0u;
+        if (g - s_base[sh] < s_cnt[sh]) {
+            lc = plan.ops[2 * g];
+            rc = plan.ops[2 * g + 1];
+            work = lc != MPS_NONE;
+        }
+    }
+    if (!work) return;
     uint64_t rcs[TIP5_ROUNDS];
 #pragma unroll
     for (int r = 0; r < TIP5_ROUNDS; ++r) rcs[r] = c_tip5_rc_raw[r * 16 + e];
@@ -1074,7 +1092,8 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         const uint64_t per = b.max_lcw >> (l + 1);
         const uint32_t lcw_blocks = (uint32_t)((per * n + 255) / 256);
         if (mp_blocks + lcw_blocks == 0) continue;
-        if (lcw_blocks == 0 && cap <= MP_WIDE_MAX_OPS)
+        const bool wide = lcw_blocks == 0 && cap <= MP_WIDE_MAX_OPS;
+        if (wide)
             hipLaunchKernelGGL(k_mp_hash_wide, dim3((unsigned)((cap * 16 + 255) / 256)), dim3(256), 0, st, b.words,
                                b.dig, b.mp, l);
         else

@@ -47,7 +47,8 @@ class Stats(ctypes.Structure):
                 ("ms_row_hash", ctypes.c_double), ("ms_merkle", ctypes.c_double),
                 ("ms_ood_air", ctypes.c_double), ("ms_fri", ctypes.c_double), ("ms_deep", ctypes.c_double),
                 ("ms_device_total", ctypes.c_double), ("ms_merkle_hash", ctypes.c_double),
-                ("merkle_hash_launches", ctypes.c_uint64)]
+                ("merkle_hash_launches", ctypes.c_uint64), ("ms_mp_hash_kernel", ctypes.c_double),
+                ("mp_hash_kernel_launches", ctypes.c_uint64), ("mp_hash_kernel_perms", ctypes.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

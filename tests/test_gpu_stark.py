@@ -202,3 +202,81 @@ def test_bench_pool_heights_9_to_16_match_oracle(ctx):
     for claim, m in bad[:2]:
         assert S.verify(params, air, claim, m) is False
     b.close()
+
+
+def _pool():
+    import json as _json
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "c3_pool.npz"))
+    meta = _json.loads(bytes(z["meta"]).decode())
+    out = []
+    for h in meta["heights"]:
+        c = meta["claims"][str(h)]
+        out.append(((c["digest"], c["version"], c["input"], c["output"]), z[f"proof_{h}"], meta["main_rows"][str(h)]))
+    return z["air"], out
+
+
+def test_full_size_random_mutations_vs_c_oracle(ctx):
+    """Stark::default()-sized proofs (heights 9..16) with one random word changed anywhere in the
+    proof (count fields, discriminants, roots, auth structures, FRI data, rows) or the claim
+    changed: every GPU verdict equals the C restatement's (oracle/stark_oracle.c)."""
+    import coracle as C
+    NS = _ns()
+    air_w, pool = _pool()
+    params = S.StarkParams()
+    rng = np.random.default_rng(0xDEE9)
+    claims, proofs = [], []
+    for claim, proof, _ in pool:
+        claims.append(claim)
+        proofs.append(proof)
+        for _ in range(48):
+            m = proof.copy()
+            pos = int(rng.integers(0, m.size))
+            r = int(rng.integers(0, 3))
+            m[pos] = np.uint64((int(m[pos]) + 1) % S.P) if r == 0 else (
+                np.uint64(int(rng.integers(0, 1 << 62))) if r == 1 else np.uint64(0))
+            claims.append(claim)
+            proofs.append(m)
+        cl = list(claim)
+        cl[2] = list(cl[2]) + [int(rng.integers(0, 1 << 40))]
+        claims.append(tuple(cl))
+        proofs.append(proof)
+    got = NS.verify_batch(ctx, NS.Air([int(w) for w in air_w]), NS.Stark.default(),
+                          [(NS.Claim(*c), p) for c, p in zip(claims, proofs)])
+    want = [bool(x) for x in C.stark_verify_batch(air_w, params, claims, proofs, threads=16)]
+    assert got == want
+    assert sum(want) >= len(pool)  # the clean proofs accept (a mutation may hit an unused word)
+
+
+def test_async_launch_wait_matches_run(ctx):
+    """nhip_batch_launch / nhip_batch_wait on two batches in flight at once == nhip_batch_run."""
+    NS = _ns()
+    air_w, pool = _pool()
+    gair = NS.Air([int(w) for w in air_w])
+    stark = NS.Stark.default()
+    claims = [NS.Claim(*c) for c, _, _ in pool]
+    bad = []
+    for _, p, (lo, hi) in pool:
+        m = p.copy()
+        m[(lo + hi) // 2] = np.uint64((int(m[(lo + hi) // 2]) + 7) % S.P)
+        bad.append(m)
+    b1 = NS.Batch(ctx, gair, stark, claims, [p for _, p, _ in pool])
+    b2 = NS.Batch(ctx, gair, stark, claims, bad)
+    b1.launch()
+    b2.launch()
+    v2, ok2 = b2.wait()
+    v1, ok1 = b1.wait()
+    assert list(v1) == [1] * len(pool) and ok1
+    assert list(v2) == [0] * len(pool) and not ok2
+    r1, _ = b1.run()
+    assert list(r1) == list(v1)
+    b1.close()
+    b2.close()
+
+
+def test_empty_and_single_malformed_batches(ctx):
+    NS = _ns()
+    air_w, pool = _pool()
+    gair = NS.Air([int(w) for w in air_w])
+    assert NS.verify_batch(ctx, gair, NS.Stark.default(), []) == []
+    claim = NS.Claim(*pool[0][0])
+    assert NS.verify_batch(ctx, gair, NS.Stark.default(), [(claim, [5, 4, 3])]) == [False]

@@ -24,6 +24,15 @@ if stats:
         name = kname(r["Name"])
         print(f"| {name} | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | {float(r['MinNs'])/1e6:.3f} | "
               f"{float(r['MaxNs'])/1e6:.3f} | {float(r['Percentage']):.1f} |")
+if stats:
+    tot_ns, calls = 0.0, 0
+    for r in csv.DictReader(open(stats[0])):
+        if kname(r["Name"]).endswith(("k_mp_hash", "k_mp_hash_wide")):
+            tot_ns += float(r["TotalDurationNs"])
+            calls += int(r["Calls"])
+    if calls:
+        print(f"\nMerkle hash launches (k_mp_hash + k_mp_hash_wide): {calls} calls, average "
+              f"{tot_ns / calls / 1e6:.3f} ms per launch")
 bench = os.path.join(d, "bench_trace.json")
 if os.path.exists(bench):
     b = json.load(open(bench))
