@@ -107,6 +107,53 @@ def make_batch(pool, collections: int, corrupt_frac: float, seed: int):
     return claims, proofs, np.array(expect, dtype=bool)
 
 
+def make_config4(pool, total: int, corrupt_frac: float, world: int, rank: int):
+    """BASELINE config 4: `total` transaction proofs with log2 padded heights drawn uniformly from
+    the ProofCollection member mix (seed 0xC4), corrupt_frac of them with one flipped MainRows word,
+    LPT-sharded over the ranks by estimated Tip5 cost (neptune_hip.shard.lpt_shard).  Returns this
+    rank's (claims, proofs, expect)."""
+    from neptune_hip import shard
+    rng = np.random.default_rng(0xC4)
+    hs = rng.choice(COLLECTION_HEIGHTS, size=total)
+    bad = set(rng.choice(total, size=int(round(total * corrupt_frac)), replace=False).tolist())
+    cost = [10_000 + 600 * int(h) for h in hs]  # ~ Tip5 permutations per proof of that height
+    mine = shard.lpt_shard(cost, world)[rank]
+    claims, proofs, expect = [], [], []
+    for i in mine:
+        e = pool[int(hs[i])]
+        proof = e["proof"]
+        if i in bad:
+            proof = proof.copy()
+            lo, hi = e["main_rows"]
+            pos = lo + (i * 7919) % (hi - lo)
+            proof[pos] = np.uint64((int(proof[pos]) + 1) % P)
+        claims.append(e["claim"])
+        proofs.append(proof)
+        expect.append(i not in bad)
+    return claims, proofs, np.array(expect, dtype=bool)
+
+
+def make_config5(air_words, total: int, log2_ph: int, world: int, rank: int):
+    """BASELINE config 5: `total` proofs at log2 padded height `log2_ph` (seed 0xC5 + i; constant-
+    codeword synthetic prover, oracle/stark_prover_const.py), contiguous shards over the ranks."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import stark_prover_const as K  # test-data generator (proof construction only)
+    import stark_ref as S
+    import tip5_ref as T
+    from neptune_hip import shard
+    T.use_c_backend()
+    params = S.StarkParams()
+    _, recipe = S.synth_air(params, seed=1)
+    air = S.AirCircuit.from_words([int(w) for w in air_words])
+    claims, proofs = [], []
+    for i in shard.contiguous_shard(total, world, rank):
+        claim = ([0xC5, i, 0, 0, 0], 0, [i], [])
+        proof, _ = K.prove(params, air, recipe, claim, log2_ph, seed=0xC5 + i)
+        claims.append(claim)
+        proofs.append(np.asarray(proof, dtype=np.uint64))
+    return claims, proofs, np.ones(len(proofs), dtype=bool)
+
+
 # ------------------------------------------------------------------ CPU baseline (oracle)
 def cpu_baseline(air_words, claims, proofs, expect, target_s: float, threads: int):
     """The C restatement of the verifier (oracle/stark_oracle.c), one proof per host thread, over a
@@ -181,6 +228,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, choices=(3, 4, 5),
+                    help="3: 256 ProofCollections (2,048 proofs) per GPU, weak scaling (default); 4: 4,096 mixed "
+                         "proofs over all ranks, strong scaling; 5: 64 proofs at log2 padded height 23 over all "
+                         "ranks, strong scaling")
+    ap.add_argument("--proofs", type=int, default=None, help="config 4 / 5 total proofs (4096 / 64)")
+    ap.add_argument("--log2-height", type=int, default=23, help="config 5 padded height")
     ap.add_argument("--collections", type=int, default=256)
     ap.add_argument("--corrupt-frac", type=float, default=0.05)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
@@ -198,7 +251,16 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     air_words, pool = load_pool()
-    claims, proofs, expect = make_batch(pool, args.collections, args.corrupt_frac, 0xC3 + rank)
+    sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
+    if args.config == 3:
+        claims, proofs, expect = make_batch(pool, args.collections, args.corrupt_frac, 0xC3 + rank)
+        total = world * len(proofs)
+    elif args.config == 4:
+        total = args.proofs or 4096
+        claims, proofs, expect = make_config4(pool, total, 0.01, world, rank)
+    else:
+        total = args.proofs or 64
+        claims, proofs, expect = make_config5(air_words, total, args.log2_height, world, rank)
     n = len(proofs)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -220,9 +282,10 @@ def main():
     t0 = time.time()
     gair = NS.Air([int(w) for w in air_words])
     stark = NS.Stark.default()
-    n_coll = args.collections
-    P = max(1, min(args.pipeline, n_coll))
-    cuts = [n_coll * i // P * len(COLLECTION_HEIGHTS) for i in range(P + 1)]
+    unit = len(COLLECTION_HEIGHTS) if args.config == 3 else 1  # split on whole collections
+    n_units = n // unit
+    P = max(1, min(args.pipeline, n_units))
+    cuts = [n_units * i // P * unit for i in range(P + 1)]
     batches = [NS.Batch(ctx, gair, stark, [NS.Claim(*c) for c in claims[a:b]], proofs[a:b])
                for a, b in zip(cuts[:-1], cuts[1:])]
     prep_s = time.time() - t0
@@ -276,6 +339,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, any_bad = float(t[0].item()), float(t[1].item())
         correct = any_bad == 0.0
+    perms_rank = (acc.get("tip5_perms_static", 0.0) + acc.get("tip5_perms_merkle", 0.0)) / max(args.steps, 1)
+    perms_job = perms_rank
+    if dist is not None:
+        import torch
+        tp = torch.tensor([perms_rank], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tp, op=dist.ReduceOp.SUM)
+        perms_job = float(tp[0].item())
     if not correct:
         log("ERROR: verdicts differ from expected")
     K = args.steps
@@ -290,29 +360,40 @@ def main():
     perms_per_launch = avg["mp_hash_kernel_perms"] / launches
     achieved = perms_per_launch * TIP5_VALU_OPS_PER_PERM / kern_avg_s if kern_avg_s > 0 else 0.0
     traffic, traffic_tag = pmc_traffic("k_mp_hash")
+    if args.config == 3:
+        workload = (f"BASELINE config 3: {args.collections} ProofCollections x 8 proofs (log2 padded heights "
+                    f"{COLLECTION_HEIGHTS}) = {n} STARK verifications per GPU, Stark::default()")
+    elif args.config == 4:
+        workload = (f"BASELINE config 4: {total} transaction proofs (log2 padded heights drawn from "
+                    f"{COLLECTION_HEIGHTS}, 1% corrupted), LPT-sharded over {world} GPU(s), Stark::default()")
+    else:
+        workload = (f"BASELINE config 5: {total} proofs at log2 padded height {args.log2_height} (FRI domain "
+                    f"2^{args.log2_height + 3}), sharded over {world} GPU(s), Stark::default()")
     res = {
         "metric": "STARK proofs verified/s (BASELINE config 3 per GPU) + Tip5 perms/s vs VALU roofline",
-        "value": world * n * K / elapsed,
+        "value": total * K / elapsed,
         "unit": "proofs/s",
         "n_gpus": world,
         "steps": K,
         "warmup": args.warmup,
         "ms_per_step": elapsed / K * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.config == 3 else "strong",
         "vs_baseline": None,
         "dtype": "u64 (Goldilocks mod p; XFE = cubic extension)",
-        "data": "synthetic: one accepting proof per padded height (tests/golden/c3_pool.npz, synthetic AIR with "
-                "triton-vm column counts), 5% of collections with one flipped MainRows word",
-        "config": {"workload": f"BASELINE config 3: {args.collections} ProofCollections x 8 proofs (log2 padded "
-                               f"heights {COLLECTION_HEIGHTS}) = {n} STARK verifications per GPU, Stark::default()",
-                   "proofs_per_gpu": n, "collections_per_gpu": args.collections,
+        "data": ("synthetic: one accepting proof per padded height (tests/golden/c3_pool.npz, synthetic AIR with "
+                 "triton-vm column counts), 5% of collections with one flipped MainRows word" if args.config == 3 else
+                 "synthetic: proofs of the config-3 pool (tests/golden/c3_pool.npz), 1% with one flipped MainRows word"
+                 if args.config == 4 else
+                 "synthetic: constant-codeword proofs (oracle/stark_prover_const.py), synthetic AIR with triton-vm "
+                 "column counts"),
+        "config": {"workload": workload, "proofs_total": total, "proofs_rank0": n,
                    "parallelism": f"proof-sharded x{world}"},
         "verdicts_correct": correct,
         "batch_verdict": batch_ok,
-        "expected_rejects_per_gpu": int((~expect).sum()),
+        "expected_rejects_rank0": int((~expect).sum()),
         "tip5_perms_per_proof": perms / n,
-        "tip5_perms_per_s": world * perms * K / elapsed,
+        "tip5_perms_per_s": perms_job * K / elapsed,
         # per sub-batch (each sub-batch's phases are timed by HIP events on its own two streams)
         "phase_ms": {k[3:]: round(avg[k] / P, 4) for k in ("ms_fiat_shamir", "ms_row_hash", "ms_merkle",
                                                             "ms_merkle_hash", "ms_ood_air", "ms_fri", "ms_deep",

@@ -280,3 +280,33 @@ def test_empty_and_single_malformed_batches(ctx):
     assert NS.verify_batch(ctx, gair, NS.Stark.default(), []) == []
     claim = NS.Claim(*pool[0][0])
     assert NS.verify_batch(ctx, gair, NS.Stark.default(), [(claim, [5, 4, 3])]) == [False]
+
+
+def test_large_padded_heights_config5_shape(ctx):
+    """BASELINE config 5 shape: proofs at log2 padded height 20 and 23 (FRI domain 2^23 / 2^26,
+    14 / 17 FRI rounds) from the constant-codeword prover: GPU verdicts and every Fiat-Shamir
+    sample equal the oracle's; mutated copies reject on both."""
+    import stark_prover_const as K
+    T.use_c_backend()
+    NS = _ns()
+    params = S.StarkParams()
+    air, recipe = S.synth_air(params, seed=1)
+    cases, bad = [], []
+    for lph in (20, 23):
+        claim = ([lph, 9, 9, 9, 9], 0, [lph], [1, 2])
+        proof, _ = K.prove(params, air, recipe, claim, lph, seed=lph)
+        cases.append((claim, proof))
+        for pos in (len(proof) // 3, len(proof) - 7):
+            m = list(proof)
+            m[pos] = (m[pos] + 1) % S.P
+            bad.append((claim, m))
+    b = NS.Batch(ctx, NS.Air(air.to_words()), NS.Stark.default(), [NS.Claim(*c) for c, _ in cases + bad],
+                 [p for _, p in cases + bad])
+    v, _ = b.run()
+    want = [S.verify(params, air, c, p) for c, p in cases + bad]
+    assert [bool(x) for x in v] == want and want[:2] == [True, True]
+    for i, (claim, proof) in enumerate(cases):
+        ok_o, samples, indices = _oracle_samples(params, air, claim, proof)
+        xs, idx, fail = b.transcript(i)
+        assert ok_o and fail == 0 and xs == samples and idx == indices
+    b.close()

@@ -78,3 +78,46 @@ def test_lpt_shard_balances_and_covers():
     loads = [sum(costs[i] for i in r) for r in s]
     assert max(loads) - min(loads) <= max(costs)
     assert shard.contiguous_shard(10, 3, 2) == range(8, 10)
+
+
+def _stark_worker(rank, world, port, q):
+    for p in ("oracle", "neptune-core_amd", ""):
+        sys.path.insert(0, os.path.join(ROOT, p))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    import bench
+    import coracle as C
+    import stark_ref as S
+    from neptune_hip import shard
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    air, pool = bench.load_pool()
+    total = 48
+    claims, proofs, expect = bench.make_config4(pool, total, 0.1, world, rank)
+    v = C.stark_verify_batch(air, S.StarkParams(), claims, proofs, threads=2)
+    rng = np.random.default_rng(0xC4)
+    hs = rng.choice(bench.COLLECTION_HEIGHTS, size=total)
+    shards = shard.lpt_shard([10_000 + 600 * int(h) for h in hs], world)
+    ok = shard.all_ok(bool(v.all()), dist)
+    full = shard.gather_verdicts(v, shards, total, dist)
+    q.put((rank, ok, full.tolist(), [bool(x) == bool(e) for x, e in zip(v, expect)], [len(s) for s in shards]))
+    dist.destroy_process_group()
+
+
+def test_two_rank_config4_stark_sharding():
+    """bench.py config 4 on world size 2 (gloo; the C verifier stands in for the GPU): the LPT
+    shards cover every proof once, each rank's verdicts are the expected ones, and the verdict
+    exchange (all-reduce MIN + all-gather) reconstructs the job's verdict vector."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stark_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    fulls = [r[2] for r in res]
+    assert fulls[0] == fulls[1] and sum(fulls[0]) == 48 - 5
+    for rank, ok, full, matches, sizes in res:
+        assert ok is False and all(matches) and sum(sizes) == 48
