@@ -72,10 +72,12 @@ struct StarkBatchDev {
 };
 
 // events: 0 start | fs | rows | mp plan | mp hash levels | mp roots | ood | fri | deep | 9 verdicts
-static constexpr int STARK_EVENTS = 10;
+// 10: main stream at the aux-chain release point, 11: aux stream after that wait
+static constexpr int STARK_EVENTS = 12;
 struct StarkPhaseTimer {
     hipEvent_t ev[STARK_EVENTS];
     uint32_t mp_hash_launches;
+    uint32_t aux_after_level = 0;  // hash levels launched before the OOD/FRI/DEEP chain is released
 };
 
 // Phases on two streams: st_aux runs the latency-bound chain (Fiat-Shamir -> Merkle plan -> OOD ->

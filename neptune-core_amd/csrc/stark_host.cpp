@@ -28,7 +28,8 @@ using namespace nhip;
 namespace {
 
 constexpr uint64_t P = GL_P;
-constexpr size_t OUT_HDR = 16;  // pinned readback: [skipped ops u64 | pad | plan counters | verdicts]
+constexpr size_t OUT_HDR = 16;
+constexpr uint32_t AUX_AFTER_LEVEL_DEFAULT = 0;  // tuned on MI355X  // pinned readback: [skipped ops u64 | pad | plan counters | verdicts]
 
 enum ItemKind : uint32_t {
     MERKLE_ROOT = 0, OOD_MAIN_ROW, OOD_AUX_ROW, OOD_QUOT_SEGMENTS, AUTH_STRUCTURE, MAIN_ROWS, AUX_ROWS,
@@ -784,6 +785,8 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
     if (!b->timed) {
         for (int i = 0; i < STARK_EVENTS; ++i)
             if (hipEventCreate(&b->tm.ev[i]) != hipSuccess) return NHIP_ERR_HIP;
+        const char* al = std::getenv("NHIP_AUX_AFTER_LEVEL");
+        b->tm.aux_after_level = al ? (uint32_t)std::strtoul(al, nullptr, 10) : AUX_AFTER_LEVEL_DEFAULT;
         if (hipStreamCreateWithFlags(&b->main, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
         if (hipStreamCreateWithFlags(&b->aux, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
         if (hipHostMalloc((void**)&b->h_out, OUT_HDR + (size_t)b->dev.mp.levels * MP_SHARDS * 4 + b->dev.n_proofs + 16,
@@ -841,7 +844,7 @@ int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* al
         b->ph.plan = el(1, 3);
         b->ph.hash = std::min(el(2, 4), el(3, 4));
         b->ph.roots = el(4, 5);
-        b->ph.ood = el(3, 6);
+        b->ph.ood = el(11, 6);
         b->ph.fri = el(6, 7);
         b->ph.deep = el(7, 8);
         b->ph.total = el(0, 9);

@@ -1062,17 +1062,6 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         hipLaunchKernelGGL(k_mp_plan<256>, dim3(n, 1 + b.max_R), dim3(256), 0, sa, b.words, b.desc, n, k, tpp, b.dig,
                            b.idx, b.mp, b.fail, b.perm_counter);
     mark(3, sa);
-    hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(256), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims, b.air_prog,
-                       b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs, b.ood, b.fail);
-    mark(6, sa);
-    hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
-    mark(7, sa);
-    {
-        const uint32_t S = deep_chunks(b.dims);
-        hipLaunchKernelGGL(k_deep, dim3(n), dim3(S * k), deep_lds_bytes(b.dims), sa, b.words, b.desc, n, b.dims, S,
-                           b.xs, b.xdom, b.ood, b.fail);
-    }
-    mark(8, sa);
     // ---- main stream: VALU-bound hashing
     {
         const uint64_t rows = (uint64_t)n * k;
@@ -1082,11 +1071,33 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     }
     mark(2, st);
     (void)hipStreamWaitEvent(st, tm->ev[3], 0);  // plan done
+    // The OOD / FRI / DEEP chain only needs the Fiat-Shamir samples, but its kernels are latency-bound
+    // and hold CU resources for long; started after the first `aux_after_level` (wide, VALU-bound)
+    // hash levels it overlaps the narrow, latency-bound top levels instead.
+    auto launch_aux_chain = [&]() {
+        mark(10, st);
+        (void)hipStreamWaitEvent(sa, tm->ev[10], 0);
+        mark(11, sa);
+        hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(256), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims, b.air_prog,
+                           b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs, b.ood, b.fail);
+        mark(6, sa);
+        hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
+        mark(7, sa);
+        const uint32_t S = deep_chunks(b.dims);
+        hipLaunchKernelGGL(k_deep, dim3(n), dim3(S * k), deep_lds_bytes(b.dims), sa, b.words, b.desc, n, b.dims, S,
+                           b.xs, b.xdom, b.ood, b.fail);
+        mark(8, sa);
+    };
     uint32_t launches = 0;
+    bool aux_started = false;
     const LcwTree lcw{b.lcw, b.max_lcw};
     const uint32_t log2_lcw = 31 - __builtin_clz(b.max_lcw);
     const uint32_t hash_levels = b.mp.levels > log2_lcw ? b.mp.levels : log2_lcw;
     for (uint32_t l = 0; l < hash_levels; ++l) {
+        if (!aux_started && l >= tm->aux_after_level) {
+            launch_aux_chain();
+            aux_started = true;
+        }
         const uint64_t cap = l < b.mp.levels ? b.mp_cap_host[l] : 0;
         const uint32_t mp_blocks = (uint32_t)((cap + 255) / 256);
         const uint64_t per = b.max_lcw >> (l + 1);
@@ -1101,6 +1112,7 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
                                mp_blocks, b.desc, n, b.fail_init, lcw);
         ++launches;
     }
+    if (!aux_started) launch_aux_chain();
     tm->mp_hash_launches = launches;
     mark(4, st);
     const uint32_t nrec = n * tpp;
