@@ -175,6 +175,16 @@ int nhip_batch_transcript(nhip_ctx *ctx, const nhip_batch *batch, size_t proof, 
                           uint32_t *idx_out, size_t idx_cap, uint32_t *fail_bits, size_t *n_xfe);
 void nhip_batch_destroy(nhip_batch *batch);
 
+/* ---- ingestion formats -------------------------------------------
+ * Proof files of neptune-core/src/protocol/proof_abstractions/tasm/program.rs:374-390: 8-byte
+ * big-endian chunks, each BFieldElement::new (reduced mod p); n_bytes not a multiple of 8 ->
+ * NHIP_ERR_ARG (the reference returns None).  words == NULL: size query (*n_words). */
+int nhip_proof_from_be_bytes(const uint8_t *bytes, size_t n_bytes, uint64_t *words, size_t cap, size_t *n_words);
+/* Writer side (program.rs:565-572): value().to_be_bytes() per element; out: 8 * n bytes. */
+int nhip_proof_to_be_bytes(const uint64_t *words, size_t n, uint8_t *out);
+/* Tip5::hash(claim) = hash_varlen(claim.encode()) (program.rs:355-358, proof file name). */
+int nhip_claim_hash(nhip_ctx *ctx, const nhip_claim *claim, uint64_t digest_out[5]);
+
 /* ---- kernel timing (HIP events on the ctx stream around every kernel launch) ------------ */
 int nhip_timing_enable(nhip_ctx *ctx, int on);
 /* Total device time of the kernels launched since the last reset, and their count. */

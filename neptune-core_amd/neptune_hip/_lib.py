@@ -16,6 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NHIP_LIB") or os.path.join(_HERE, "libneptune_hip.so")
 
 NHIP_OK = 0
+NHIP_OK, NHIP_ERR_NO_DEVICE, NHIP_ERR_HIP, NHIP_ERR_OOM, NHIP_ERR_ARG = range(5)
 _ERRORS = {1: "no HIP device", 2: "HIP runtime error", 3: "out of device memory", 4: "invalid argument"}
 
 _u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
@@ -84,6 +85,9 @@ SIGNATURES = {
     "nhip_air_destroy": ([_vp], None),
     "nhip_air_info": ([_vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                        ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+    "nhip_proof_from_be_bytes": ([ctypes.c_void_p, _sz, ctypes.c_void_p, _sz, ctypes.POINTER(_sz)], ctypes.c_int),
+    "nhip_proof_to_be_bytes": ([ctypes.c_void_p, _sz, ctypes.c_void_p], ctypes.c_int),
+    "nhip_claim_hash": ([_vp, ctypes.POINTER(Claim), _u64p], ctypes.c_int),
     "nhip_proof_decodes": ([_vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof)],
                            ctypes.c_int),
     "nhip_verify_batch": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof),
