@@ -185,6 +185,41 @@ int nhip_proof_to_be_bytes(const uint64_t *words, size_t n, uint8_t *out);
 /* Tip5::hash(claim) = hash_varlen(claim.encode()) (program.rs:355-358, proof file name). */
 int nhip_claim_hash(nhip_ctx *ctx, const nhip_claim *claim, uint64_t digest_out[5]);
 
+/* ---- proof of work (neptune-core/src/protocol/consensus/block/pow.rs) ---
+ * PowMastPaths (pow.rs:202-207): MAST authentication paths of the pow field (BlockHeader, 3),
+ * the header (BlockKernel, 2) and the kernel (Block, 1); canonical digests. */
+typedef struct {
+    uint64_t pow[3][5];
+    uint64_t header[2][5];
+    uint64_t kernel[1][5];
+} nhip_pow_mast_paths;
+typedef struct nhip_pow_buffer nhip_pow_buffer;
+/* PowMastPaths::commit (pow.rs:209-217) */
+int nhip_pow_mast_commit(nhip_ctx *ctx, const nhip_pow_mast_paths *mast, uint64_t out[5]);
+/* Pow::preprocess (pow.rs:365-469): the guesser buffer of 2^height leaves (buds, 5 bud layers, the
+ * HardforkAlpha bit-reversal swap unless reboot_rules, MTree::build_inplace), resident on the
+ * device (2 x 2^height x 40 B).  reboot_rules: ConsensusRuleSet::Reboot (bud prefix = mast
+ * commit); else HardforkAlpha (bud prefix = prev_block_digest). */
+int nhip_pow_preprocess(nhip_ctx *ctx, uint32_t height, const nhip_pow_mast_paths *mast, int reboot_rules,
+                        const uint64_t prev_block_digest[5], nhip_pow_buffer **out);
+void nhip_pow_buffer_destroy(nhip_pow_buffer *buffer);
+/* MTree::root / leafs[index] / MTree::path (pow.rs:147-160) of the buffer's tree */
+int nhip_pow_buffer_root(nhip_ctx *ctx, const nhip_pow_buffer *buffer, uint64_t out[5]);
+int nhip_pow_buffer_leaf(nhip_ctx *ctx, const nhip_pow_buffer *buffer, uint64_t index, uint64_t out[5]);
+int nhip_pow_buffer_path(nhip_ctx *ctx, const nhip_pow_buffer *buffer, uint64_t index, uint64_t *out /* height x 5 */);
+/* Pow::guess (pow.rs:471-507) for n nonces: pow digests (fast_mast_hash), the two opened indices,
+ * and success = (digest <= target) under twenty-first's Digest ordering (unpinned: canonical
+ * values compared from the last element down).  digests_out / indices_out nullable. */
+int nhip_pow_guess_batch(nhip_ctx *ctx, const nhip_pow_buffer *buffer, const nhip_pow_mast_paths *mast,
+                         const uint64_t index_picker_preimage[5], const uint64_t *nonces, size_t n,
+                         const uint64_t target[5], uint64_t *digests_out, uint64_t *indices_out, uint8_t *success_out);
+/* Pow::validate (pow.rs:509-557) for n blocks: verdicts[i] = 1 iff both paths verify against the
+ * root and the pow digest meets the target.  paths: n x height x 5; reboot_rules: n bytes. */
+int nhip_pow_validate_batch(nhip_ctx *ctx, uint32_t height, const uint64_t *roots, const uint64_t *paths_a,
+                            const uint64_t *paths_b, const uint64_t *nonces, const nhip_pow_mast_paths *masts,
+                            const uint64_t *targets, const uint64_t *parents, const uint8_t *reboot_rules, size_t n,
+                            uint8_t *verdicts);
+
 /* ---- kernel timing (HIP events on the ctx stream around every kernel launch) ------------ */
 int nhip_timing_enable(nhip_ctx *ctx, int on);
 /* Total device time of the kernels launched since the last reset, and their count. */

@@ -88,6 +88,18 @@ SIGNATURES = {
     "nhip_proof_from_be_bytes": ([ctypes.c_void_p, _sz, ctypes.c_void_p, _sz, ctypes.POINTER(_sz)], ctypes.c_int),
     "nhip_proof_to_be_bytes": ([ctypes.c_void_p, _sz, ctypes.c_void_p], ctypes.c_int),
     "nhip_claim_hash": ([_vp, ctypes.POINTER(Claim), _u64p], ctypes.c_int),
+    "nhip_pow_mast_commit": ([_vp, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "nhip_pow_preprocess": ([_vp, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                             ctypes.POINTER(_vp)], ctypes.c_int),
+    "nhip_pow_buffer_destroy": ([_vp], None),
+    "nhip_pow_buffer_root": ([_vp, _vp, ctypes.c_void_p], ctypes.c_int),
+    "nhip_pow_buffer_leaf": ([_vp, _vp, ctypes.c_uint64, ctypes.c_void_p], ctypes.c_int),
+    "nhip_pow_buffer_path": ([_vp, _vp, ctypes.c_uint64, ctypes.c_void_p], ctypes.c_int),
+    "nhip_pow_guess_batch": ([_vp, _vp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _sz, ctypes.c_void_p,
+                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "nhip_pow_validate_batch": ([_vp, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                 _sz, ctypes.c_void_p], ctypes.c_int),
     "nhip_proof_decodes": ([_vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof)],
                            ctypes.c_int),
     "nhip_verify_batch": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof),
