@@ -220,6 +220,18 @@ int nhip_pow_validate_batch(nhip_ctx *ctx, uint32_t height, const uint64_t *root
                             const uint64_t *targets, const uint64_t *parents, const uint8_t *reboot_rules, size_t n,
                             uint8_t *verdicts);
 
+/* ---- MAST and mutator-set hashing ----------------------------------
+ * MastHash::mast_hash (neptune-core/src/protocol/proof_abstractions/mast_hash.rs:22-39) of n
+ * objects with `fields` (1..16) field sequences each (TransactionKernel: 8): sequence (i, f) =
+ * data[offsets[i*fields+f] .. offsets[i*fields+f+1]); roots_out: n digests. */
+int nhip_mast_hash_batch(nhip_ctx *ctx, const uint64_t *data, const uint64_t *offsets, uint32_t fields, size_t n,
+                         uint64_t *roots_out);
+/* AbsoluteIndexSet::compute (util_types/mutator_set/removal_record/absolute_index_set.rs:86-113)
+ * for n removal records: minimum_out n x 2 u64 (u128, little-endian), distances_out n x 45 u32. */
+int nhip_absolute_index_sets(nhip_ctx *ctx, const uint64_t *items, const uint64_t *sender_randomness,
+                             const uint64_t *receiver_preimages, const uint64_t *aocl_leaf_indices, size_t n,
+                             uint64_t *minimum_out, uint32_t *distances_out);
+
 /* ---- kernel timing (HIP events on the ctx stream around every kernel launch) ------------ */
 int nhip_timing_enable(nhip_ctx *ctx, int on);
 /* Total device time of the kernels launched since the last reset, and their count. */

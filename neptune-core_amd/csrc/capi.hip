@@ -439,4 +439,75 @@ int nhip_timing_read(nhip_ctx* c, double* total_ms, uint64_t* launches, int rese
     return NHIP_OK;
 }
 
+// MastHash::mast_hash (mast_hash.rs:22-39) for n objects of `fields` field sequences each:
+// field sequence (i, f) = data[offsets[i*fields+f] .. offsets[i*fields+f+1]).
+int nhip_mast_hash_batch(nhip_ctx* c, const uint64_t* data, const uint64_t* offsets, uint32_t fields, size_t n,
+                         uint64_t* roots_out) {
+    if (!c || fields < 1 || fields > 16 || (n && (!offsets || !roots_out))) return NHIP_ERR_ARG;
+    if (n == 0) return NHIP_OK;
+    const size_t nl = n * fields;
+    for (size_t i = 0; i < nl; ++i)
+        if (offsets[i + 1] < offsets[i]) return NHIP_ERR_ARG;
+    const size_t total = (size_t)offsets[nl];
+    if (total && !data) return NHIP_ERR_ARG;
+    uint32_t pow2 = 1;
+    while (pow2 < fields) pow2 <<= 1;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    size_t sizes[4] = {total * 8, (nl + 1) * 8, nl * 40, n * 40};
+    void* p[4];
+    int rc = carve(c, sizes, p);
+    if (rc) return rc;
+    hipError_t e = hipSuccess;
+    if (total) e = hipMemcpyAsync(p[0], data, sizes[0], hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(p[1], offsets, sizes[1], hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_fail(e);
+    rc = timed_launch(c, [&] {
+        return nhip::launch_hash_varlen((const uint64_t*)p[0], (const uint64_t*)p[1], nl, (uint64_t*)p[2], c->stream);
+    });
+    if (rc) return rc;
+    rc = timed_launch(c, [&] {
+        return nhip::launch_mast_roots((const uint64_t*)p[2], fields, pow2, n, (uint64_t*)p[3], c->stream);
+    });
+    if (rc) return rc;
+    e = hipMemcpyAsync(roots_out, p[3], sizes[3], hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return hip_fail(e);
+}
+
+// AbsoluteIndexSet::compute (absolute_index_set.rs:86-113) for n removal records.
+int nhip_absolute_index_sets(nhip_ctx* c, const uint64_t* items, const uint64_t* sender_randomness,
+                             const uint64_t* receiver_preimages, const uint64_t* aocl_leaf_indices, size_t n,
+                             uint64_t* minimum_out, uint32_t* distances_out) {
+    if (!c || (n && (!items || !sender_randomness || !receiver_preimages || !aocl_leaf_indices || !minimum_out ||
+                     !distances_out)))
+        return NHIP_ERR_ARG;
+    if (n == 0) return NHIP_OK;
+    std::vector<uint64_t> in(15 * n);
+    for (size_t i = 0; i < n; ++i)
+        for (int q = 0; q < 5; ++q) {
+            in[15 * i + q] = items[5 * i + q];
+            in[15 * i + 5 + q] = sender_randomness[5 * i + q];
+            in[15 * i + 10 + q] = receiver_preimages[5 * i + q];
+        }
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    size_t sizes[4] = {15 * n * 8, n * 8, 2 * n * 8, 45 * n * 4};
+    void* p[4];
+    int rc = carve(c, sizes, p);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(p[0], in.data(), sizes[0], hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(p[1], aocl_leaf_indices, sizes[1], hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_fail(e);
+    rc = timed_launch(c, [&] {
+        return nhip::launch_absolute_index_sets((const uint64_t*)p[0], (const uint64_t*)p[1], n, (uint64_t*)p[2],
+                                                (uint32_t*)p[3], c->stream);
+    });
+    if (rc) return rc;
+    e = hipMemcpyAsync(minimum_out, p[2], sizes[2], hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(distances_out, p[3], sizes[3], hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return hip_fail(e);
+}
+
 }  // extern "C"

@@ -18,6 +18,12 @@ hipError_t launch_mtree_verify(const uint64_t* d_roots, int per_path_root, const
                                const uint64_t* d_leaves, const uint64_t* d_paths, uint32_t depth, size_t n,
                                uint8_t* d_verdicts, hipStream_t st);
 
+// ---- MAST / mutator-set hashing (mast_kernels.hip)
+hipError_t launch_mast_roots(const uint64_t* d_leaves, uint32_t fields, uint32_t pow2, size_t n, uint64_t* d_roots,
+                             hipStream_t st);
+hipError_t launch_absolute_index_sets(const uint64_t* d_digests, const uint64_t* d_aocl, size_t n, uint64_t* d_min,
+                                      uint32_t* d_dist, hipStream_t st);
+
 // ---- batched STARK verifier (stark_kernels.hip)
 static constexpr uint32_t AIR_LDS_HEADER = (256 + 4 + 4 + 4) * 24 + 16;  // red, zinv, derived, misc, flag
 

@@ -100,6 +100,10 @@ SIGNATURES = {
     "nhip_pow_validate_batch": ([_vp, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                  _sz, ctypes.c_void_p], ctypes.c_int),
+    "nhip_mast_hash_batch": ([_vp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, _sz, ctypes.c_void_p],
+                             ctypes.c_int),
+    "nhip_absolute_index_sets": ([_vp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _sz,
+                                  ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "nhip_proof_decodes": ([_vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof)],
                            ctypes.c_int),
     "nhip_verify_batch": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof),
