@@ -28,8 +28,10 @@ using namespace nhip;
 namespace {
 
 constexpr uint64_t P = GL_P;
-constexpr size_t OUT_HDR = 16;
-constexpr uint32_t AUX_AFTER_LEVEL_DEFAULT = 0;  // tuned on MI355X  // pinned readback: [skipped ops u64 | pad | plan counters | verdicts]
+constexpr size_t OUT_HDR = 16;  // pinned readback: [skipped ops u64 | pad | plan counters | verdicts]
+// hash levels launched before the OOD / FRI / DEEP chain is released (NHIP_AUX_AFTER_LEVEL
+// overrides); tuned on MI355X
+constexpr uint32_t AUX_AFTER_LEVEL_DEFAULT = 0;
 
 enum ItemKind : uint32_t {
     MERKLE_ROOT = 0, OOD_MAIN_ROW, OOD_AUX_ROW, OOD_QUOT_SEGMENTS, AUTH_STRUCTURE, MAIN_ROWS, AUX_ROWS,
