@@ -11,6 +11,16 @@
   digests, `Digest::reversed()`), the member proofs verified (here: one batch instead of the
   sequential awaits at :343-385, zip-truncated like the reference's `zip`) and AND-ed (:388).
   `ProofCollection.verify_many` batches many collections (a mempool batch) in one call.
+* `single_proof_claim` / `TransactionProof.verify_many` — single_proof.rs:227-230,295-304 and
+  transaction_proof.rs:134-153: a SingleProof is one claim (the SingleProof program with input =
+  the kernel MAST hash reversed), a ProofCollection its members; any mix of transactions goes
+  into one GPU batch.  `transactions_are_valid` adds `Transaction::is_valid`'s kernel MAST hash
+  (transaction/mod.rs:172-177), computed on the GPU from the kernel's field encodings.
+* `BlockProgram.claim` / `validate_block_proofs` — block_program.rs:45-65 (input = body MAST
+  hash reversed, output = `BlockAppendix::claims_as_output`, the Tip5 hashes of the appendix
+  claims; block_appendix.rs:40-47) and `Block::validate` rules 1.a-1.d (block/mod.rs:783-804)
+  for a batch of blocks (bootstrap import `state/mod.rs:2226-2272`, peer block batches
+  `peer_loop.rs:315-323`): every block proof of the batch in one GPU batch.
 The consensus programs' digests (RemovalRecordsIntegrity, KernelToOutputs, CollectLockScripts,
 CollectTypeScripts) come from tasm-lib code generation, which is not vendored, so they are
 parameters (`ConsensusPrograms`).
@@ -67,11 +77,19 @@ def _rev(d: Sequence[int]) -> List[int]:
 
 @dataclass
 class ConsensusPrograms:
-    """Program digests of the four ProofCollection consensus programs (tasm-lib codegen)."""
+    """Program digests of the consensus programs (tasm-lib codegen): the four ProofCollection
+    programs, SingleProof and BlockProgram."""
     removal_records_integrity: Sequence[int]
     kernel_to_outputs: Sequence[int]
     collect_lock_scripts: Sequence[int]
     collect_type_scripts: Sequence[int]
+    single_proof: Sequence[int] = (0, 0, 0, 0, 0)
+    block_program: Sequence[int] = (0, 0, 0, 0, 0)
+
+
+def single_proof_claim(txk_mast_hash: Sequence[int], programs: ConsensusPrograms) -> Claim:
+    """single_proof.rs:227-230 (`SingleProof::claim`), selected for both rule sets by :295-304."""
+    return Claim(list(programs.single_proof), 0, _rev(txk_mast_hash), [])
 
 
 @dataclass
@@ -131,3 +149,125 @@ class ProofCollection:
         for ci, v in zip(owner, verdicts):
             out[ci] = out[ci] and v
         return out
+
+
+# ------------------------------------------------------------------ transactions
+WITNESS, SINGLE_PROOF, PROOF_COLLECTION = "witness", "single_proof", "proof_collection"
+
+
+@dataclass
+class TransactionProof:
+    """transaction_proof.rs: `Witness(PrimitiveWitness)`, `SingleProof(Proof)` or
+    `ProofCollection(ProofCollection)`; `payload` is the proof words or the ProofCollection."""
+    kind: str
+    payload: object = None
+
+    @staticmethod
+    def verify_many(items: Sequence[Tuple["TransactionProof", Sequence[int]]], verifier: Verifier,
+                    programs: ConsensusPrograms, network: Network = Network.MAIN) -> List[bool]:
+        """`TransactionProof::verify(kernel_mast_hash, ..)` for many transactions in ONE verifier batch.
+        A primitive witness is validated by running the consensus programs on the host
+        (`PrimitiveWitness::validate`), which is not a STARK verification and not on this path."""
+        pairs, owner, out = [], [], []
+        for ti, (tp, txk) in enumerate(items):
+            if tp.kind == SINGLE_PROOF:
+                pairs.append((single_proof_claim(txk, programs), tp.payload))
+                owner.append(ti)
+                out.append(True)
+            elif tp.kind == PROOF_COLLECTION:
+                pc = tp.payload
+                ok = [int(x) for x in pc.kernel_mast_hash] == [int(x) for x in txk]  # proof_collection.rs:280-282
+                out.append(ok)
+                if ok:
+                    for pr in pc.claims_and_proofs(programs):
+                        pairs.append(pr)
+                        owner.append(ti)
+            elif tp.kind == WITNESS:
+                raise ValueError("a primitive witness is validated on the host, not by the STARK verifier")
+            else:
+                raise ValueError(f"unknown transaction proof kind {tp.kind!r}")
+        verdicts = verifier.verify_batch(pairs, network)
+        for ti, v in zip(owner, verdicts):
+            out[ti] = out[ti] and v
+        return out
+
+
+def transactions_are_valid(ctx, items: Sequence[Tuple[Sequence[Sequence[int]], TransactionProof]],
+                           verifier: Verifier, programs: ConsensusPrograms,
+                           network: Network = Network.MAIN) -> List[bool]:
+    """`Transaction::is_valid` (transaction/mod.rs:172-177) for many transactions: the kernel MAST
+    hashes (`kernel.mast_hash()`; items carry each kernel's 8 field encodings,
+    transaction_kernel.rs:246-277) in one GPU call, then every proof in one verifier batch."""
+    if not items:
+        return []
+    from .mast import mast_hash_batch
+    hashes = mast_hash_batch(ctx, [fields for fields, _ in items])
+    return TransactionProof.verify_many([(tp, h) for (_, tp), h in zip(items, hashes)], verifier, programs, network)
+
+
+# ------------------------------------------------------------------ blocks
+MAX_NUM_CLAIMS = 500                 # block_appendix.rs:19
+GENESIS, INVALID = "genesis", "invalid"   # BlockProof (block/mod.rs:114-119); SINGLE_PROOF as above
+
+
+def claims_as_output(ctx, claims: Sequence[Claim]) -> List[int]:
+    """`BlockAppendix::claims_as_output` (block_appendix.rs:40-47): the concatenated Tip5 hashes of
+    the appendix claims (`Tip5::hash(claim)`, on the GPU)."""
+    from .proof_files import claim_hash
+    return [int(x) for c in claims for x in claim_hash(ctx, c)]
+
+
+class BlockProgram:
+    @staticmethod
+    def claim(ctx, body_mast_hash: Sequence[int], appendix: Sequence[Claim], programs: ConsensusPrograms) -> Claim:
+        """block_program.rs:45-49."""
+        return Claim(list(programs.block_program), 0, _rev(body_mast_hash), claims_as_output(ctx, appendix))
+
+
+@dataclass
+class BlockToValidate:
+    """What `Block::validate` rules 1.a-1.d read: the body MAST hash, the transaction kernel's MAST
+    hash, the appendix claims and the block proof (`kind` GENESIS / INVALID / SINGLE_PROOF)."""
+    body_mast_hash: Sequence[int]
+    tx_kernel_mast_hash: Sequence[int]
+    appendix: Sequence[Claim]
+    proof_kind: str
+    proof: object = None
+
+
+# BlockValidationError variants of rules 1.a-1.d (block/mod.rs:783-804); None = passed
+APPENDIX_MISSING_CLAIM, APPENDIX_TOO_LARGE, PROOF_QUALITY, PROOF_VALIDITY = (
+    "AppendixMissingClaim", "AppendixTooLarge", "ProofQuality", "ProofValidity")
+
+
+def _same_claim(a: Claim, b: Claim) -> bool:
+    key = lambda c: ([int(x) for x in c.program_digest], int(c.version), [int(x) for x in c.input],  # noqa: E731
+                     [int(x) for x in c.output])
+    return key(a) == key(b)
+
+
+def validate_block_proofs(ctx, blocks: Sequence[BlockToValidate], verifier: Verifier, programs: ConsensusPrograms,
+                          network: Network = Network.MAIN) -> List[Optional[str]]:
+    """`Block::validate` rules 1.a-1.d, in the reference's order, for a batch of blocks; the
+    BlockProgram proofs of all blocks that reach 1.d are verified in ONE GPU batch."""
+    out: List[Optional[str]] = []
+    pairs, owner = [], []
+    for bi, blk in enumerate(blocks):
+        required = [single_proof_claim(blk.tx_kernel_mast_hash, programs)]  # consensus_claims, :53-61
+        if not all(any(_same_claim(r, c) for c in blk.appendix) for r in required):
+            out.append(APPENDIX_MISSING_CLAIM)
+        elif len(blk.appendix) > MAX_NUM_CLAIMS:
+            out.append(APPENDIX_TOO_LARGE)
+        elif blk.proof_kind != SINGLE_PROOF:
+            out.append(PROOF_QUALITY)
+        else:
+            out.append(None)
+            claim = (Claim(list(programs.block_program), 0, [], []) if network.use_mock_proof()
+                     else BlockProgram.claim(ctx, blk.body_mast_hash, blk.appendix, programs))
+            pairs.append((claim, blk.proof))
+            owner.append(bi)
+    verdicts = verifier.verify_batch(pairs, network)
+    for bi, v in zip(owner, verdicts):
+        if not v:
+            out[bi] = PROOF_VALIDITY
+    return out

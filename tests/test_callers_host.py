@@ -74,3 +74,41 @@ def test_mock_network_gate_never_runs_the_verifier():
     assert out == [True, False, False]
     with pytest.raises(AttributeError):
         ver.verify_batch(pairs, V.Network.MAIN)  # a real network needs a GPU context
+
+
+PROGS6 = V.ConsensusPrograms([1] * 5, [2] * 5, [3] * 5, [4] * 5, single_proof=[5] * 5, block_program=[6] * 5)
+
+
+def test_single_proof_claim_and_transaction_dispatch_mock():
+    txk = [10, 11, 12, 13, 14]
+    c = V.single_proof_claim(txk, PROGS6)
+    assert (c.program_digest, c.version, c.input, c.output) == ([5] * 5, 0, [14, 13, 12, 11, 10], [])
+    ver = V.Verifier(ctx=None, air=None, stark=V.Stark())
+    pc = _collection()
+    items = [(V.TransactionProof(V.SINGLE_PROOF, [0]), txk), (V.TransactionProof(V.SINGLE_PROOF, [1]), txk),
+             (V.TransactionProof(V.PROOF_COLLECTION, pc), pc.kernel_mast_hash),
+             (V.TransactionProof(V.PROOF_COLLECTION, pc), txk)]  # collection of another kernel
+    assert V.TransactionProof.verify_many(items, ver, PROGS6, V.Network.REGTEST) == [True, False, True, False]
+    with pytest.raises(ValueError):
+        V.TransactionProof.verify_many([(V.TransactionProof(V.WITNESS, None), txk)], ver, PROGS6, V.Network.REGTEST)
+
+
+def test_block_rules_1a_to_1d_in_reference_order_mock():
+    ver = V.Verifier(ctx=None, air=None, stark=V.Stark())
+    txk, body = [1, 2, 3, 4, 5], [7, 7, 7, 7, 8]
+    tx_claim = V.single_proof_claim(txk, PROGS6)
+    other = Claim([9] * 5, 0, [], [])
+
+    def blk(appendix, kind=V.SINGLE_PROOF, proof=(0,)):
+        return V.BlockToValidate(body, txk, appendix, kind, list(proof))
+
+    blocks = [blk([tx_claim]),                                  # valid (mock)
+              blk([other]),                                     # 1.a missing consensus claim
+              blk([other] * 500 + [tx_claim]),                  # 1.b more than MAX_NUM_CLAIMS
+              blk([tx_claim], kind=V.GENESIS, proof=()),        # 1.c not a SingleProof
+              blk([tx_claim], proof=(1,)),                      # 1.d invalid mock
+              blk([other, tx_claim]),                           # extra claims are fine
+              blk([Claim(tx_claim.program_digest, 0, tx_claim.input[::-1], [])])]  # un-reversed input
+    assert V.validate_block_proofs(None, blocks, ver, PROGS6, V.Network.REGTEST) == [
+        None, V.APPENDIX_MISSING_CLAIM, V.APPENDIX_TOO_LARGE, V.PROOF_QUALITY, V.PROOF_VALIDITY, None,
+        V.APPENDIX_MISSING_CLAIM]

@@ -81,3 +81,47 @@ def test_proof_collection_verify_on_gpu(ctx):
     # the oracle agrees member by member
     assert all(S.verify(params, air, (c.program_digest, c.version, c.input, c.output), p)
                for (c, _), p in zip(pairs, proofs))
+
+
+def test_transactions_and_blocks_on_gpu(ctx):
+    """Transaction::is_valid (kernel MAST hash on the GPU, then the SingleProof claim) and
+    Block::validate rules 1.a-1.d over a batch of blocks, with every proof made for exactly the
+    claim the mirror builds; BlockProgram's claim output equals the oracle's claim hashes."""
+    import mast_ref as M
+    _, NS, V = _mods()
+    T.use_c_backend()
+    params = S.StarkParams()
+    air, recipe = S.synth_air(params, seed=1)
+    rng = np.random.default_rng(0x7B)
+    d = lambda k: [k, 3 * k, 5 * k, 7 * k, 11 * k]  # noqa: E731
+    progs = V.ConsensusPrograms(d(1001), d(1002), d(1003), d(1004), single_proof=d(1005), block_program=d(1006))
+    ver = V.Verifier(ctx, NS.Air(air.to_words()))
+    prove = lambda c, h, seed: np.asarray(  # noqa: E731
+        K.prove(params, air, recipe, (c.program_digest, c.version, c.input, c.output), h, seed=seed)[0], dtype=np.uint64)
+    # two transactions: kernel field encodings -> MAST hash -> SingleProof claim
+    kernels = [[list(rng.integers(0, T.P, size=int(rng.integers(1, 12)), dtype=np.uint64)) for _ in range(8)]
+               for _ in range(2)]
+    txk = [M.mast_hash(k) for k in kernels]
+    sp = [prove(V.single_proof_claim(h, progs), 9, seed=i + 1) for i, h in enumerate(txk)]
+    items = [(kernels[0], V.TransactionProof(V.SINGLE_PROOF, sp[0])),
+             (kernels[1], V.TransactionProof(V.SINGLE_PROOF, sp[1])),
+             (kernels[1], V.TransactionProof(V.SINGLE_PROOF, sp[0]))]  # proof of the other kernel
+    assert V.transactions_are_valid(ctx, items, ver, progs) == [True, True, False]
+    # blocks: appendix = [transaction validity claim] (+ an extra claim), BlockProgram proof
+    body = [list(rng.integers(0, T.P, size=5, dtype=np.uint64)) for _ in range(2)]
+    appendix = [[V.single_proof_claim(txk[0], progs)],
+                [V.single_proof_claim(txk[1], progs), NS.Claim(d(77), 0, [1, 2], [3])]]
+    bclaims = [V.BlockProgram.claim(ctx, body[i], appendix[i], progs) for i in range(2)]
+    for bc, app in zip(bclaims, appendix):
+        want = [int(x) for c in app for x in T.hash_varlen(S.encode_claim(c.program_digest, c.version, c.input, c.output))]
+        assert bc.output == want
+    bproofs = [prove(bclaims[i], 10, seed=20 + i) for i in range(2)]
+    blocks = [V.BlockToValidate(body[0], txk[0], appendix[0], V.SINGLE_PROOF, bproofs[0]),
+              V.BlockToValidate(body[1], txk[1], appendix[1], V.SINGLE_PROOF, bproofs[1]),
+              V.BlockToValidate(body[1], txk[1], appendix[1], V.SINGLE_PROOF, bproofs[0]),  # other block's proof
+              V.BlockToValidate(body[0], txk[1], appendix[0], V.SINGLE_PROOF, bproofs[0]),  # claim missing
+              V.BlockToValidate(body[0], txk[0], appendix[0], V.GENESIS, None)]
+    assert V.validate_block_proofs(ctx, blocks, ver, progs) == [
+        None, None, V.PROOF_VALIDITY, V.APPENDIX_MISSING_CLAIM, V.PROOF_QUALITY]
+    assert all(S.verify(params, air, (c.program_digest, c.version, c.input, c.output), p)
+               for c, p in zip(bclaims, bproofs))
