@@ -39,7 +39,7 @@ def _parse():
     for m in re.finditer(r"void mont_mul(\d+)_asm\(.*?\n}\n", src, re.S):
         n = int(m.group(1))
         stmts = []
-        for a in re.finditer(r'asm volatile\("(.*?)"\s*:(.*?):(.*?)\);', m.group(0), re.S):
+        for a in re.finditer(r'asm(?: volatile)?\("(.*?)"\s*:(.*?):(.*?)\);', m.group(0), re.S):
             lines = a.group(1).split("\\n\\t")
             ops = [(c, name, int(i)) for c, name, i in
                    re.findall(r'"([=&+]*[vs])"\((\w+)\[(\d+)\]\)', a.group(2) + "," + a.group(3))]
