@@ -85,6 +85,22 @@ K64(k_lshladd64, "v_lshl_add_u64 %0, %1, 2, %0")
 K64(k_lshr64, "v_lshrrev_b64 %0, 3, %0")
 K64(k_cmp64, "v_cmp_lt_u64_e32 vcc, %0, %1")
 K64(k_fma64, "v_fma_f64 %0, %1, %0, %1")
+// second batch: the remaining instruction classes of the Tip5 round
+K32(k_mov_e32, "v_mov_b32_e32 %0, %1")
+K32(k_or_e32, "v_or_b32_e32 %0, %1, %0")
+K32(k_and_e32, "v_and_b32_e32 %0, %1, %0")
+K32(k_sub_e32, "v_sub_u32_e32 %0, %1, %0")
+K32(k_lshl_or, "v_lshl_or_b32 %0, %1, 8, %0")
+K32(k_or3, "v_or3_b32 %0, %1, %0, %2")
+K32(k_lshl_add32, "v_lshl_add_u32 %0, %1, 3, %0")
+K32(k_alignbit, "v_alignbit_b32 %0, %1, %0, 7")
+K32(k_lshr_e32, "v_lshrrev_b32_e32 %0, %1, %0")
+K32(k_max_e32, "v_max_u32_e32 %0, %1, %0")
+K32(k_subco_e32, "v_sub_co_u32_e32 %0, vcc, %1, %0")
+K32(k_subb_e32, "v_subb_co_u32_e32 %0, vcc, %1, %0, vcc")
+K32(k_subbrev_e32, "v_subbrev_co_u32_e32 %0, vcc, 0, %0, vcc")
+K64(k_mov64, "v_mov_b64 %0, %1")
+K64(k_lshl64, "v_lshlrev_b64 %0, 3, %0")
 
 __global__ void k_ds_u8(uint32_t* out, uint32_t s) {
     __shared__ uint8_t lut[256];
@@ -128,11 +144,17 @@ int main() {
         {"v_add_co_u32_e32(vcc)", k_addco_e32, 8, 0}, {"v_addc_co_u32_e32 chain", k_addc_e32, 8, 0},
         {"v_mad_u64_u32", k_mad64, 8, 0}, {"v_lshl_add_u64", k_lshladd64, 8, 0}, {"v_lshrrev_b64", k_lshr64, 8, 0},
         {"v_cmp_lt_u64_e32", k_cmp64, 8, 0}, {"v_fma_f64", k_fma64, 8, 0},
+        {"v_mov_b32_e32", k_mov_e32, 8, 0}, {"v_or_b32_e32", k_or_e32, 8, 0}, {"v_and_b32_e32", k_and_e32, 8, 0},
+        {"v_sub_u32_e32", k_sub_e32, 8, 0}, {"v_lshl_or_b32", k_lshl_or, 8, 0}, {"v_or3_b32", k_or3, 8, 0},
+        {"v_lshl_add_u32", k_lshl_add32, 8, 0}, {"v_alignbit_b32", k_alignbit, 8, 0},
+        {"v_lshrrev_b32_e32(vgpr)", k_lshr_e32, 8, 0}, {"v_max_u32_e32", k_max_e32, 8, 0},
+        {"v_sub_co_u32_e32(vcc)", k_subco_e32, 8, 0}, {"v_subb_co_u32_e32 chain", k_subb_e32, 8, 0},
+        {"v_subbrev_co_u32_e32 chain", k_subbrev_e32, 8, 0}, {"v_mov_b64", k_mov64, 8, 0},
         {"ds_read_u8 256B (+3 valu)", k_ds_u8, 8, 0}, {"ds_read_u16 128KiB (+3 valu)", k_ds_u16_128k, 8, 131072}};
     hipEvent_t a, b; CHECK(hipEventCreate(&a)); CHECK(hipEventCreate(&b));
     CHECK(hipFuncSetAttribute((const void*)k_ds_u16_128k, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
     printf("CUs=%d\n", cus);
-    for (int waves_per_simd : {8, 2, 1}) {
+    for (int waves_per_simd : {8, 4, 1}) {
         double base = 0;
         printf("--- %d waves/SIMD ---\n", waves_per_simd);
         for (auto& k : ks) {
