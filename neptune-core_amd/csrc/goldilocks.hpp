@@ -10,10 +10,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#ifndef NHIP_MM_V2
-#define NHIP_MM_V2 0
-#endif
-
 namespace nhip {
 
 static constexpr uint64_t GL_P = 0xFFFFFFFF00000001ull;
@@ -77,26 +73,12 @@ __host__ __device__ __forceinline__ void mont_mul_n(const uint64_t* a, const uin
     for (int i = 0; i < N; ++i) p00[i] = (uint64_t)(uint32_t)a[i] * (uint32_t)b[i];
 #pragma unroll
     for (int i = 0; i < N; ++i) t[i] = (uint64_t)(uint32_t)a[i] * (uint32_t)(b[i] >> 32) + (p00[i] >> 32);
-#if NHIP_MM_V2
-    // u = a1 * b0 + t as a 65-bit value; xh = a1 * b1 + (u >> 32) (< 2^64 for a, b < p).  Measured
-    // slower on MI355X (k_mtree_verify 4.63 -> 4.44e9 perms/s): 3% fewer VALU ops, 30% more s_nop.
-    uint64_t uh[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        const unsigned __int128 w = (unsigned __int128)((uint64_t)(uint32_t)(a[i] >> 32) * (uint32_t)b[i]) + t[i];
-        u[i] = (uint64_t)w;
-        uh[i] = (uint64_t)(w >> 32);
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) xh[i] = (uint64_t)(uint32_t)(a[i] >> 32) * (uint32_t)(b[i] >> 32) + uh[i];
-#else
 #pragma unroll
     for (int i = 0; i < N; ++i) u[i] = (uint64_t)(uint32_t)(a[i] >> 32) * (uint32_t)b[i] + (uint32_t)t[i];
 #pragma unroll
     for (int i = 0; i < N; ++i) xh[i] = (uint64_t)(uint32_t)(a[i] >> 32) * (uint32_t)(b[i] >> 32) + (t[i] >> 32);
 #pragma unroll
     for (int i = 0; i < N; ++i) xh[i] += (u[i] >> 32);
-#endif
 #pragma unroll
     for (int i = 0; i < N; ++i) ah[i] = __builtin_addc((uint32_t)u[i], (uint32_t)p00[i], 0u, &e[i]);
 #pragma unroll
