@@ -19,6 +19,8 @@ struct nhip_ctx {
     std::mutex mu;
     void* ws = nullptr;  // workspace for host-buffer calls
     size_t ws_bytes = 0;
+    void* staging = nullptr;  // pinned host staging for batch uploads (grow-only, under mu)
+    size_t staging_bytes = 0;
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;  // recorded, not yet read
     std::vector<hipEvent_t> free_events;
@@ -173,6 +175,7 @@ void nhip_destroy(nhip_ctx* c) {
     }
     for (auto e : c->free_events) (void)hipEventDestroy(e);
     if (c->ws) (void)hipFree(c->ws);
+    if (c->staging) (void)hipHostFree(c->staging);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -183,6 +186,20 @@ int nhip_device_ordinal(const nhip_ctx* c) { return c ? c->device : -1; }
 hipStream_t nhip_internal_stream(nhip_ctx* c) { return c->stream; }
 int nhip_internal_device(nhip_ctx* c) { return c->device; }
 std::mutex* nhip_internal_mutex(nhip_ctx* c) { return &c->mu; }
+// Pinned staging of at least `bytes` (caller holds c->mu); nullptr if it cannot be pinned.
+void* nhip_internal_staging(nhip_ctx* c, size_t bytes) {
+    if (bytes <= c->staging_bytes) return c->staging;
+    if (c->staging) (void)hipHostFree(c->staging);
+    c->staging = nullptr;
+    c->staging_bytes = 0;
+    const size_t want = bytes + bytes / 4;  // headroom for slightly larger batches
+    if (hipHostMalloc(&c->staging, want, hipHostMallocDefault) != hipSuccess) {
+        c->staging = nullptr;
+        return nullptr;
+    }
+    c->staging_bytes = want;
+    return c->staging;
+}
 
 // ------------------------------------------------------------------ device-resident form
 int nhip_dev_alloc(nhip_ctx* c, size_t bytes, void** dptr) {

@@ -11,11 +11,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/neptune_hip.h"
@@ -127,10 +129,10 @@ bool decode_item(const uint64_t* w, uint64_t lo, uint64_t hi, const Dims& D, Ite
 
 struct HostBatch {
     Dims D;
-    std::vector<uint64_t> words;
     std::vector<ProofDesc> desc;
     std::vector<FsOp> ops;
     std::vector<uint32_t> fail;
+    uint64_t words_total = 0;  // proof words + staged claim encodings, uploaded to dev.words
     uint64_t xs_total = 0, idx_total = 0;
     uint32_t max_R = 0, max_last_cw = 1;
     uint64_t perms_static = 0;  // FS + row hashing (multiproof Merkle hashes are counted on device)
@@ -140,18 +142,30 @@ struct HostBatch {
 
 uint64_t absorb_perms(uint64_t len) { return len / 10 + 1; }
 
-// Decode proof p into its descriptor; on malformation mark FAIL_DECODE and leave a benign desc.
-void decode_proof(HostBatch& B, const nhip_claim& claim, const nhip_proof& proof) {
-    const Dims& D = B.D;
+// words one proof occupies in the batch buffer: the proof, then its staged claim encoding
+uint64_t staged_words(const nhip_claim& claim, const nhip_proof& proof) {
+    return proof.len + claim.output_len + claim.input_len + 10;
+}
+
+// What decoding one proof produces; merged into the HostBatch in proof order.
+struct ProofOut {
+    ProofDesc pd{};
+    std::vector<FsOp> ops;  // this proof's Fiat-Shamir program (absolute word offsets)
+    uint32_t fail = 0;
+    uint64_t perms = 0, perms_lcw = 0;
+};
+
+// Stage proof p at words[base, base + staged_words) (canonical: BFieldElement::new reduces) and
+// decode it into its descriptor; on malformation mark FAIL_DECODE and leave a benign desc.
+// Independent per proof: nhip_batch_prepare runs it on several host threads.
+void decode_proof(const Dims& D, const nhip_claim& claim, const nhip_proof& proof, uint64_t* words,
+                  uint64_t base, ProofOut& out) {
     const StarkDims& d = D.d;
     ProofDesc pd{};
     uint32_t fail = 0;
-    const uint64_t base = B.words.size();
     const uint64_t len = proof.len;
-    B.proof_words += len;
-    B.words.resize(base + len);
     {
-        uint64_t* dst = B.words.data() + base;
+        uint64_t* dst = words + base;
         const uint64_t* src = proof.words;
         for (uint64_t i = 0; i < len; ++i) {
             const uint64_t v = src[i];
@@ -159,23 +173,26 @@ void decode_proof(HostBatch& B, const nhip_claim& claim, const nhip_proof& proof
         }
     }
     // stage the claim encoding (pinned layout): [out_n+1, out_n, out.., in_n+1, in_n, in.., version, digest]
-    const uint64_t cbase = B.words.size();
-    B.words.push_back(claim.output_len + 1);
-    B.words.push_back(claim.output_len);
-    for (size_t i = 0; i < claim.output_len; ++i) B.words.push_back(claim.output[i] % P);
-    B.words.push_back(claim.input_len + 1);
-    B.words.push_back(claim.input_len);
-    for (size_t i = 0; i < claim.input_len; ++i) B.words.push_back(claim.input[i] % P);
-    B.words.push_back(claim.version);
-    for (int i = 0; i < 5; ++i) B.words.push_back(claim.program_digest[i] % P);
-    const uint64_t clen = B.words.size() - cbase;
+    const uint64_t cbase = base + len;
+    {
+        uint64_t* c = words + cbase;
+        *c++ = claim.output_len + 1;
+        *c++ = claim.output_len;
+        for (size_t i = 0; i < claim.output_len; ++i) *c++ = claim.output[i] % P;
+        *c++ = claim.input_len + 1;
+        *c++ = claim.input_len;
+        for (size_t i = 0; i < claim.input_len; ++i) *c++ = claim.input[i] % P;
+        *c++ = claim.version;
+        for (int i = 0; i < 5; ++i) *c++ = claim.program_digest[i] % P;
+    }
+    const uint64_t clen = claim.output_len + claim.input_len + 10;
     pd.claim_out_off = cbase + 2;
     pd.claim_out_n = (uint32_t)claim.output_len;
     pd.claim_in_off = cbase + 2 + claim.output_len + 2;
     pd.claim_in_n = (uint32_t)claim.input_len;
     pd.claim_digest_off = cbase + clen - 5;
 
-    const uint64_t* w = B.words.data();
+    const uint64_t* w = words;
     std::vector<Item> items;
     bool ok = len >= 2 && w[base] == len - 1;
     if (ok) {
@@ -287,14 +304,14 @@ void decode_proof(HostBatch& B, const nhip_claim& claim, const nhip_proof& proof
             pd.quot_auth_n = (uint32_t)qauth->n;
             pd.rows_n = k;
             // Fiat-Shamir program (order of Stark::verify + Fri::verify)
-            pd.fs_op_off = (uint32_t)B.ops.size();
+            std::vector<FsOp>& ops = out.ops;
             uint64_t perms = 0;
             auto absorb = [&](uint64_t off, uint64_t n) {
-                B.ops.push_back(FsOp{FS_ABSORB, (uint32_t)n, off});
+                ops.push_back(FsOp{FS_ABSORB, (uint32_t)n, off});
                 perms += absorb_perms(n);
             };
             auto squeeze = [&](uint32_t n) {
-                B.ops.push_back(FsOp{FS_SQUEEZE_X, n, 0});
+                ops.push_back(FsOp{FS_SQUEEZE_X, n, 0});
                 perms += (3ull * n + 9) / 10;
             };
             auto absorb_item = [&](const Item* it) { absorb(it->lo, it->hi - it->lo); };
@@ -315,15 +332,15 @@ void decode_proof(HostBatch& B, const nhip_claim& claim, const nhip_proof& proof
                 absorb_item(fr[r]);
                 if (r < R) squeeze(1);
             }
-            B.ops.push_back(FsOp{FS_SAMPLE_IDX, k, 1ull << log2_N});
+            ops.push_back(FsOp{FS_SAMPLE_IDX, k, 1ull << log2_N});
             perms += (k + 9) / 10;
             squeeze(1);
-            pd.fs_op_n = (uint32_t)(B.ops.size() - pd.fs_op_off);
+            pd.fs_op_n = (uint32_t)ops.size();
             // rows + last codeword tree
             perms += (uint64_t)k * (absorb_perms(d.num_main) + absorb_perms(3ull * d.num_aux) +
                                     absorb_perms(3ull * d.num_quot_seg));
-            B.perms_static += perms;
-            B.perms_lcw += cw->n - 1;  // last-codeword tree, hashed by k_mp_hash
+            out.perms = perms;
+            out.perms_lcw = cw->n - 1;  // last-codeword tree, hashed by k_mp_hash
         }
     }
     if (!ok) {
@@ -332,17 +349,60 @@ void decode_proof(HostBatch& B, const nhip_claim& claim, const nhip_proof& proof
         pd.claim_out_off = cbase + 2;
         pd.claim_in_off = cbase + 2 + claim.output_len + 2;
         pd.claim_digest_off = cbase + clen - 5;
+        out.ops.clear();
+        out.perms = out.perms_lcw = 0;
     }
-    const SampleLayout sl = SampleLayout::of(d, pd.R);
+    out.pd = pd;
+    out.fail = fail;
+}
+
+// Append one decoded proof to the batch (serial, in proof order): global Fiat-Shamir program
+// offsets, sample / index areas, batch maxima and permutation counts.
+void merge_proof(HostBatch& B, ProofOut& o, uint64_t proof_len) {
+    ProofDesc pd = o.pd;
+    pd.fs_op_off = (uint32_t)B.ops.size();
+    B.ops.insert(B.ops.end(), o.ops.begin(), o.ops.end());
+    const SampleLayout sl = SampleLayout::of(B.D.d, pd.R);
     pd.xs_off = B.xs_total;
     pd.n_xs = sl.total;
     B.xs_total += sl.total;
     pd.idx_off = B.idx_total;
-    B.idx_total += d.num_checks;
+    B.idx_total += B.D.d.num_checks;
     if (pd.R > B.max_R) B.max_R = pd.R;
     if (pd.last_cw_n > B.max_last_cw) B.max_last_cw = pd.last_cw_n;
+    B.perms_static += o.perms;
+    B.perms_lcw += o.perms_lcw;
+    B.proof_words += proof_len;
     B.desc.push_back(pd);
-    B.fail.push_back(fail);
+    B.fail.push_back(o.fail);
+}
+
+// Host threads for decoding (NHIP_HOST_THREADS overrides; at most 16, the GPU box's CPU share).
+unsigned host_threads(size_t n) {
+    unsigned t = std::thread::hardware_concurrency();
+    if (const char* e = std::getenv("NHIP_HOST_THREADS")) t = (unsigned)std::strtoul(e, nullptr, 10);
+    t = std::max(1u, std::min(t, 16u));
+    return n < 32 ? 1u : std::min<unsigned>(t, (unsigned)(n / 8));
+}
+
+// Decode proofs [0, n) into words (staged at bases[i]) on up to `threads` threads.
+void decode_all(const Dims& D, const nhip_claim* claims, const nhip_proof* proofs, size_t n, uint64_t* words,
+                const std::vector<uint64_t>& bases, std::vector<ProofOut>& outs, unsigned threads) {
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        constexpr size_t CHUNK = 4;
+        for (size_t a; (a = next.fetch_add(CHUNK)) < n;)
+            for (size_t i = a; i < std::min(n, a + CHUNK); ++i)
+                decode_proof(D, claims[i], proofs[i], words, bases[i], outs[i]);
+    };
+    if (threads <= 1) {
+        work();
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < threads; ++t) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
 }
 
 }  // namespace
@@ -391,6 +451,7 @@ struct nhip_batch {
 extern "C" hipStream_t nhip_internal_stream(nhip_ctx* c);
 extern "C" int nhip_internal_device(nhip_ctx* c);
 extern "C" std::mutex* nhip_internal_mutex(nhip_ctx* c);
+extern "C" void* nhip_internal_staging(nhip_ctx* c, size_t bytes);
 
 namespace {
 
@@ -605,10 +666,10 @@ int nhip_proof_decodes(const nhip_air* air, const nhip_stark_params* sp, const n
                        const nhip_proof* proof) {
     Dims D{};
     if (!claim || !proof || (proof->len && !proof->words) || !dims_from(sp, air, D)) return -NHIP_ERR_ARG;
-    HostBatch B;
-    B.D = D;
-    decode_proof(B, *claim, *proof);
-    return B.fail[0] ? 0 : 1;
+    std::vector<uint64_t> words(staged_words(*claim, *proof));
+    ProofOut o;
+    decode_proof(D, *claim, *proof, words.data(), 0, o);
+    return o.fail ? 0 : 1;
 }
 
 int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
@@ -627,17 +688,30 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     if (!b) return NHIP_ERR_OOM;
     b->air = air;
     b->device = nhip_internal_device(ctx);
-    auto t0 = std::chrono::steady_clock::now();
     HostBatch& H = b->H;
     H.D = D;
     H.desc.reserve(n);
     H.fail.reserve(n);
-    {
-        size_t tot = 0;
-        for (size_t i = 0; i < n; ++i) tot += proofs[i].len + claims[i].input_len + claims[i].output_len + 10;
-        H.words.reserve(tot);
+    // stage every proof (+ claim encoding) straight into the context's pinned staging buffer
+    // (pinned once per context and reused: not part of the decode time), on several host
+    // threads, then merge the descriptors in proof order
+    std::vector<uint64_t> bases(n);
+    for (size_t i = 0; i < n; ++i) {
+        bases[i] = H.words_total;
+        H.words_total += staged_words(claims[i], proofs[i]);
     }
-    for (size_t i = 0; i < n; ++i) decode_proof(H, claims[i], proofs[i]);
+    std::vector<uint64_t> pageable;
+    uint64_t* words = (uint64_t*)nhip_internal_staging(ctx, H.words_total * 8 + 8);
+    if (!words) {
+        pageable.resize(H.words_total + 1);
+        words = pageable.data();
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    {
+        std::vector<ProofOut> outs(n);
+        decode_all(D, claims, proofs, n, words, bases, outs, host_threads(n));
+        for (size_t i = 0; i < n; ++i) merge_proof(H, outs[i], proofs[i].len);
+    }
     auto t1 = std::chrono::steady_clock::now();
     b->decode_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     int rc = air_upload(ctx, air);
@@ -679,7 +753,7 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
             mp_total += mp_scap[(size_t)l * MP_SHARDS + q];
             b->mp_cap[l] += mp_scap[(size_t)l * MP_SHARDS + q];
         }
-    const size_t sz[] = {H.words.size() * 8 + 8,
+    const size_t sz[] = {H.words_total * 8 + 8,
                          std::max<size_t>(1, n) * sizeof(ProofDesc),
                          H.ops.size() * sizeof(FsOp) + 8,
                          H.xs_total * 24 + 8,
@@ -715,7 +789,7 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
         p += al(sz[i]);
     }
     hipStream_t st = nhip_internal_stream(ctx);
-    e = hipMemcpyAsync(ptr[0], H.words.data(), H.words.size() * 8, hipMemcpyHostToDevice, st);
+    e = hipMemcpyAsync(ptr[0], words, H.words_total * 8, hipMemcpyHostToDevice, st);
     if (e == hipSuccess && n) e = hipMemcpyAsync(ptr[1], H.desc.data(), n * sizeof(ProofDesc), hipMemcpyHostToDevice, st);
     if (e == hipSuccess && !H.ops.empty())
         e = hipMemcpyAsync(ptr[2], H.ops.data(), H.ops.size() * sizeof(FsOp), hipMemcpyHostToDevice, st);
