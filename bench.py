@@ -111,7 +111,8 @@ def make_config4(pool, total: int, corrupt_frac: float, world: int, rank: int):
     """BASELINE config 4: `total` transaction proofs with log2 padded heights drawn uniformly from
     the ProofCollection member mix (seed 0xC4), corrupt_frac of them with one flipped MainRows word,
     LPT-sharded over the ranks by estimated Tip5 cost (neptune_hip.shard.lpt_shard).  Returns this
-    rank's (claims, proofs, expect)."""
+    rank's (claims, proofs, expect), the shard assignment every rank agrees on, and the expected
+    verdict of every proof of the job."""
     from neptune_hip import shard
     rng = np.random.default_rng(0xC4)
     hs = rng.choice(COLLECTION_HEIGHTS, size=total)
@@ -130,7 +131,8 @@ def make_config4(pool, total: int, corrupt_frac: float, world: int, rank: int):
         claims.append(e["claim"])
         proofs.append(proof)
         expect.append(i not in bad)
-    return claims, proofs, np.array(expect, dtype=bool)
+    expect_all = np.array([i not in bad for i in range(total)], dtype=bool)
+    return claims, proofs, np.array(expect, dtype=bool), shard.lpt_shard(cost, world), expect_all
 
 
 def make_config5(air_words, total: int, log2_ph: int, world: int, rank: int):
@@ -151,7 +153,8 @@ def make_config5(air_words, total: int, log2_ph: int, world: int, rank: int):
         proof, _ = K.prove(params, air, recipe, claim, log2_ph, seed=0xC5 + i)
         claims.append(claim)
         proofs.append(np.asarray(proof, dtype=np.uint64))
-    return claims, proofs, np.ones(len(proofs), dtype=bool)
+    shards = [list(shard.contiguous_shard(total, world, r)) for r in range(world)]
+    return claims, proofs, np.ones(len(proofs), dtype=bool), shards, np.ones(total, dtype=bool)
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle)
@@ -252,15 +255,16 @@ def main():
 
     air_words, pool = load_pool()
     sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
+    shards = expect_all = None  # configs 4 / 5: per-proof verdicts are all-gathered every step
     if args.config == 3:
         claims, proofs, expect = make_batch(pool, args.collections, args.corrupt_frac, 0xC3 + rank)
         total = world * len(proofs)
     elif args.config == 4:
         total = args.proofs or 4096
-        claims, proofs, expect = make_config4(pool, total, 0.01, world, rank)
+        claims, proofs, expect, shards, expect_all = make_config4(pool, total, 0.01, world, rank)
     else:
         total = args.proofs or 64
-        claims, proofs, expect = make_config5(air_words, total, args.log2_height, world, rank)
+        claims, proofs, expect, shards, expect_all = make_config5(air_words, total, args.log2_height, world, rank)
     n = len(proofs)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -269,16 +273,22 @@ def main():
         log(f"[cpu] {cpu['value']:.1f} proofs/s ({time.time() - t:.1f}s)")
 
     dist = None
+    dev_index = local_rank
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        # NHIP_DIST_BACKEND=gloo rehearses the multi-rank logic with several ranks on one GPU
+        # (collectives on host tensors); the default is RCCL ("nccl") over xGMI
+        backend = os.environ.get("NHIP_DIST_BACKEND", "nccl")
+        if backend != "nccl":
+            dev_index = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_index)
+        dist.init_process_group(backend)
     import neptune_hip as nh
     import neptune_hip.stark as NS
     from neptune_hip import shard
 
-    ctx = nh.Context(local_rank)
+    ctx = nh.Context(dev_index)
     t0 = time.time()
     gair = NS.Air([int(w) for w in air_words])
     stark = NS.Stark.default()
@@ -304,10 +314,14 @@ def main():
             ok = ok and o
         return np.concatenate(vs), ok
 
+    gathered = [None]
+
     def step():
-        _, ok = run_all()
+        v, ok = run_all()
         if dist is not None:
-            ok = shard.all_ok(ok, dist)  # the one exchange: RCCL all-reduce(MIN) of the batch verdict
+            ok = shard.all_ok(ok, dist)  # RCCL all-reduce(MIN) of the batch verdict
+            if shards is not None:  # block validation: every rank gets every proof's verdict
+                gathered[0] = shard.gather_verdicts(v, shards, total, dist)
         return ok
 
     def barrier_sync():
@@ -333,9 +347,11 @@ def main():
 
     v, _ = run_all()
     correct = bool((np.asarray(v, dtype=bool) == expect).all())
+    if gathered[0] is not None:
+        correct = correct and bool((gathered[0].astype(bool) == expect_all).all())
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed, 0.0 if correct else 1.0], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, 0.0 if correct else 1.0], dtype=torch.float64, device=shard._device_for(dist))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, any_bad = float(t[0].item()), float(t[1].item())
         correct = any_bad == 0.0
@@ -343,7 +359,7 @@ def main():
     perms_job = perms_rank
     if dist is not None:
         import torch
-        tp = torch.tensor([perms_rank], dtype=torch.float64, device="cuda")
+        tp = torch.tensor([perms_rank], dtype=torch.float64, device=shard._device_for(dist))
         dist.all_reduce(tp, op=dist.ReduceOp.SUM)
         perms_job = float(tp[0].item())
     if not correct:
