@@ -21,6 +21,8 @@ struct nhip_ctx {
     size_t ws_bytes = 0;
     void* staging = nullptr;  // pinned host staging for batch uploads (grow-only, under mu)
     size_t staging_bytes = 0;
+    void* verify_scratch = nullptr;  // reusable device / stream resources of nhip_verify_batch
+    void (*verify_scratch_free)(void*) = nullptr;
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;  // recorded, not yet read
     std::vector<hipEvent_t> free_events;
@@ -176,6 +178,7 @@ void nhip_destroy(nhip_ctx* c) {
     for (auto e : c->free_events) (void)hipEventDestroy(e);
     if (c->ws) (void)hipFree(c->ws);
     if (c->staging) (void)hipHostFree(c->staging);
+    if (c->verify_scratch && c->verify_scratch_free) c->verify_scratch_free(c->verify_scratch);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -186,6 +189,16 @@ int nhip_device_ordinal(const nhip_ctx* c) { return c ? c->device : -1; }
 hipStream_t nhip_internal_stream(nhip_ctx* c) { return c->stream; }
 int nhip_internal_device(nhip_ctx* c) { return c->device; }
 std::mutex* nhip_internal_mutex(nhip_ctx* c) { return &c->mu; }
+// The context's nhip_verify_batch scratch (created by `make` on first use, freed by `freefn` in
+// nhip_destroy).
+void* nhip_internal_verify_scratch(nhip_ctx* c, void* (*make)(), void (*freefn)(void*)) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->verify_scratch) {
+        c->verify_scratch = make();
+        c->verify_scratch_free = freefn;
+    }
+    return c->verify_scratch;
+}
 // Pinned staging of at least `bytes` (caller holds c->mu); nullptr if it cannot be pinned.
 void* nhip_internal_staging(nhip_ctx* c, size_t bytes) {
     if (bytes <= c->staging_bytes) return c->staging;

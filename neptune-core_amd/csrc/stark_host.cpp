@@ -425,8 +425,38 @@ struct nhip_air {
     Xfe* d_consts = nullptr;
 };
 
+// Device memory, streams, events and pinned readback of nhip_verify_batch, kept in the context
+// and reused call after call: a one-proof call is otherwise dominated by hipMalloc / stream /
+// event / pinned-buffer setup and teardown (~10 ms against ~2 ms of device work).  `mu` holds
+// the scratch for a whole call, so concurrent callers are serialized.
+struct VerifyScratch {
+    std::mutex mu;
+    void* dmem = nullptr;
+    size_t dmem_bytes = 0;
+    hipStream_t main = nullptr, aux = nullptr;
+    hipEvent_t ev[STARK_EVENTS] = {};
+    bool streams = false;
+    uint8_t* h_out = nullptr;
+    size_t h_out_bytes = 0;
+};
+
+static void free_verify_scratch(void* p) {
+    auto* sc = (VerifyScratch*)p;
+    if (sc->streams) {
+        (void)hipStreamSynchronize(sc->main);
+        (void)hipStreamSynchronize(sc->aux);
+        for (int i = 0; i < STARK_EVENTS; ++i) (void)hipEventDestroy(sc->ev[i]);
+        (void)hipStreamDestroy(sc->main);
+        (void)hipStreamDestroy(sc->aux);
+    }
+    if (sc->h_out) (void)hipHostFree(sc->h_out);
+    if (sc->dmem) (void)hipFree(sc->dmem);
+    delete sc;
+}
+
 struct nhip_batch {
     HostBatch H;
+    VerifyScratch* scratch = nullptr;  // borrowed resources (nhip_verify_batch), not owned
     const nhip_air* air = nullptr;
     int device = 0;
     // device buffers
@@ -452,6 +482,7 @@ extern "C" hipStream_t nhip_internal_stream(nhip_ctx* c);
 extern "C" int nhip_internal_device(nhip_ctx* c);
 extern "C" std::mutex* nhip_internal_mutex(nhip_ctx* c);
 extern "C" void* nhip_internal_staging(nhip_ctx* c, size_t bytes);
+extern "C" void* nhip_internal_verify_scratch(nhip_ctx* c, void* (*make)(), void (*freefn)(void*));
 
 namespace {
 
@@ -672,8 +703,9 @@ int nhip_proof_decodes(const nhip_air* air, const nhip_stark_params* sp, const n
     return o.fail ? 0 : 1;
 }
 
-int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
-                       const nhip_proof* proofs, size_t n, nhip_batch** out) {
+namespace {
+int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
+                  const nhip_proof* proofs, size_t n, nhip_batch** out, VerifyScratch* scr) {
     if (!ctx || !out || (n && (!claims || !proofs))) return NHIP_ERR_ARG;
     *out = nullptr;
     Dims D{};
@@ -688,6 +720,7 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     if (!b) return NHIP_ERR_OOM;
     b->air = air;
     b->device = nhip_internal_device(ctx);
+    b->scratch = scr;
     HostBatch& H = b->H;
     H.D = D;
     H.desc.reserve(n);
@@ -777,8 +810,21 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     constexpr int NBUF = sizeof(sz) / sizeof(sz[0]);
     size_t total = 0;
     for (size_t s : sz) total += al(s);
-    hipError_t e = hipMalloc(&b->dmem, total);
+    hipError_t e = hipSuccess;
+    if (scr) {  // grow-only device scratch of the context
+        if (scr->dmem_bytes < total) {
+            if (scr->dmem) (void)hipFree(scr->dmem);
+            scr->dmem = nullptr;
+            scr->dmem_bytes = 0;
+            e = hipMalloc(&scr->dmem, total + total / 4);
+            if (e == hipSuccess) scr->dmem_bytes = total + total / 4;
+        }
+        b->dmem = scr->dmem;
+    } else {
+        e = hipMalloc(&b->dmem, total);
+    }
     if (e != hipSuccess) {
+        if (scr) b->dmem = nullptr;
         delete b;
         return hipfail(e);
     }
@@ -802,7 +848,7 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     auto t2 = std::chrono::steady_clock::now();
     b->upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
     if (e != hipSuccess) {
-        (void)hipFree(b->dmem);
+        if (!scr) (void)hipFree(b->dmem);
         delete b;
         return hipfail(e);
     }
@@ -843,12 +889,18 @@ int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp
     dv.air_cons_off = air->cons_off;
     dv.air_lds_bytes = AIR_LDS_HEADER + (size_t)air->slots * 24;
     if (dv.air_lds_bytes > 160 * 1024 - 8192) {
-        (void)hipFree(b->dmem);
+        if (!scr) (void)hipFree(b->dmem);
         delete b;
         return NHIP_ERR_ARG;  // AIR too large for the single-workgroup LDS evaluator
     }
     *out = b;
     return NHIP_OK;
+}
+}  // namespace
+
+int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
+                       const nhip_proof* proofs, size_t n, nhip_batch** out) {
+    return batch_prepare(ctx, air, sp, claims, proofs, n, out, nullptr);
 }
 
 // Enqueue every device phase of the batch on the batch's own two streams (no host wait).  Batches
@@ -859,15 +911,36 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
     (void)hipSetDevice(b->device);
     if (b->in_flight) return NHIP_ERR_ARG;
     if (!b->timed) {
-        for (int i = 0; i < STARK_EVENTS; ++i)
-            if (hipEventCreate(&b->tm.ev[i]) != hipSuccess) return NHIP_ERR_HIP;
         const char* al = std::getenv("NHIP_AUX_AFTER_LEVEL");
         b->tm.aux_after_level = al ? (uint32_t)std::strtoul(al, nullptr, 10) : AUX_AFTER_LEVEL_DEFAULT;
-        if (hipStreamCreateWithFlags(&b->main, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
-        if (hipStreamCreateWithFlags(&b->aux, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
-        if (hipHostMalloc((void**)&b->h_out, OUT_HDR + (size_t)b->dev.mp.levels * MP_SHARDS * 4 + b->dev.n_proofs + 16,
-                          hipHostMallocDefault) != hipSuccess)
-            return NHIP_ERR_OOM;
+        const size_t out_bytes = OUT_HDR + (size_t)b->dev.mp.levels * MP_SHARDS * 4 + b->dev.n_proofs + 16;
+        if (VerifyScratch* sc = b->scratch) {
+            if (!sc->streams) {
+                for (int i = 0; i < STARK_EVENTS; ++i)
+                    if (hipEventCreate(&sc->ev[i]) != hipSuccess) return NHIP_ERR_HIP;
+                if (hipStreamCreateWithFlags(&sc->main, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
+                if (hipStreamCreateWithFlags(&sc->aux, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
+                sc->streams = true;
+            }
+            if (sc->h_out_bytes < out_bytes) {
+                if (sc->h_out) (void)hipHostFree(sc->h_out);
+                sc->h_out = nullptr;
+                sc->h_out_bytes = 0;
+                if (hipHostMalloc((void**)&sc->h_out, out_bytes * 2, hipHostMallocDefault) != hipSuccess)
+                    return NHIP_ERR_OOM;
+                sc->h_out_bytes = out_bytes * 2;
+            }
+            for (int i = 0; i < STARK_EVENTS; ++i) b->tm.ev[i] = sc->ev[i];
+            b->main = sc->main;
+            b->aux = sc->aux;
+            b->h_out = sc->h_out;
+        } else {
+            for (int i = 0; i < STARK_EVENTS; ++i)
+                if (hipEventCreate(&b->tm.ev[i]) != hipSuccess) return NHIP_ERR_HIP;
+            if (hipStreamCreateWithFlags(&b->main, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
+            if (hipStreamCreateWithFlags(&b->aux, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
+            if (hipHostMalloc((void**)&b->h_out, out_bytes, hipHostMallocDefault) != hipSuccess) return NHIP_ERR_OOM;
+        }
         b->timed = true;
     }
     hipStream_t st = b->main;
@@ -997,9 +1070,13 @@ int nhip_batch_transcript(nhip_ctx* ctx, const nhip_batch* b, size_t proof, uint
 void nhip_batch_destroy(nhip_batch* b) {
     if (!b) return;
     (void)hipSetDevice(b->device);
+    if (b->in_flight && b->main) (void)hipStreamSynchronize(b->main);
+    if (b->scratch) {  // resources belong to the context's verify scratch
+        delete b;
+        return;
+    }
     if (b->timed)
         for (int i = 0; i < STARK_EVENTS; ++i) (void)hipEventDestroy(b->tm.ev[i]);
-    if (b->in_flight && b->main) (void)hipStreamSynchronize(b->main);
     if (b->main) (void)hipStreamDestroy(b->main);
     if (b->aux) (void)hipStreamDestroy(b->aux);
     if (b->h_out) (void)hipHostFree(b->h_out);
@@ -1010,8 +1087,13 @@ void nhip_batch_destroy(nhip_batch* b) {
 int nhip_verify_batch(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
                       const nhip_proof* proofs, size_t n, uint8_t* verdicts, nhip_stats* stats) {
     if (!verdicts && n) return NHIP_ERR_ARG;
+    if (!ctx) return NHIP_ERR_ARG;
+    auto* scr = (VerifyScratch*)nhip_internal_verify_scratch(
+        ctx, []() -> void* { return new (std::nothrow) VerifyScratch(); }, &free_verify_scratch);
+    if (!scr) return NHIP_ERR_OOM;
+    std::lock_guard<std::mutex> g(scr->mu);
     nhip_batch* b = nullptr;
-    int rc = nhip_batch_prepare(ctx, air, sp, claims, proofs, n, &b);
+    int rc = batch_prepare(ctx, air, sp, claims, proofs, n, &b, scr);
     if (rc) return rc;
     rc = nhip_batch_run(ctx, b, verdicts, nullptr);
     if (!rc && stats) nhip_batch_stats(b, stats);

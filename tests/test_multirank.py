@@ -93,14 +93,15 @@ def _stark_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     air, pool = bench.load_pool()
     total = 48
-    claims, proofs, expect = bench.make_config4(pool, total, 0.1, world, rank)
+    claims, proofs, expect, shards, expect_all = bench.make_config4(pool, total, 0.1, world, rank)
     v = C.stark_verify_batch(air, S.StarkParams(), claims, proofs, threads=2)
     rng = np.random.default_rng(0xC4)
     hs = rng.choice(bench.COLLECTION_HEIGHTS, size=total)
-    shards = shard.lpt_shard([10_000 + 600 * int(h) for h in hs], world)
+    assert shards == shard.lpt_shard([10_000 + 600 * int(h) for h in hs], world)
     ok = shard.all_ok(bool(v.all()), dist)
     full = shard.gather_verdicts(v, shards, total, dist)
-    q.put((rank, ok, full.tolist(), [bool(x) == bool(e) for x, e in zip(v, expect)], [len(s) for s in shards]))
+    q.put((rank, ok, full.tolist(), [bool(x) == bool(e) for x, e in zip(v, expect)], [len(s) for s in shards],
+           full.astype(bool).tolist() == expect_all.tolist()))
     dist.destroy_process_group()
 
 
@@ -119,5 +120,5 @@ def test_two_rank_config4_stark_sharding():
         p.join(timeout=60)
     fulls = [r[2] for r in res]
     assert fulls[0] == fulls[1] and sum(fulls[0]) == 48 - 5
-    for rank, ok, full, matches, sizes in res:
-        assert ok is False and all(matches) and sum(sizes) == 48
+    for rank, ok, full, matches, sizes, gathered_ok in res:
+        assert ok is False and all(matches) and sum(sizes) == 48 and gathered_ok
