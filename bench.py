@@ -70,6 +70,30 @@ def pmc_traffic(kernel: str):
         return None, None
 
 
+def pmc_valu_per_step():
+    """Wave-level VALU instructions one config-3 step issues, from the latest committed PMC pass
+    (profiles/<LATEST>/pmc_valu_counter_collection.csv: SQ_INSTS_VALU summed over a step's
+    dispatches, microbench kernels excluded; steps = k_hash_rows dispatches); None when absent."""
+    import csv
+    try:
+        tag = open(os.path.join(ROOT, "profiles", "LATEST")).read().strip()
+        tot, steps = 0.0, 0
+        for r in csv.DictReader(open(os.path.join(ROOT, "profiles", tag, "pmc_valu_counter_collection.csv"))):
+            k = r["Kernel_Name"]
+            if r["Counter_Name"] != "SQ_INSTS_VALU" or "mtree" in k or "rocclr" in k:
+                continue
+            tot += float(r["Counter_Value"])
+            steps += "k_hash_rows" in k
+        return (tot / steps, tag) if steps else (None, None)
+    except (OSError, KeyError):
+        return None, None
+
+
+# measured gfx950 issue ceiling for this instruction mix: ~1 wave64 VALU instruction per 4 clocks
+# per SIMD (DESIGN.md §3, tools/valu_microbench.hip)
+VALU_ISSUE_CEILING = 256 * 4 * 2.4e9 / 4
+
+
 # ------------------------------------------------------------------ config 3 batch
 def load_pool():
     z = np.load(POOL)  # plain arrays, allow_pickle=False
@@ -425,6 +449,13 @@ def main():
                      "perms_per_launch": perms_per_launch,
                      "valu_ops_per_perm": TIP5_VALU_OPS_PER_PERM},
     }
+    valu_step, valu_tag = pmc_valu_per_step()
+    if args.config == 3 and valu_step:
+        # the whole pipeline against the measured VALU issue ceiling: committed PMC instruction
+        # count of one step (per GPU) / this run's step time
+        res["valu_issue"] = {"wave_instr_per_step": valu_step, "profile": valu_tag,
+                             "ceiling_wave_instr_per_s": VALU_ISSUE_CEILING,
+                             "frac": valu_step / (elapsed / K) / VALU_ISSUE_CEILING}
     if rank == 0 and args.paths_log2 > 0:
         res["tip5_paths"] = tip5_paths(ctx, args.paths_log2, 5)
     if cpu is not None:
