@@ -161,6 +161,12 @@ int nhip_verify_batch(nhip_ctx *ctx, nhip_air *air, const nhip_stark_params *par
  * of times, read stats / the Fiat-Shamir transcript of one proof, destroy. */
 int nhip_batch_prepare(nhip_ctx *ctx, nhip_air *air, const nhip_stark_params *params, const nhip_claim *claims,
                        const nhip_proof *proofs, size_t n, nhip_batch **out);
+/* Refill an idle batch in place with new proofs (same semantics as prepare; its streams,
+ * events and device memory are reused when large enough).  Streaming from host memory:
+ * launch(A); refill(B, next); wait(A); launch(B); refill(A, next); ... overlaps each host decode
+ * + upload with the other batch's device run.  On failure the batch is left empty (n = 0). */
+int nhip_batch_refill(nhip_ctx *ctx, nhip_batch *batch, nhip_air *air, const nhip_stark_params *params,
+                      const nhip_claim *claims, const nhip_proof *proofs, size_t n);
 int nhip_batch_run(nhip_ctx *ctx, nhip_batch *batch, uint8_t *verdicts, uint8_t *all_ok);
 /* Asynchronous form of nhip_batch_run: launch enqueues every phase on the batch's own streams and
  * returns; wait blocks until that batch is done.  Batches launched back to back run concurrently

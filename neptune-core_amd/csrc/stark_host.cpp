@@ -468,6 +468,7 @@ struct nhip_batch {
     hipStream_t main = nullptr;  // hashing chain (rows -> Merkle levels -> roots -> verdicts)
     hipStream_t aux = nullptr;   // latency-bound chain (Fiat-Shamir -> plan -> OOD -> FRI -> DEEP)
     uint8_t* h_out = nullptr;    // pinned: [perm counter (8 B) | verdicts (n B)]
+    size_t dmem_bytes = 0, h_out_bytes = 0;  // owned allocations (refill reuses them when they fit)
     bool timed = false, in_flight = false;
     struct {
         double fs, rows, plan, hash, roots, ood, fri, deep, total;
@@ -704,10 +705,14 @@ int nhip_proof_decodes(const nhip_air* air, const nhip_stark_params* sp, const n
 }
 
 namespace {
+// Decode + upload a batch.  reuse == nullptr: a new batch (*out); otherwise `reuse` is refilled
+// in place (same streams and events; its device memory reused when large enough).
 int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
-                  const nhip_proof* proofs, size_t n, nhip_batch** out, VerifyScratch* scr) {
+                  const nhip_proof* proofs, size_t n, nhip_batch** out, VerifyScratch* scr,
+                  nhip_batch* reuse = nullptr) {
     if (!ctx || !out || (n && (!claims || !proofs))) return NHIP_ERR_ARG;
-    *out = nullptr;
+    if (reuse && (reuse->in_flight || reuse->scratch)) return NHIP_ERR_ARG;
+    if (!reuse) *out = nullptr;
     Dims D{};
     if (!dims_from(sp, air, D)) return NHIP_ERR_ARG;
     for (size_t i = 0; i < n; ++i)
@@ -716,11 +721,23 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
             return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
     (void)hipSetDevice(nhip_internal_device(ctx));
-    nhip_batch* b = new (std::nothrow) nhip_batch();
+    nhip_batch* b = reuse ? reuse : new (std::nothrow) nhip_batch();
     if (!b) return NHIP_ERR_OOM;
+    // on failure: a new batch is deleted; a refilled one is left empty (n = 0) but usable
+    auto fail_out = [&](int rc) {
+        if (!reuse) {
+            if (!scr && b->dmem) (void)hipFree(b->dmem);
+            delete b;
+        } else {
+            b->H = HostBatch{};
+            b->dev.n_proofs = 0;
+        }
+        return rc;
+    };
     b->air = air;
     b->device = nhip_internal_device(ctx);
     b->scratch = scr;
+    b->H = HostBatch{};
     HostBatch& H = b->H;
     H.D = D;
     H.desc.reserve(n);
@@ -748,16 +765,10 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     auto t1 = std::chrono::steady_clock::now();
     b->decode_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     int rc = air_upload(ctx, air);
-    if (rc) {
-        delete b;
-        return rc;
-    }
+    if (rc) return fail_out(rc);
     static bool attrs = false;
     if (!attrs) {
-        if (stark_set_kernel_attributes() != hipSuccess) {
-            delete b;
-            return NHIP_ERR_HIP;
-        }
+        if (stark_set_kernel_attributes() != hipSuccess) return fail_out(NHIP_ERR_HIP);
         attrs = true;
     }
     const uint32_t k = D.d.num_checks;
@@ -820,13 +831,17 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
             if (e == hipSuccess) scr->dmem_bytes = total + total / 4;
         }
         b->dmem = scr->dmem;
-    } else {
-        e = hipMalloc(&b->dmem, total);
+    } else if (b->dmem_bytes < total) {  // new batch, or a refill that no longer fits
+        if (b->dmem) (void)hipFree(b->dmem);
+        b->dmem = nullptr;
+        b->dmem_bytes = 0;
+        const size_t want = reuse ? total + total / 4 : total;
+        e = hipMalloc(&b->dmem, want);
+        if (e == hipSuccess) b->dmem_bytes = want;
     }
     if (e != hipSuccess) {
         if (scr) b->dmem = nullptr;
-        delete b;
-        return hipfail(e);
+        return fail_out(hipfail(e));
     }
     char* p = (char*)b->dmem;
     void* ptr[NBUF];
@@ -847,11 +862,7 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     auto t2 = std::chrono::steady_clock::now();
     b->upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
-    if (e != hipSuccess) {
-        if (!scr) (void)hipFree(b->dmem);
-        delete b;
-        return hipfail(e);
-    }
+    if (e != hipSuccess) return fail_out(hipfail(e));
     StarkBatchDev& dv = b->dev;
     dv.n_proofs = (uint32_t)n;
     dv.max_R = H.max_R;
@@ -888,11 +899,8 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     dv.air_consts = air->d_consts;
     dv.air_cons_off = air->cons_off;
     dv.air_lds_bytes = AIR_LDS_HEADER + (size_t)air->slots * 24;
-    if (dv.air_lds_bytes > 160 * 1024 - 8192) {
-        if (!scr) (void)hipFree(b->dmem);
-        delete b;
-        return NHIP_ERR_ARG;  // AIR too large for the single-workgroup LDS evaluator
-    }
+    if (dv.air_lds_bytes > 160 * 1024 - 8192)
+        return fail_out(NHIP_ERR_ARG);  // AIR too large for the single-workgroup LDS evaluator
     *out = b;
     return NHIP_OK;
 }
@@ -901,6 +909,13 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
 int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
                        const nhip_proof* proofs, size_t n, nhip_batch** out) {
     return batch_prepare(ctx, air, sp, claims, proofs, n, out, nullptr);
+}
+
+int nhip_batch_refill(nhip_ctx* ctx, nhip_batch* b, nhip_air* air, const nhip_stark_params* sp,
+                      const nhip_claim* claims, const nhip_proof* proofs, size_t n) {
+    if (!b) return NHIP_ERR_ARG;
+    nhip_batch* out = b;
+    return batch_prepare(ctx, air, sp, claims, proofs, n, &out, nullptr, b);
 }
 
 // Enqueue every device phase of the batch on the batch's own two streams (no host wait).  Batches
@@ -939,9 +954,18 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
                 if (hipEventCreate(&b->tm.ev[i]) != hipSuccess) return NHIP_ERR_HIP;
             if (hipStreamCreateWithFlags(&b->main, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
             if (hipStreamCreateWithFlags(&b->aux, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
-            if (hipHostMalloc((void**)&b->h_out, out_bytes, hipHostMallocDefault) != hipSuccess) return NHIP_ERR_OOM;
         }
         b->timed = true;
+    }
+    if (!b->scratch) {  // pinned readback, grown when a refill needs more
+        const size_t out_bytes = OUT_HDR + (size_t)b->dev.mp.levels * MP_SHARDS * 4 + b->dev.n_proofs + 16;
+        if (b->h_out_bytes < out_bytes) {
+            if (b->h_out) (void)hipHostFree(b->h_out);
+            b->h_out = nullptr;
+            b->h_out_bytes = 0;
+            if (hipHostMalloc((void**)&b->h_out, out_bytes, hipHostMallocDefault) != hipSuccess) return NHIP_ERR_OOM;
+            b->h_out_bytes = out_bytes;
+        }
     }
     hipStream_t st = b->main;
     const uint32_t n = b->dev.n_proofs;

@@ -110,6 +110,8 @@ SIGNATURES = {
                            _sz, _u8p, ctypes.POINTER(Stats)], ctypes.c_int),
     "nhip_batch_prepare": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof),
                             _sz, _pp], ctypes.c_int),
+    "nhip_batch_refill": ([_vp, _vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim),
+                           ctypes.POINTER(Proof), _sz], ctypes.c_int),
     "nhip_batch_run": ([_vp, _vp, _u8p, ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
     "nhip_batch_launch": ([_vp, _vp], ctypes.c_int),
     "nhip_batch_wait": ([_vp, _vp, _u8p, ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),

@@ -112,6 +112,15 @@ class Batch:
                                          ctypes.byref(h)), "nhip_batch_prepare")
         self.handle = h.value
 
+    def refill(self, claims: Sequence[Claim], proofs: Sequence[Sequence[int]]) -> None:
+        """Replace the batch's proofs in place (`nhip_batch_refill`; the batch must be idle)."""
+        m = _Marshal(claims, proofs)
+        params = self.stark.c()
+        self.n = 0
+        check(self.ctx.lib.nhip_batch_refill(self.ctx.handle, self.handle, self.air.handle, ctypes.byref(params),
+                                             m.claims, m.proofs, m.n), "nhip_batch_refill")
+        self.n = m.n
+
     def run(self) -> Tuple[np.ndarray, bool]:
         v = np.zeros(max(self.n, 1), dtype=np.uint8)
         ok = ctypes.c_uint8(0)

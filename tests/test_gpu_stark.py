@@ -339,3 +339,35 @@ def test_config1_singleproof_gpu(ctx):
     xs, idx, fail = b.transcript(0)
     assert ok_o and fail == 0 and xs == samples and idx == indices
     b.close()
+
+
+def test_batch_refill_and_streaming(ctx):
+    """nhip_batch_refill: an idle batch refilled in place with other proofs (smaller, then larger
+    than its device allocation) gives the expected verdicts each time; two batches alternating
+    launch / refill / wait (the streaming pattern) too."""
+    import bench
+    NS = _ns()
+    air_words, pool = bench.load_pool()
+    gair = NS.Air([int(w) for w in air_words])
+    sets = [bench.make_batch(pool, c, 0.25, 100 + c) for c in (2, 1, 6, 3, 4)]
+    mk = lambda s: ([NS.Claim(*c) for c in s[0]], s[1])  # noqa: E731
+    b = NS.Batch(ctx, gair, NS.Stark.default(), *mk(sets[0]))
+    for s in sets:
+        b.refill(*mk(s))
+        v, ok = b.run()
+        assert [bool(x) for x in v] == list(s[2]) and ok == bool(s[2].all())
+    a2 = NS.Batch(ctx, gair, NS.Stark.default(), *mk(sets[1]))
+    got = []
+    b.refill(*mk(sets[0]))
+    cur, nxt = b, a2
+    cur.launch()
+    for s in sets[1:]:
+        nxt.refill(*mk(s))
+        got.append(cur.wait()[0])
+        nxt.launch()
+        cur, nxt = nxt, cur
+    got.append(cur.wait()[0])
+    for v, s in zip(got, sets):
+        assert [bool(x) for x in v] == list(s[2])
+    b.close()
+    a2.close()
