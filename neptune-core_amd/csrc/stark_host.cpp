@@ -17,6 +17,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -400,7 +401,11 @@ void decode_all(const Dims& D, const nhip_claim* claims, const nhip_proof* proof
         return;
     }
     std::vector<std::thread> pool;
-    for (unsigned t = 1; t < threads; ++t) pool.emplace_back(work);
+    try {
+        for (unsigned t = 1; t < threads; ++t) pool.emplace_back(work);
+    } catch (const std::system_error&) {
+        // fewer threads than asked: the ones running (and this one) take the remaining proofs
+    }
     work();
     for (auto& th : pool) th.join();
 }
@@ -906,16 +911,27 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
 }
 }  // namespace
 
+// host allocations failing inside an entry point become an error code, never an exception
+// crossing the C ABI
+#define NHIP_GUARD(expr)                                    \
+    try {                                                   \
+        return (expr);                                      \
+    } catch (const std::bad_alloc&) {                       \
+        return NHIP_ERR_OOM;                                \
+    } catch (...) {                                         \
+        return NHIP_ERR_HIP;                                \
+    }
+
 int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
                        const nhip_proof* proofs, size_t n, nhip_batch** out) {
-    return batch_prepare(ctx, air, sp, claims, proofs, n, out, nullptr);
+    NHIP_GUARD(batch_prepare(ctx, air, sp, claims, proofs, n, out, nullptr))
 }
 
 int nhip_batch_refill(nhip_ctx* ctx, nhip_batch* b, nhip_air* air, const nhip_stark_params* sp,
                       const nhip_claim* claims, const nhip_proof* proofs, size_t n) {
     if (!b) return NHIP_ERR_ARG;
     nhip_batch* out = b;
-    return batch_prepare(ctx, air, sp, claims, proofs, n, &out, nullptr, b);
+    NHIP_GUARD(batch_prepare(ctx, air, sp, claims, proofs, n, &out, nullptr, b))
 }
 
 // Enqueue every device phase of the batch on the batch's own two streams (no host wait).  Batches
@@ -1117,7 +1133,12 @@ int nhip_verify_batch(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp,
     if (!scr) return NHIP_ERR_OOM;
     std::lock_guard<std::mutex> g(scr->mu);
     nhip_batch* b = nullptr;
-    int rc = batch_prepare(ctx, air, sp, claims, proofs, n, &b, scr);
+    int rc;
+    try {
+        rc = batch_prepare(ctx, air, sp, claims, proofs, n, &b, scr);
+    } catch (const std::bad_alloc&) {
+        return NHIP_ERR_OOM;
+    }
     if (rc) return rc;
     rc = nhip_batch_run(ctx, b, verdicts, nullptr);
     if (!rc && stats) nhip_batch_stats(b, stats);
