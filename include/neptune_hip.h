@@ -48,7 +48,8 @@ enum {
     NHIP_ERR_NO_DEVICE = 1,
     NHIP_ERR_HIP = 2,
     NHIP_ERR_OOM = 3,
-    NHIP_ERR_ARG = 4
+    NHIP_ERR_ARG = 4,
+    NHIP_ERR_DECODE = 5  /* malformed bincode input (block files, peer transactions) */
 };
 
 /* ---- context --------------------------------------------------------------------------- */
@@ -190,6 +191,65 @@ int nhip_proof_from_be_bytes(const uint8_t *bytes, size_t n_bytes, uint64_t *wor
 int nhip_proof_to_be_bytes(const uint64_t *words, size_t n, uint8_t *out);
 /* Tip5::hash(claim) = hash_varlen(claim.encode()) (program.rs:355-358, proof file name). */
 int nhip_claim_hash(nhip_ctx *ctx, const nhip_claim *claim, uint64_t digest_out[5]);
+
+/* ---- block files and peer transactions ----------------------------
+ * bincode 1.x as neptune-core writes them; host-only, no GPU.  Field lists, BFieldCodec rules and
+ * their pin status: neptune-core_amd/csrc/bincode.cpp and DESIGN.md §8f.
+ *
+ * Block files replace `blocks_from_file_without_record`
+ * (state/archival_state/import_blocks_from_files.rs:100-115): blocks back to back, each
+ * `bincode::deserialize::<Block>` then advance by its serialized size; a malformed block fails the
+ * whole file (NHIP_ERR_DECODE; *n_blocks = the blocks before it).  pow_tree_height is BlockPow's
+ * MERKLE_TREE_HEIGHT (pow.rs:33-37: 29, 10 in the reference's test builds). */
+enum { NHIP_BLOCK_PROOF_GENESIS = 0, NHIP_BLOCK_PROOF_INVALID = 1, NHIP_BLOCK_PROOF_SINGLE = 2 };
+typedef struct {
+    uint64_t offset, size;          /* the block's bytes in the buffer */
+    uint64_t height, timestamp;     /* BlockHeader::height, ::timestamp (canonical) */
+    uint64_t prev_block_digest[5];
+    uint32_t proof_kind;            /* BlockProof variant (block/mod.rs:114-119) */
+    uint32_t n_claims;              /* BlockAppendix claims */
+    uint64_t proof_offset;          /* SingleProof: byte offset of Proof.0's first word */
+    uint64_t proof_len;             /* SingleProof: words */
+    uint64_t kernel_offset;         /* byte offset of body.transaction_kernel */
+    uint64_t appendix_offset;       /* byte offset of the appendix claims */
+    uint64_t claim_words;           /* input + output words of all appendix claims */
+    uint64_t seq_words;             /* words of nhip_blk_sequences' output (0 on a count-only scan) */
+} nhip_blk_block;
+/* blocks == NULL: count only.  Otherwise cap >= the block count. */
+int nhip_blk_scan(const uint8_t *bytes, size_t n_bytes, uint32_t pow_tree_height, nhip_blk_block *blocks,
+                  size_t cap, size_t *n_blocks);
+/* BFieldCodec MAST sequences: the transaction kernel's 8 (transaction_kernel.rs:246-277), then the
+ * body's sequences 2-4 (block_body.rs:175-182: mutator set accumulator, lock-free MMR, block MMR;
+ * sequence 1 is the kernel's MAST hash).  Sequence i = words[offsets[i] .. offsets[i+1]);
+ * words == NULL: offsets only (offsets[11] = total words). */
+int nhip_blk_sequences(const uint8_t *bytes, size_t n_bytes, uint32_t pow_tree_height, const nhip_blk_block *block,
+                       uint64_t *words, size_t cap, uint64_t offsets[12]);
+/* The appendix claims: claims[n_claims] whose input / output point into words[claim_words]. */
+int nhip_blk_claims(const uint8_t *bytes, size_t n_bytes, const nhip_blk_block *block, uint64_t *words,
+                    nhip_claim *claims);
+/* n little-endian u64 words at byte `offset` (any alignment), reduced mod p: proof words straight
+ * into a (pinned) staging buffer. */
+int nhip_le_words(const uint8_t *bytes, size_t n_bytes, uint64_t offset, size_t n, uint64_t *out);
+
+/* Peer transactions: `TransferTransaction { kernel, proof }` (protocol/peer/transfer_transaction.rs:31-47). */
+enum { NHIP_TX_PROOF_COLLECTION = 0, NHIP_TX_SINGLE_PROOF = 1 };
+typedef struct {
+    uint64_t size;                  /* bytes consumed */
+    uint32_t kind;                  /* TransferTransactionProof variant */
+    uint32_t n_proofs;              /* 1, or ProofCollection::num_proofs() */
+    uint32_t n_lock_scripts, n_type_scripts;    /* lock_scripts_halt / type_scripts_halt lengths */
+    uint32_t n_lock_hashes, n_type_hashes, n_merge_path;
+    uint32_t n_digests;             /* n_lock_hashes + n_type_hashes + 3 + n_merge_path (ProofCollection) */
+    uint64_t seq_words;             /* words of the kernel's 8 MAST sequences */
+} nhip_tx;
+int nhip_tx_scan(const uint8_t *bytes, size_t n_bytes, nhip_tx *tx);
+/* seq_words[tx->seq_words] + seq_offsets[9]: the kernel's MAST sequences; proof_spans[2 * n_proofs]:
+ * (byte offset, word count) per proof in ProofCollection field order (removal_records_integrity,
+ * collect_lock_scripts, lock_scripts_halt.., kernel_to_outputs, collect_type_scripts,
+ * type_scripts_halt..; proof_collection.rs:36-49); digests[5 * n_digests]: lock_script_hashes,
+ * type_script_hashes, kernel_mast_hash, salted_inputs_hash, salted_outputs_hash, merge_bit_mast_path. */
+int nhip_tx_parts(const uint8_t *bytes, size_t n_bytes, const nhip_tx *tx, uint64_t *seq_words,
+                  uint64_t seq_offsets[9], uint64_t *proof_spans, uint64_t *digests);
 
 /* ---- proof of work (neptune-core/src/protocol/consensus/block/pow.rs) ---
  * PowMastPaths (pow.rs:202-207): MAST authentication paths of the pow field (BlockHeader, 3),

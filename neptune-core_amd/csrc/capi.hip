@@ -142,6 +142,7 @@ const char* nhip_strerror(int code) {
         case NHIP_ERR_HIP: return "HIP runtime error";
         case NHIP_ERR_OOM: return "out of device memory";
         case NHIP_ERR_ARG: return "invalid argument";
+        case NHIP_ERR_DECODE: return "malformed encoding";
         default: return "unknown error";
     }
 }

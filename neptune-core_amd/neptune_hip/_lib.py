@@ -16,8 +16,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NHIP_LIB") or os.path.join(_HERE, "libneptune_hip.so")
 
 NHIP_OK = 0
-NHIP_OK, NHIP_ERR_NO_DEVICE, NHIP_ERR_HIP, NHIP_ERR_OOM, NHIP_ERR_ARG = range(5)
-_ERRORS = {1: "no HIP device", 2: "HIP runtime error", 3: "out of device memory", 4: "invalid argument"}
+NHIP_OK, NHIP_ERR_NO_DEVICE, NHIP_ERR_HIP, NHIP_ERR_OOM, NHIP_ERR_ARG, NHIP_ERR_DECODE = range(6)
+_ERRORS = {1: "no HIP device", 2: "HIP runtime error", 3: "out of device memory", 4: "invalid argument",
+           5: "malformed encoding"}
 
 _u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
 _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
@@ -53,6 +54,22 @@ class Stats(ctypes.Structure):
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class BlkBlock(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint64), ("size", ctypes.c_uint64), ("height", ctypes.c_uint64),
+                ("timestamp", ctypes.c_uint64), ("prev_block_digest", ctypes.c_uint64 * 5),
+                ("proof_kind", ctypes.c_uint32), ("n_claims", ctypes.c_uint32),
+                ("proof_offset", ctypes.c_uint64), ("proof_len", ctypes.c_uint64),
+                ("kernel_offset", ctypes.c_uint64), ("appendix_offset", ctypes.c_uint64),
+                ("claim_words", ctypes.c_uint64), ("seq_words", ctypes.c_uint64)]
+
+
+class Tx(ctypes.Structure):
+    _fields_ = [("size", ctypes.c_uint64), ("kind", ctypes.c_uint32), ("n_proofs", ctypes.c_uint32),
+                ("n_lock_scripts", ctypes.c_uint32), ("n_type_scripts", ctypes.c_uint32),
+                ("n_lock_hashes", ctypes.c_uint32), ("n_type_hashes", ctypes.c_uint32),
+                ("n_merge_path", ctypes.c_uint32), ("n_digests", ctypes.c_uint32), ("seq_words", ctypes.c_uint64)]
 
 
 _pp = ctypes.POINTER(ctypes.c_void_p)
@@ -119,6 +136,12 @@ SIGNATURES = {
     "nhip_batch_transcript": ([_vp, _vp, _sz, _u64p, _sz, ctypes.POINTER(ctypes.c_uint32), _sz,
                                ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "nhip_batch_destroy": ([_vp], None),
+    "nhip_blk_scan": ([_vp, _sz, ctypes.c_uint32, _vp, _sz, ctypes.POINTER(_sz)], ctypes.c_int),
+    "nhip_blk_sequences": ([_vp, _sz, ctypes.c_uint32, ctypes.POINTER(BlkBlock), _vp, _sz, _vp], ctypes.c_int),
+    "nhip_blk_claims": ([_vp, _sz, ctypes.POINTER(BlkBlock), _vp, _vp], ctypes.c_int),
+    "nhip_le_words": ([_vp, _sz, ctypes.c_uint64, _sz, _vp], ctypes.c_int),
+    "nhip_tx_scan": ([_vp, _sz, ctypes.POINTER(Tx)], ctypes.c_int),
+    "nhip_tx_parts": ([_vp, _sz, ctypes.POINTER(Tx), _vp, _vp, _vp, _vp], ctypes.c_int),
     "nhip_timing_enable": ([_vp, ctypes.c_int], ctypes.c_int),
     "nhip_timing_read": ([_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int],
                          ctypes.c_int),
