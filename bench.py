@@ -11,14 +11,20 @@ multiproofs, out-of-domain AIR evaluation, FRI, DEEP.  5% of the collections car
 padded height from tests/golden/c3_pool.npz (made by tests/golden/make_bench_pool.py), each
 collection member stored separately in HBM.
 
-One step = every device phase over the resident batch + the verdict copy back (nhip_batch_launch /
-nhip_batch_wait over --pipeline sub-batches of whole collections, launched back to back on their own
-streams so that their latency-bound tails overlap) and, for N > 1, the batch verdict AND over ranks with one RCCL all-reduce(MIN) — the path's only
-exchange.  Every rank owns its own 2,048-proof batch (weak scaling).  Host decode +
+One step = every device phase over one resident batch + the verdict copy back (nhip_batch_launch /
+nhip_batch_wait) and, for N > 1, the batch verdict AND over ranks with one RCCL all-reduce(MIN) —
+the path's only exchange.  Steps are pipelined as a node verifying a stream of
+batches would run them (--inflight 2, default): two resident copies of the batch alternate, step k+1
+is launched before step k is waited on, so one step's latency-bound phases (Fiat-Shamir replay,
+Merkle plan, top Merkle levels) overlap the other's VALU-bound hashing.  Every timed step is
+launched and waited inside the timed region.  Two copies x 2 streams need more than HIP's default 4
+hardware queues per process (streams sharing a queue serialize), so GPU_MAX_HW_QUEUES defaults to 8
+here.  Every rank owns its own 2,048-proof batch (weak scaling).  Host decode +
 upload (nhip_batch_prepare) happens before the timed region and is reported separately.
 
 roofline: the dominant kernel, k_mp_hash (the per-level Merkle hash_pair launches), as Tip5
-VALU lane-ops/s against the gfx950 VALU peak; `tip5_paths` adds the config-2 Tip5 path microbench.
+VALU lane-ops/s against the gfx950 VALU peak, timed over the timed region (sharing the chip with the
+other step in flight); roofline_isolated: the same kernel in steps run one at a time; `tip5_paths` adds the config-2 Tip5 path microbench.
 cpu_baseline: the C restatement of the verifier (oracle/stark_oracle.c), one proof per host thread,
 over a bounded sample of this batch's proofs (the reference, Rust triton-vm, cannot be built here).
 
@@ -36,6 +42,11 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# before anything initialises HIP: 2 batches x 2 streams + the context stream (see above); the GPU
+# boxes export HIP's default of 4, which would put two streams on one queue
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+ISO_STEPS = 5
 sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
 
 P = (1 << 64) - (1 << 32) + 1
@@ -271,6 +282,10 @@ def main():
                     help="split the per-GPU batch into this many sub-batches (whole collections) launched "
                          "back to back on their own streams (measured slower: 2 -> 9.7 ms vs 6.6 ms, probably because the 4 HW "
                          "queues per process serialize the extra streams; DESIGN.md §3)")
+    ap.add_argument("--inflight", type=int, default=2, choices=(1, 2, 3),
+                    help="R > 1: R resident copies of the batch in rotation, R - 1 steps in flight (step k+1 is "
+                         "launched before step k is waited on, so its row hashing fills step k's latency-bound "
+                         "Merkle tail)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -328,15 +343,35 @@ def main():
         f"prepare {prep_s:.2f}s (decode {sum(x['ms_decode'] for x in st0):.0f} ms, "
         f"upload {sum(x['ms_upload'] for x in st0):.0f} ms)")
 
-    def run_all():
-        for b in batches:
+    R = args.inflight
+    ring = [batches] + [[NS.Batch(ctx, gair, stark, [NS.Claim(*c) for c in claims[a:b]], proofs[a:b])
+                         for a, b in zip(cuts[:-1], cuts[1:])] for _ in range(R - 1)]
+    launched = []   # ring slots in flight, oldest first
+    next_slot = [0]
+
+    def launch_next():
+        for b in ring[next_slot[0]]:
             b.launch()
+        launched.append(next_slot[0])
+        next_slot[0] = (next_slot[0] + 1) % R
+
+    last_waited = [batches]
+    to_launch = [0]  # launches left in the current region: each region starts and ends with nothing in flight
+
+    def run_all():
+        # keep up to R steps in flight (one per resident copy), then wait for the oldest
+        while to_launch[0] and len(launched) < R:
+            launch_next()
+            to_launch[0] -= 1
+        cur = ring[launched.pop(0)]
+        last_waited[0] = cur
         vs, ok = [], True
-        for b in batches:
+        for b in cur:
             v, o = b.wait()
             vs.append(v)
             ok = ok and o
         return np.concatenate(vs), ok
+
 
     gathered = [None]
 
@@ -355,22 +390,36 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    for _ in range(args.warmup):
+    to_launch[0] = args.warmup
+    for i in range(args.warmup):
         step()
     barrier_sync()
     acc = {}
     batch_ok = None
     t_start = time.perf_counter()
-    for _ in range(args.steps):
+    to_launch[0] = args.steps  # every timed step is launched and waited inside the region
+    for i in range(args.steps):
         batch_ok = step()
-        for b in batches:
+        for b in last_waited[0]:
             for k, v in b.stats().items():
                 acc[k] = acc.get(k, 0.0) + v
     barrier_sync()
     elapsed = time.perf_counter() - t_start
 
+    to_launch[0] = 1
     v, _ = run_all()
     correct = bool((np.asarray(v, dtype=bool) == expect).all())
+    # the same kernels with nothing else on the device: ISO_STEPS steps one at a time (with steps in
+    # flight the hash launches share the chip with the next step's kernels, which stretches them)
+    acc_iso = {}
+    if R > 1:
+        for _ in range(ISO_STEPS):
+            for b in batches:
+                b.launch()
+            for b in batches:
+                b.wait()
+                for k, val in b.stats().items():
+                    acc_iso[k] = acc_iso.get(k, 0.0) + val
     if gathered[0] is not None:
         correct = correct and bool((gathered[0].astype(bool) == expect_all).all())
     if dist is not None:
@@ -395,11 +444,21 @@ def main():
     # back on the batch's main stream between two HIP events: their summed duration / launch count is
     # the average launch duration (rocprofv3 cross-check: profiles/<tag>/SUMMARY.md, "Merkle hash
     # launches" line)
-    launches = max(avg["mp_hash_kernel_launches"], 1.0)
-    kern_avg_s = avg["ms_mp_hash_kernel"] / launches / 1e3
-    perms_per_launch = avg["mp_hash_kernel_perms"] / launches
-    achieved = perms_per_launch * TIP5_VALU_OPS_PER_PERM / kern_avg_s if kern_avg_s > 0 else 0.0
     traffic, traffic_tag = pmc_traffic("k_mp_hash")
+
+    def roofline(a, steps, measured):
+        a = {k: v / steps for k, v in a.items()}
+        launches = max(a["mp_hash_kernel_launches"], 1.0)
+        kern_avg_s = a["ms_mp_hash_kernel"] / launches / 1e3
+        perms_per_launch = a["mp_hash_kernel_perms"] / launches
+        achieved = perms_per_launch * TIP5_VALU_OPS_PER_PERM / kern_avg_s if kern_avg_s > 0 else 0.0
+        return {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
+                "unit": "T VALU lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS, "traffic": traffic,
+                "traffic_unit": "bytes per launch (FETCH_SIZE+WRITE_SIZE, raw; see DESIGN.md §3)",
+                "traffic_profile": traffic_tag, "kernel": "k_mp_hash (+ k_mp_hash_wide on the smallest levels)",
+                "kernel_avg_ms": kern_avg_s * 1e3, "launches_per_step": launches,
+                "perms_per_launch": perms_per_launch, "valu_ops_per_perm": TIP5_VALU_OPS_PER_PERM,
+                "measured": measured}
     if args.config == 3:
         workload = (f"BASELINE config 3: {args.collections} ProofCollections x 8 proofs (log2 padded heights "
                     f"{COLLECTION_HEIGHTS}) = {n} STARK verifications per GPU, Stark::default()")
@@ -441,14 +500,11 @@ def main():
         "host_prepare_ms": {"decode": sum(x["ms_decode"] for x in st0), "upload": sum(x["ms_upload"] for x in st0),
                             "total": prep_s * 1e3},
         "pipeline_sub_batches": P,
-        "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
-                     "unit": "T VALU lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS, "traffic": traffic,
-                     "traffic_unit": "bytes per launch (FETCH_SIZE+WRITE_SIZE, raw; see DESIGN.md §3)",
-                     "traffic_profile": traffic_tag, "kernel": "k_mp_hash (+ k_mp_hash_wide on the smallest levels)",
-                     "kernel_avg_ms": kern_avg_s * 1e3, "launches_per_step": launches,
-                     "perms_per_launch": perms_per_launch,
-                     "valu_ops_per_perm": TIP5_VALU_OPS_PER_PERM},
+        "inflight": R,
+        "roofline": roofline(acc, K, f"HIP events over the timed region ({R} step(s) in flight)"),
     }
+    if acc_iso:
+        res["roofline_isolated"] = roofline(acc_iso, ISO_STEPS, f"{ISO_STEPS} steps one at a time after the timed region")
     valu_step, valu_tag = pmc_valu_per_step()
     if args.config == 3 and valu_step:
         # the whole pipeline against the measured VALU issue ceiling: committed PMC instruction

@@ -9,5 +9,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -2 $OUT/pytest_gpu.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 1; }
 timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
-python3 -c "import json;b=json.load(open('$OUT/bench.json'));print(b['value'],b['ms_per_step'],b['roofline']['frac'],b['cpu_baseline']['value'],b['tip5_paths']['perms_per_s'])"
+python3 -c "import json;b=json.load(open('$OUT/bench.json'));print(b['value'],b['ms_per_step'],b['roofline']['frac'],b.get('roofline_isolated',{}).get('frac'),b['cpu_baseline']['value'],b['tip5_paths']['perms_per_s'])"
 bash tools/profile_round.sh $TAG

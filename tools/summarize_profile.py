@@ -34,9 +34,26 @@ if stats:
         print(f"\nMerkle hash launches (k_mp_hash + k_mp_hash_wide): {calls} calls, average "
               f"{tot_ns / calls / 1e6:.3f} ms per launch")
 bench = os.path.join(d, "bench_trace.json")
-if os.path.exists(bench):
-    b = json.load(open(bench))
-    print(f"\nbench (under profiler): value {b['value']:.4g} {b['unit']}, kernel avg {b['roofline']['kernel_avg_ms']:.3f} ms\n")
+b = json.load(open(bench)) if os.path.exists(bench) else None
+trace = glob.glob(os.path.join(d, "trace", "*kernel_trace.csv"))
+if trace and b and b.get("roofline_isolated"):
+    # bench.py runs the timed steps (steps in flight), then 5 steps one at a time: split the Merkle
+    # hash launches in time order into those two groups, each to compare with its bench figure
+    rows = sorted(csv.DictReader(open(trace[0])), key=lambda r: int(r["Start_Timestamp"]))
+    mh = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows
+          if kname(r["Kernel_Name"]).endswith(("k_mp_hash", "k_mp_hash_wide"))]
+    per_step = int(round(b["roofline"]["launches_per_step"]))
+    iso = 5 * per_step
+    timed = b["steps"] * per_step
+    if len(mh) >= iso + timed:
+        t, i = mh[-iso - timed:-iso], mh[-iso:]
+        print(f"\nMerkle hash launches of the timed steps (2 in flight): {len(t)} calls, average "
+              f"{sum(t) / len(t) / 1e6:.3f} ms; bench: {b['roofline']['kernel_avg_ms']:.3f} ms")
+        print(f"Merkle hash launches of the isolated steps: {len(i)} calls, average {sum(i) / len(i) / 1e6:.3f} ms; "
+              f"bench: {b['roofline_isolated']['kernel_avg_ms']:.3f} ms")
+if b:
+    print(f"\nbench (under profiler): value {b['value']:.4g} {b['unit']}, {b['ms_per_step']:.3f} ms per step, "
+          f"kernel avg {b['roofline']['kernel_avg_ms']:.3f} ms\n")
 print("## PMC (separate passes, per dispatch, averaged over dispatches of each kernel)\n")
 print("| kernel | counter | dispatches | mean per dispatch |")
 print("|---|---|---|---|")
