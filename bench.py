@@ -493,6 +493,10 @@ def main():
         "expected_rejects_rank0": int((~expect).sum()),
         "tip5_perms_per_proof": perms / n,
         "tip5_perms_per_s": perms_job * K / elapsed,
+        # BASELINE's second metric at the pipeline level: every Tip5 permutation of the step (sponge
+        # replay, rows, Merkle levels) x the analytic VALU lane-ops per permutation, per second of
+        # wall time, against the VALU peak
+        "tip5_valu_frac": perms_job * K / elapsed * TIP5_VALU_OPS_PER_PERM / (VALU_PEAK_LANE_OPS * world),
         # per sub-batch (each sub-batch's phases are timed by HIP events on its own two streams)
         "phase_ms": {k[3:]: round(avg[k] / P, 4) for k in ("ms_fiat_shamir", "ms_row_hash", "ms_merkle",
                                                             "ms_merkle_hash", "ms_ood_air", "ms_fri", "ms_deep",

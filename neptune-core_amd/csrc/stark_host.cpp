@@ -15,6 +15,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <system_error>
@@ -410,6 +411,52 @@ void decode_all(const Dims& D, const nhip_claim* claims, const nhip_proof* proof
     for (auto& th : pool) th.join();
 }
 
+// decode_all with the upload overlapped: the proofs are cut into chunks of ~CHUNK_WORDS staged
+// words; worker threads decode in proof order while this thread hands each finished chunk to
+// `ready(first_word, n_words)` (an async DMA), so the copy of chunk c runs under the decode of
+// c + 1.  Returns false when no worker thread could be started (the caller then decodes and
+// copies in one piece).
+template <class Ready>
+bool decode_all_streamed(const Dims& D, const nhip_claim* claims, const nhip_proof* proofs, size_t n,
+                         uint64_t* words, const std::vector<uint64_t>& bases, uint64_t words_total,
+                         std::vector<ProofOut>& outs, unsigned threads, Ready&& ready) {
+    constexpr uint64_t CHUNK_WORDS = 8ull << 20;  // 64 MB
+    std::vector<size_t> cut{0};                   // chunk c = proofs [cut[c], cut[c+1])
+    for (size_t i = 1; i < n; ++i)
+        if (bases[i] - bases[cut.back()] >= CHUNK_WORDS) cut.push_back(i);
+    cut.push_back(n);
+    const size_t nc = cut.size() - 1;
+    std::vector<size_t> chunk_of(n);
+    std::unique_ptr<std::atomic<size_t>[]> left(new std::atomic<size_t>[nc]);
+    for (size_t c = 0; c < nc; ++c) {
+        left[c].store(cut[c + 1] - cut[c]);
+        for (size_t i = cut[c]; i < cut[c + 1]; ++i) chunk_of[i] = c;
+    }
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        constexpr size_t STEP = 4;
+        for (size_t a; (a = next.fetch_add(STEP)) < n;)
+            for (size_t i = a; i < std::min(n, a + STEP); ++i) {
+                decode_proof(D, claims[i], proofs[i], words, bases[i], outs[i]);
+                left[chunk_of[i]].fetch_sub(1, std::memory_order_release);
+            }
+    };
+    std::vector<std::thread> pool;
+    try {
+        for (unsigned t = 0; t < threads; ++t) pool.emplace_back(work);
+    } catch (const std::system_error&) {
+    }
+    if (pool.empty()) return false;
+    for (size_t c = 0; c < nc; ++c) {
+        while (left[c].load(std::memory_order_acquire) != 0)
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        const uint64_t w0 = bases[cut[c]], w1 = c + 1 < nc ? bases[cut[c + 1]] : words_total;
+        ready(w0, w1 - w0);
+    }
+    for (auto& th : pool) th.join();
+    return true;
+}
+
 }  // namespace
 
 // ====================================================================== AIR object
@@ -438,6 +485,8 @@ struct VerifyScratch {
     std::mutex mu;
     void* dmem = nullptr;
     size_t dmem_bytes = 0;
+    void* dwords = nullptr;  // proof words (uploaded while they are decoded)
+    size_t dwords_bytes = 0;
     hipStream_t main = nullptr, aux = nullptr;
     hipEvent_t ev[STARK_EVENTS] = {};
     bool streams = false;
@@ -456,6 +505,7 @@ static void free_verify_scratch(void* p) {
     }
     if (sc->h_out) (void)hipHostFree(sc->h_out);
     if (sc->dmem) (void)hipFree(sc->dmem);
+    if (sc->dwords) (void)hipFree(sc->dwords);
     delete sc;
 }
 
@@ -474,6 +524,8 @@ struct nhip_batch {
     hipStream_t aux = nullptr;   // latency-bound chain (Fiat-Shamir -> plan -> OOD -> FRI -> DEEP)
     uint8_t* h_out = nullptr;    // pinned: [perm counter (8 B) | verdicts (n B)]
     size_t dmem_bytes = 0, h_out_bytes = 0;  // owned allocations (refill reuses them when they fit)
+    void* dwords = nullptr;                  // proof words (owned unless borrowed from the scratch)
+    size_t dwords_bytes = 0;
     bool timed = false, in_flight = false;
     struct {
         double fs, rows, plan, hash, roots, ood, fri, deep, total;
@@ -732,6 +784,7 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     auto fail_out = [&](int rc) {
         if (!reuse) {
             if (!scr && b->dmem) (void)hipFree(b->dmem);
+            if (!scr && b->dwords) (void)hipFree(b->dwords);
             delete b;
         } else {
             b->H = HostBatch{};
@@ -761,14 +814,54 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         pageable.resize(H.words_total + 1);
         words = pageable.data();
     }
+    // device buffer for the proof words (grow-only; its own allocation, so that it can be filled
+    // while the rest of the batch's sizes are still being decoded)
+    const size_t wbytes = H.words_total * 8 + 8;
+    {
+        void** dw = scr ? &scr->dwords : &b->dwords;
+        size_t* dwb = scr ? &scr->dwords_bytes : &b->dwords_bytes;
+        if (*dwb < wbytes) {
+            if (*dw) (void)hipFree(*dw);
+            *dw = nullptr;
+            *dwb = 0;
+            const size_t want = (reuse || scr) ? wbytes + wbytes / 4 : wbytes;
+            const hipError_t ea = hipMalloc(dw, want);
+            if (ea != hipSuccess) {
+                if (scr) b->dwords = nullptr;
+                return fail_out(hipfail(ea));
+            }
+            *dwb = want;
+        }
+        b->dwords = *dw;
+    }
+    hipStream_t st = nhip_internal_stream(ctx);
+    uint64_t* d_words = (uint64_t*)b->dwords;
+    hipError_t e = hipSuccess;
     auto t0 = std::chrono::steady_clock::now();
     {
         std::vector<ProofOut> outs(n);
-        decode_all(D, claims, proofs, n, words, bases, outs, host_threads(n));
+        const unsigned threads = host_threads(n);
+        bool streamed = false;
+        if (threads > 1 && words != pageable.data())
+            streamed = decode_all_streamed(D, claims, proofs, n, words, bases, H.words_total, outs, threads,
+                                           [&](uint64_t w0, uint64_t nw) {
+                                               if (e == hipSuccess && nw)
+                                                   e = hipMemcpyAsync(d_words + w0, words + w0, nw * 8,
+                                                                      hipMemcpyHostToDevice, st);
+                                           });
+        if (!streamed) {
+            decode_all(D, claims, proofs, n, words, bases, outs, threads);
+            if (H.words_total) e = hipMemcpyAsync(d_words, words, H.words_total * 8, hipMemcpyHostToDevice, st);
+        }
         for (size_t i = 0; i < n; ++i) merge_proof(H, outs[i], proofs[i].len);
     }
     auto t1 = std::chrono::steady_clock::now();
     b->decode_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    if (e != hipSuccess) {
+        (void)hipStreamSynchronize(st);
+        if (scr) b->dwords = nullptr;
+        return fail_out(hipfail(e));
+    }
     int rc = air_upload(ctx, air);
     if (rc) return fail_out(rc);
     static bool attrs = false;
@@ -802,7 +895,7 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
             mp_total += mp_scap[(size_t)l * MP_SHARDS + q];
             b->mp_cap[l] += mp_scap[(size_t)l * MP_SHARDS + q];
         }
-    const size_t sz[] = {H.words_total * 8 + 8,
+    const size_t sz[] = {8,  // (slot 0 unused: the proof words have their own allocation)
                          std::max<size_t>(1, n) * sizeof(ProofDesc),
                          H.ops.size() * sizeof(FsOp) + 8,
                          H.xs_total * 24 + 8,
@@ -826,7 +919,6 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     constexpr int NBUF = sizeof(sz) / sizeof(sz[0]);
     size_t total = 0;
     for (size_t s : sz) total += al(s);
-    hipError_t e = hipSuccess;
     if (scr) {  // grow-only device scratch of the context
         if (scr->dmem_bytes < total) {
             if (scr->dmem) (void)hipFree(scr->dmem);
@@ -854,9 +946,7 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         ptr[i] = p;
         p += al(sz[i]);
     }
-    hipStream_t st = nhip_internal_stream(ctx);
-    e = hipMemcpyAsync(ptr[0], words, H.words_total * 8, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess && n) e = hipMemcpyAsync(ptr[1], H.desc.data(), n * sizeof(ProofDesc), hipMemcpyHostToDevice, st);
+    if (n) e = hipMemcpyAsync(ptr[1], H.desc.data(), n * sizeof(ProofDesc), hipMemcpyHostToDevice, st);
     if (e == hipSuccess && !H.ops.empty())
         e = hipMemcpyAsync(ptr[2], H.ops.data(), H.ops.size() * sizeof(FsOp), hipMemcpyHostToDevice, st);
     if (e == hipSuccess && n) e = hipMemcpyAsync(ptr[8], H.fail.data(), n * 4, hipMemcpyHostToDevice, st);
@@ -872,7 +962,7 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     dv.n_proofs = (uint32_t)n;
     dv.max_R = H.max_R;
     dv.dims = D.d;
-    dv.words = (const uint64_t*)ptr[0];
+    dv.words = d_words;
     dv.desc = (const ProofDesc*)ptr[1];
     dv.ops = (const FsOp*)ptr[2];
     dv.xs = (uint64_t*)ptr[3];
@@ -1121,6 +1211,7 @@ void nhip_batch_destroy(nhip_batch* b) {
     if (b->aux) (void)hipStreamDestroy(b->aux);
     if (b->h_out) (void)hipHostFree(b->h_out);
     if (b->dmem) (void)hipFree(b->dmem);
+    if (b->dwords) (void)hipFree(b->dwords);
     delete b;
 }
 
