@@ -8,6 +8,6 @@ for r in $(seq 1 $R); do
   for v in "$@"; do
     i=$((i+1))
     env $v timeout -k 10 300 python -u bench.py --no-cpu --paths-log2 0 > $OUT/v$i.$r.json 2> $OUT/v$i.$r.err || { tail $OUT/v$i.$r.err; exit 1; }
-    python3 -c "import json;b=json.load(open('$OUT/v$i.$r.json'));p=b['phase_ms'];print('$v',round(b['ms_per_step'],3),'rows',p['row_hash'],'hash',p['merkle_hash'],'ood',p['ood_air'],'fri',p['fri'],'deep',p['deep'],b['verdicts_correct'])"
+    python3 -c "import json;b=json.load(open('$OUT/v$i.$r.json'));p=b['phase_ms'];print('$v',round(b['ms_per_step'],3),'rf',round(b['roofline']['frac'],3),round(b['roofline']['kernel_avg_ms'],3),'rows',p['row_hash'],'hash',p['merkle_hash'],'ood',p['ood_air'],'fri',p['fri'],'deep',p['deep'],b['verdicts_correct'])"
   done
 done
