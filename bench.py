@@ -100,6 +100,30 @@ def pmc_valu_per_step():
         return None, None
 
 
+def pmc_bytes_per_step():
+    """HBM bytes (raw FETCH_SIZE + WRITE_SIZE, x 1024) one config-3 step moves, summed over the step's
+    dispatches in the latest committed PMC passes (microbench and runtime copy kernels excluded;
+    steps = k_hash_rows dispatches); None when absent."""
+    import csv
+    try:
+        tag = open(os.path.join(ROOT, "profiles", "LATEST")).read().strip()
+        tot, steps = 0.0, 0
+        for part, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+            n_rows = 0
+            for r in csv.DictReader(open(os.path.join(ROOT, "profiles", tag, f"pmc_{part}_counter_collection.csv"))):
+                k = r["Kernel_Name"]
+                if r["Counter_Name"] != ctr or "mtree" in k or "rocclr" in k:
+                    continue
+                tot += float(r["Counter_Value"]) * 1024
+                n_rows += "k_hash_rows" in k
+            steps = n_rows
+        return (tot / steps, tag) if steps else (None, None)
+    except (OSError, KeyError):
+        return None, None
+
+
+HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md; 6.29 TB/s measured copy)
+
 # measured gfx950 issue ceiling for this instruction mix: ~1 wave64 VALU instruction per 4 clocks
 # per SIMD (DESIGN.md §3, tools/valu_microbench.hip)
 VALU_ISSUE_CEILING = 256 * 4 * 2.4e9 / 4
@@ -519,6 +543,15 @@ def main():
         res["valu_issue"] = {"wave_instr_per_step": valu_step, "profile": valu_tag,
                              "ceiling_wave_instr_per_s": VALU_ISSUE_CEILING,
                              "frac": valu_step / (elapsed / K) / VALU_ISSUE_CEILING}
+    # proof streaming: every proof word is read by the device at least once per step
+    words_step = sum(x["proof_words"] for x in st0)
+    step_s = elapsed / K
+    res["hbm"] = {"proof_bytes_per_step": words_step * 8, "achieved_GBps": words_step * 8 / step_s / 1e9,
+                  "peak_GBps": HBM_PEAK / 1e9, "frac": words_step * 8 / step_s / HBM_PEAK}
+    bytes_step, bytes_tag = pmc_bytes_per_step()
+    if args.config == 3 and bytes_step:
+        res["hbm"].update({"pmc_bytes_per_step": bytes_step, "pmc_GBps": bytes_step / step_s / 1e9,
+                           "pmc_frac": bytes_step / step_s / HBM_PEAK, "pmc_profile": bytes_tag})
     if rank == 0 and args.paths_log2 > 0:
         res["tip5_paths"] = tip5_paths(ctx, args.paths_log2, 5)
     if cpu is not None:
