@@ -485,6 +485,10 @@ def main():
                 "traffic_profile": traffic_tag, "kernel": "k_mp_hash (+ k_mp_hash_wide on the smallest levels)",
                 "kernel_avg_ms": kern_avg_s * 1e3, "launches_per_step": launches,
                 "perms_per_launch": perms_per_launch, "valu_ops_per_perm": TIP5_VALU_OPS_PER_PERM,
+                # beside the spec peak: the measured integer issue ceiling (1 wave64 instruction per
+                # 4 clocks per SIMD = 64 lane-ops per instruction), DESIGN.md §3
+                "measured_ceiling": VALU_ISSUE_CEILING * 64 / 1e12,
+                "frac_of_measured_ceiling": achieved / (VALU_ISSUE_CEILING * 64),
                 "measured": measured}
     if args.config == 3:
         workload = (f"BASELINE config 3: {args.collections} ProofCollections x 8 proofs (log2 padded heights "
