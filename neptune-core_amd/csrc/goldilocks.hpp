@@ -118,8 +118,19 @@ __host__ __device__ __forceinline__ uint64_t gl_sub(uint64_t a, uint64_t b) {
     return a < b ? d + GL_P : d;
 }
 
-// Any u64 (BFieldElement::new semantics: reduced mod p) -> raw Montgomery word.
-__host__ __device__ __forceinline__ uint64_t to_mont(uint64_t x) { return mont_mul(x, GL_R2); }
+// Any u64 (BFieldElement::new semantics: reduced mod p) -> raw Montgomery word x * 2^64 mod p.
+// With x = h * 2^32 + l and 2^64 == 2^32 - 1 (mod p):  x * 2^64 == l * 2^32 - h - l, and that
+// integer lies in (-2^33, p - 1], so one conditional + p makes it canonical: the same word as
+// mont_mul(x, 2^128 mod p) in ~7 VALU instead of a Montgomery product (tests/test_constants.py
+// and the CPU test of this header check the identity).
+__host__ __device__ __forceinline__ uint64_t to_mont(uint64_t x) {
+    const uint32_t l = (uint32_t)x, h = (uint32_t)(x >> 32);
+    const uint64_t s = (uint64_t)h + l;
+    const uint64_t t = (uint64_t)l << 32;
+    const uint64_t v = t - s;
+    return t < s ? v + GL_P : v;
+}
+__host__ __device__ __forceinline__ uint64_t to_mont_mul(uint64_t x) { return mont_mul(x, GL_R2); }
 
 // Raw Montgomery word -> canonical value (BFieldElement::value()).
 __host__ __device__ __forceinline__ uint64_t from_mont(uint64_t r) { return montyred(r, 0); }

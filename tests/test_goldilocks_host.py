@@ -1,0 +1,23 @@
+"""goldilocks.hpp compiled for the host: the closed-form to_mont equals the Montgomery product by
+2^128 mod p (BFieldElement::new -> raw word) on edge words (limbs near 0, 2^31, 2^32 - 1; words
+around p and 2^64) and 2M random words.  CPU only."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_to_mont_closed_form_matches_montgomery_product(tmp_path):
+    exe = tmp_path / "to_mont_check"
+    subprocess.check_call([HIPCC, "-O2", "-std=c++17", "-x", "hip", "--offload-arch=gfx950",
+                           "-I", os.path.join(ROOT, "neptune-core_amd", "csrc"),
+                           os.path.join(ROOT, "tests", "native", "to_mont_check.cpp"), "-o", str(exe)],
+                          stderr=subprocess.DEVNULL)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "bad 0" in out.stdout
