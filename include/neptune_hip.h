@@ -182,6 +182,30 @@ int nhip_batch_transcript(nhip_ctx *ctx, const nhip_batch *batch, size_t proof, 
                           uint32_t *idx_out, size_t idx_cap, uint32_t *fail_bits, size_t *n_xfe);
 void nhip_batch_destroy(nhip_batch *batch);
 
+/* ---- several GPUs from one process --------------------------------------
+ * neptune-core is one process; its batch callers (proof_collection.rs:342-388,
+ * state/mod.rs:2226-2272, peer_loop.rs:315-323) end in n calls of triton_vm::verify at
+ * verifier.rs:60-63.  A group owns one context per member device (duplicates allowed: several
+ * contexts on one GPU).  nhip_group_verify_batch shards the proofs over the members (LPT on the
+ * proof length, nhip_group_shard), verifies every shard concurrently on its member (one host
+ * thread each, nhip_verify_batch semantics) and writes the verdicts in the caller's order;
+ * *all_ok (nullable) = AND of the verdicts.  A non-zero return (any member's infrastructure
+ * fault) leaves the verdicts unknown: never "accept". */
+typedef struct nhip_group nhip_group;
+int nhip_group_create(const int *devices, size_t n_devices, nhip_group **out);
+/* One member per set bit of device_mask (0 = every visible device). */
+int nhip_group_init(uint32_t device_mask, nhip_group **out);
+void nhip_group_destroy(nhip_group *group);
+size_t nhip_group_size(const nhip_group *group);
+/* Borrowed member context (NULL when i is out of range). */
+nhip_ctx *nhip_group_member(nhip_group *group, size_t i);
+/* member_of[i] = the member proof i goes to: longest proofs first, each to the least-loaded
+ * member (host only, deterministic). */
+int nhip_group_shard(const nhip_proof *proofs, size_t n, size_t n_members, uint32_t *member_of);
+int nhip_group_verify_batch(nhip_group *group, nhip_air *air, const nhip_stark_params *params,
+                            const nhip_claim *claims, const nhip_proof *proofs, size_t n, uint8_t *verdicts,
+                            uint8_t *all_ok);
+
 /* ---- ingestion formats -------------------------------------------
  * Proof files of neptune-core/src/protocol/proof_abstractions/tasm/program.rs:374-390: 8-byte
  * big-endian chunks, each BFieldElement::new (reduced mod p); n_bytes not a multiple of 8 ->

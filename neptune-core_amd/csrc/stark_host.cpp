@@ -470,11 +470,17 @@ struct nhip_air {
     std::vector<uint32_t> prog_off;
     std::vector<Xfe> consts;
     uint32_t slots = 0;
-    // device copies per context (one context per process in practice)
-    nhip_ctx* dev_ctx = nullptr;
-    OodIns* d_prog = nullptr;
-    uint32_t* d_prog_off = nullptr;
-    Xfe* d_consts = nullptr;
+    // device copies, one per context that has used this AIR (a group drives several contexts
+    // from one process, possibly concurrently); created on first use, freed with the AIR
+    struct Dev {
+        nhip_ctx* ctx;
+        int device;
+        OodIns* d_prog;
+        uint32_t* d_prog_off;
+        Xfe* d_consts;
+    };
+    std::mutex mu;
+    std::vector<Dev> devs;
 };
 
 // Device memory, streams, events and pinned readback of nhip_verify_batch, kept in the context
@@ -572,18 +578,39 @@ bool dims_from(const nhip_stark_params* sp, const nhip_air* air, Dims& D) {
     return true;
 }
 
-int air_upload(nhip_ctx* ctx, nhip_air* a) {
-    if (a->dev_ctx == ctx) return NHIP_OK;
-    hipError_t e = hipMalloc(&a->d_prog, a->prog.size() * sizeof(OodIns) + 16);
-    if (e == hipSuccess) e = hipMalloc(&a->d_prog_off, a->prog_off.size() * 4 + 4);
-    if (e == hipSuccess) e = hipMalloc(&a->d_consts, a->consts.size() * sizeof(Xfe) + 24);
+// This context's device copy of the compiled AIR (uploaded on first use).
+int air_upload(nhip_ctx* ctx, nhip_air* a, nhip_air::Dev* out) {
+    std::lock_guard<std::mutex> g(a->mu);
+    for (const auto& d : a->devs)
+        if (d.ctx == ctx) {
+            *out = d;
+            return NHIP_OK;
+        }
+    nhip_air::Dev d{ctx, nhip_internal_device(ctx), nullptr, nullptr, nullptr};
+    hipError_t e = hipMalloc(&d.d_prog, a->prog.size() * sizeof(OodIns) + 16);
+    if (e == hipSuccess) e = hipMalloc(&d.d_prog_off, a->prog_off.size() * 4 + 4);
+    if (e == hipSuccess) e = hipMalloc(&d.d_consts, a->consts.size() * sizeof(Xfe) + 24);
     if (e == hipSuccess && !a->prog.empty())
-        e = hipMemcpy(a->d_prog, a->prog.data(), a->prog.size() * sizeof(OodIns), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(a->d_prog_off, a->prog_off.data(), a->prog_off.size() * 4, hipMemcpyHostToDevice);
+        e = hipMemcpy(d.d_prog, a->prog.data(), a->prog.size() * sizeof(OodIns), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d.d_prog_off, a->prog_off.data(), a->prog_off.size() * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess && !a->consts.empty())
-        e = hipMemcpy(a->d_consts, a->consts.data(), a->consts.size() * sizeof(Xfe), hipMemcpyHostToDevice);
-    if (e != hipSuccess) return hipfail(e);
-    a->dev_ctx = ctx;
+        e = hipMemcpy(d.d_consts, a->consts.data(), a->consts.size() * sizeof(Xfe), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (d.d_prog) (void)hipFree(d.d_prog);
+        if (d.d_prog_off) (void)hipFree(d.d_prog_off);
+        if (d.d_consts) (void)hipFree(d.d_consts);
+        return hipfail(e);
+    }
+    try {
+        a->devs.reserve(a->devs.size() + 1);
+    } catch (const std::bad_alloc&) {
+        (void)hipFree(d.d_prog);
+        (void)hipFree(d.d_prog_off);
+        (void)hipFree(d.d_consts);
+        return NHIP_ERR_OOM;
+    }
+    a->devs.push_back(d);
+    *out = d;
     return NHIP_OK;
 }
 
@@ -732,10 +759,11 @@ int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
 
 void nhip_air_destroy(nhip_air* a) {
     if (!a) return;
-    if (a->dev_ctx) {
-        (void)hipFree(a->d_prog);
-        (void)hipFree(a->d_prog_off);
-        (void)hipFree(a->d_consts);
+    for (const auto& d : a->devs) {
+        (void)hipSetDevice(d.device);
+        (void)hipFree(d.d_prog);
+        (void)hipFree(d.d_prog_off);
+        (void)hipFree(d.d_consts);
     }
     delete a;
 }
@@ -862,12 +890,18 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         if (scr) b->dwords = nullptr;
         return fail_out(hipfail(e));
     }
-    int rc = air_upload(ctx, air);
+    nhip_air::Dev adev{};
+    int rc = air_upload(ctx, air, &adev);
     if (rc) return fail_out(rc);
-    static bool attrs = false;
-    if (!attrs) {
-        if (stark_set_kernel_attributes() != hipSuccess) return fail_out(NHIP_ERR_HIP);
-        attrs = true;
+    {
+        static std::mutex attrs_mu;
+        static uint64_t attrs_set = 0;  // devices whose kernel attributes are set
+        std::lock_guard<std::mutex> attrs_lock(attrs_mu);
+        const int adevice = nhip_internal_device(ctx);
+        if (adevice >= 64 || !((attrs_set >> adevice) & 1u)) {
+            if (stark_set_kernel_attributes() != hipSuccess) return fail_out(NHIP_ERR_HIP);
+            if (adevice < 64) attrs_set |= 1ull << adevice;
+        }
     }
     const uint32_t k = D.d.num_checks;
     // multiproof op capacity per (level, shard): a tree of height h has at most min(k, 2^(h-1-l))
@@ -988,10 +1022,10 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     dv.max_lcw = H.max_last_cw;
     dv.fail_init = b->d_fail_init;
     dv.mp_cap_host = b->mp_cap.data();
-    dv.air_prog = air->d_prog;
-    dv.air_prog_off = air->d_prog_off;
+    dv.air_prog = adev.d_prog;
+    dv.air_prog_off = adev.d_prog_off;
     dv.air_n_levels = (uint32_t)air->prog_off.size() - 1;
-    dv.air_consts = air->d_consts;
+    dv.air_consts = adev.d_consts;
     dv.air_cons_off = air->cons_off;
     dv.air_lds_bytes = AIR_LDS_HEADER + (size_t)air->slots * 24;
     if (dv.air_lds_bytes > 160 * 1024 - 8192)

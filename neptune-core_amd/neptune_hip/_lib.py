@@ -125,6 +125,14 @@ SIGNATURES = {
                            ctypes.c_int),
     "nhip_verify_batch": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof),
                            _sz, _u8p, ctypes.POINTER(Stats)], ctypes.c_int),
+    "nhip_group_create": ([ctypes.POINTER(ctypes.c_int), _sz, ctypes.POINTER(_vp)], ctypes.c_int),
+    "nhip_group_init": ([ctypes.c_uint32, ctypes.POINTER(_vp)], ctypes.c_int),
+    "nhip_group_destroy": ([_vp], None),
+    "nhip_group_size": ([_vp], _sz),
+    "nhip_group_member": ([_vp, _sz], _vp),
+    "nhip_group_shard": ([ctypes.POINTER(Proof), _sz, _sz, ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+    "nhip_group_verify_batch": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof),
+                                 _sz, _u8p, ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
     "nhip_batch_prepare": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof),
                             _sz, _pp], ctypes.c_int),
     "nhip_batch_refill": ([_vp, _vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim),

@@ -183,6 +183,57 @@ def verify(ctx, air: Air, stark: Stark, claim: Claim, proof: Sequence[int]) -> b
     return verify_batch(ctx, air, stark, [(claim, proof)])[0]
 
 
+class Group:
+    """Several GPUs (or several contexts on one GPU) from one process: ``nhip_group``.
+    ``Group([0, 1, 2, 3])`` or ``Group(mask=0)`` (every visible device)."""
+
+    def __init__(self, devices: Sequence[int] = None, mask: int = None):
+        self.lib = _lib.load()
+        h = ctypes.c_void_p()
+        if devices is not None:
+            arr = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+            check(self.lib.nhip_group_create(arr, len(devices), ctypes.byref(h)), "nhip_group_create")
+        else:
+            check(self.lib.nhip_group_init(ctypes.c_uint32(mask or 0), ctypes.byref(h)), "nhip_group_init")
+        self.handle = h.value
+
+    def __len__(self) -> int:
+        return int(self.lib.nhip_group_size(self.handle))
+
+    def close(self):
+        if self.handle:
+            self.lib.nhip_group_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def group_shard(proofs: Sequence[Sequence[int]], n_members: int) -> List[int]:
+    """Member of each proof under nhip_group_verify_batch's LPT split (host only)."""
+    m = _Marshal([Claim([0] * 5) for _ in proofs], proofs)
+    out = (ctypes.c_uint32 * max(m.n, 1))()
+    check(_lib.load().nhip_group_shard(m.proofs, m.n, n_members, out), "nhip_group_shard")
+    return [int(out[i]) for i in range(m.n)]
+
+
+def verify_batch_group(group: Group, air: Air, stark: Stark,
+                       pairs: Sequence[Tuple[Claim, Sequence[int]]]) -> Tuple[List[bool], bool]:
+    """`verify_batch(&[(Claim, Proof)])` over every member of the group: (verdicts, all_ok)."""
+    claims = [c for c, _ in pairs]
+    proofs = [p for _, p in pairs]
+    m = _Marshal(claims, proofs)
+    v = np.zeros(max(m.n, 1), dtype=np.uint8)
+    ok = ctypes.c_uint8(0)
+    params = stark.c()
+    check(group.lib.nhip_group_verify_batch(group.handle, air.handle, ctypes.byref(params), m.claims, m.proofs, m.n,
+                                            v, ctypes.byref(ok)), "nhip_group_verify_batch")
+    return [bool(x) for x in v[:m.n]], bool(ok.value)
+
+
 def proof_decodes(air: Air, stark: Stark, claim: Claim, proof: Sequence[int]) -> bool:
     """Host-only structural decode of the proof stream (no GPU)."""
     m = _Marshal([claim], [proof])
