@@ -114,16 +114,23 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
     for (uint32_t o = 0; o < d.fs_op_n; ++o) {
         const FsOp op = ops[d.fs_op_off + o];
         if (op.kind == FS_ABSORB) {
+            // len / 10 full chunks, then the padded one; each chunk's word is loaded while the
+            // previous chunk's permutation runs (the load is off the sponge's critical path)
             const uint64_t* __restrict__ src = words + op.arg;
             const uint32_t len = op.n;
-            uint32_t pos = 0;
-            for (; pos + TIP5_RATE <= len; pos += TIP5_RATE) {
-                if (e < TIP5_RATE) s = to_mont(src[pos + e]);
+            const uint32_t nchunks = len / TIP5_RATE + 1;
+            uint64_t w = (e < TIP5_RATE && e < len) ? src[e] : 0ull;
+            for (uint32_t c = 0; c < nchunks; ++c) {
+                const uint32_t pos = c * TIP5_RATE;
+                const uint64_t cur = w;
+                const uint32_t ni = pos + TIP5_RATE + e;
+                w = (e < TIP5_RATE && ni < len) ? src[ni] : 0ull;
+                if (e < TIP5_RATE) {
+                    const uint32_t rem = len - pos;  // >= 10 except in the last chunk
+                    s = e < rem ? to_mont(cur) : (e == rem ? MONT_ONE : 0ull);
+                }
                 s = tip5_permute_wide(s, e, rc, lds.lut);
             }
-            const uint32_t rem = len - pos;
-            if (e < TIP5_RATE) s = e < rem ? to_mont(src[pos + e]) : (e == rem ? MONT_ONE : 0ull);
-            s = tip5_permute_wide(s, e, rc, lds.lut);
         } else if (op.kind == FS_SQUEEZE_X) {
             const uint32_t nwords = 3 * op.n;
             for (uint32_t f = 0; f < nwords; f += TIP5_RATE) {
