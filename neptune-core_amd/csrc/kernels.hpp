@@ -33,6 +33,10 @@ static constexpr uint32_t AIR_LDS_HEADER = (256 + 4 + 4 + 4) * 24 + 16;  // red,
 static constexpr uint32_t MP_SHARDS = 16;
 // levels with at most this many hash ops run the 16-lane-row Tip5 (latency-bound regime)
 static constexpr uint64_t MP_WIDE_MAX_OPS = 48 * 1024;
+// batches below this many proofs replay Fiat-Shamir on the two-row pair Tip5 (k_fs_replay_wide):
+// one-collection latency 1.89 -> 1.65 ms, while from 512 proofs on (several steps in flight) the
+// one-row form is 2-3% faster (profiles/r01i/ab_pair.log)
+static constexpr uint32_t FS_PAIR_MAX_PROOFS = 512;
 struct MpRoot {
     uint64_t code;  // source code of the tree's final node, ~0 = no check (skipped or already failed)
     uint64_t root_off;

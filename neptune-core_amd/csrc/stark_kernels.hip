@@ -3,6 +3,8 @@
 // Conventions: the batch word buffer holds canonical u64 field elements (proof words and staged
 // claims); every scratch value written by these kernels (samples, row digests, OOD sums) is a raw
 // Montgomery word.  Each failed check ORs a FailBits bit into fail[proof].
+#include <cstdlib>
+
 #include "kernels.hpp"
 #include "stark.hpp"
 #include "tip5_device.hpp"
@@ -91,8 +93,13 @@ __global__ void __launch_bounds__(64) k_fs_replay(const uint64_t* __restrict__ w
     }
 }
 
-// Same program on the 16-lane "wide" Tip5 (one proof per DPP row): ~10x lower latency per
-// permutation, which is what a sequential sponge needs.
+// Same program on the 16-lane "wide" Tip5 (one proof per DPP row, PAIR = false: ~10x lower
+// latency per permutation than a lane per proof, which is what a sequential sponge needs), or on
+// the two-row "pair" Tip5 (one proof per 32 lanes, PAIR = true: about a quarter fewer dependent
+// instructions per permutation again, at ~1.5x the lane-instructions; used for batches small
+// enough that the sponge replay is on the critical path with most SIMDs idle).  Both rows of a
+// pair hold the same state; only row 0 writes.
+template <bool PAIR>
 __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restrict__ words,
                                                         const ProofDesc* __restrict__ desc,
                                                         const FsOp* __restrict__ ops, uint32_t n_proofs,
@@ -100,17 +107,27 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
                                                         const uint32_t* __restrict__ fail) {
     __shared__ Tip5Lds lds;
     tip5_lds_init(lds);
+    constexpr uint32_t LANES = PAIR ? 32u : 16u;
     const uint32_t e = threadIdx.x & 15u;
-    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
-    if (g >= n_proofs || fail[g]) return;  // uniform within the 16-lane row
+    const uint32_t h = PAIR ? (threadIdx.x >> 4) & 1u : 0u;
+    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / LANES;
+    if (g >= n_proofs || fail[g]) return;  // uniform within the proof's lanes
     uint64_t rc[TIP5_ROUNDS];
 #pragma unroll
     for (int r = 0; r < TIP5_ROUNDS; ++r) rc[r] = c_tip5_rc_raw[r * 16 + e];
+    uint32_t cm[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cm[j] = h ? TIP5_MDS[j + 8] : TIP5_MDS[j];
+    auto permute = [&](uint64_t st) {
+        if constexpr (PAIR) return tip5_permute_pair(st, e, h, rc, cm, lds.lut);
+        else return tip5_permute_wide(st, e, rc, lds.lut);
+    };
+    const bool writer = h == 0;
     const ProofDesc& d = desc[g];
     uint64_t s = 0;
     uint64_t xcur = d.xs_off * 3;
     uint64_t icur = d.idx_off;
-    const uint32_t row_shift = threadIdx.x & 48u;  // first lane of this row within the wave
+    const uint32_t row_shift = threadIdx.x & (64u - LANES);  // first lane of this proof (row 0) in the wave
     for (uint32_t o = 0; o < d.fs_op_n; ++o) {
         const FsOp op = ops[d.fs_op_off + o];
         if (op.kind == FS_ABSORB) {
@@ -129,13 +146,13 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
                     const uint32_t rem = len - pos;  // >= 10 except in the last chunk
                     s = e < rem ? to_mont(cur) : (e == rem ? MONT_ONE : 0ull);
                 }
-                s = tip5_permute_wide(s, e, rc, lds.lut);
+                s = permute(s);
             }
         } else if (op.kind == FS_SQUEEZE_X) {
             const uint32_t nwords = 3 * op.n;
             for (uint32_t f = 0; f < nwords; f += TIP5_RATE) {
-                if (e < TIP5_RATE && f + e < nwords) xs[xcur + f + e] = s;
-                s = tip5_permute_wide(s, e, rc, lds.lut);
+                if (writer && e < TIP5_RATE && f + e < nwords) xs[xcur + f + e] = s;
+                s = permute(s);
             }
             xcur += nwords;
         } else {  // FS_SAMPLE_IDX
@@ -143,12 +160,12 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
             uint32_t got = 0;
             while (got < op.n) {
                 const uint64_t v = from_mont(s);
-                s = tip5_permute_wide(s, e, rc, lds.lut);
+                s = permute(s);
                 const bool valid = e < TIP5_RATE && v != GL_P - 1;
                 const uint64_t ball = __ballot(valid);
                 const uint32_t bits = (uint32_t)(ball >> row_shift) & 0x3FFu;
                 const uint32_t rank = __popc(bits & ((1u << e) - 1u));
-                if (valid && got + rank < op.n) idx_out[icur + got + rank] = (uint32_t)((v & 0xFFFFFFFFull) % bound);
+                if (writer && valid && got + rank < op.n) idx_out[icur + got + rank] = (uint32_t)((v & 0xFFFFFFFFull) % bound);
                 got += __popc(bits);
             }
             icur += op.n;
@@ -1049,6 +1066,16 @@ __global__ void k_verdicts(const uint32_t* __restrict__ fail, uint32_t n, uint8_
 }
 
 // ------------------------------------------------------------------ launchers
+// Fiat-Shamir replay form for an n-proof batch (see k_fs_replay_wide).
+static bool fs_pair(uint32_t n) {
+    static const int forced = [] {
+        const char* v = std::getenv("NHIP_FS_PAIR");
+        return v ? (v[0] == '1' ? 1 : 0) : -1;
+    }();
+    if (forced >= 0) return forced == 1;
+    return n < FS_PAIR_MAX_PROOFS;
+}
+
 hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream_t sa, StarkPhaseTimer* tm) {
     const uint32_t n = b.n_proofs;
     if (n == 0) return hipSuccess;
@@ -1059,8 +1086,15 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     mark(0, st);
     (void)hipStreamWaitEvent(sa, tm->ev[0], 0);
     // ---- aux stream: latency-bound chain
-    hipLaunchKernelGGL(k_fs_replay_wide, dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words, b.desc, b.ops, n,
-                       b.xs, b.idx, b.fail);
+    // small batches: the sponge replay is the critical path and most SIMDs are idle, so two rows
+    // per proof (pair form) for a shorter permutation; large ones: one row per proof (fewer
+    // lane-instructions while the other steps' hashing fills the GPU).  NHIP_FS_PAIR=0/1 forces one.
+    if (fs_pair(n))
+        hipLaunchKernelGGL(k_fs_replay_wide<true>, dim3((n * 32 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
+                           b.ops, n, b.xs, b.idx, b.fail);
+    else
+        hipLaunchKernelGGL(k_fs_replay_wide<false>, dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
+                           b.ops, n, b.xs, b.idx, b.fail);
     mark(1, sa);
     if (k <= 128)
         hipLaunchKernelGGL(k_mp_plan<128>, dim3(n, 1 + b.max_R), dim3(128), 0, sa, b.words, b.desc, n, k, tpp, b.dig,

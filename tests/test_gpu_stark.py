@@ -371,3 +371,28 @@ def test_batch_refill_and_streaming(ctx):
         assert [bool(x) for x in v] == list(s[2])
     b.close()
     a2.close()
+
+
+def test_fs_row_and_pair_forms_agree(ctx):
+    """The Fiat-Shamir replay runs on the two-row pair Tip5 below FS_PAIR_MAX_PROOFS (512) proofs
+    and on the one-row form from there on: a 520-proof batch (one-row) and an 8-proof batch (pair)
+    of the same pool proofs give the same verdicts and the same transcripts (every sample, every
+    FRI index) for every pool height."""
+    NS = _ns()
+    air_w, pool = _pool()
+    gair = NS.Air([int(w) for w in air_w])
+    stark = NS.Stark.default()
+    claims = [NS.Claim(*c) for c, _, _ in pool]
+    proofs = [p for _, p, _ in pool]
+    reps = 520 // len(pool) + 1
+    big = NS.Batch(ctx, gair, stark, claims * reps, proofs * reps)
+    small = NS.Batch(ctx, gair, stark, claims, proofs)
+    vb, okb = big.run()
+    vs, oks = small.run()
+    assert okb and oks and all(vb) and all(vs) and len(vb) >= 520
+    for i in range(len(pool)):
+        tb = big.transcript(len(pool) * (reps - 1) + i)
+        ts = small.transcript(i)
+        assert tb == ts and tb[2] == 0
+    big.close()
+    small.close()
