@@ -470,10 +470,10 @@ struct nhip_air {
     std::vector<uint32_t> prog_off;
     std::vector<Xfe> consts;
     uint32_t slots = 0;
-    // device copies, one per context that has used this AIR (a group drives several contexts
-    // from one process, possibly concurrently); created on first use, freed with the AIR
+    // device copies, one per GPU that has used this AIR (read-only, so every context on that GPU
+    // shares it; a group drives several contexts from one process, possibly concurrently);
+    // created on first use, freed with the AIR
     struct Dev {
-        nhip_ctx* ctx;
         int device;
         OodIns* d_prog;
         uint32_t* d_prog_off;
@@ -578,15 +578,16 @@ bool dims_from(const nhip_stark_params* sp, const nhip_air* air, Dims& D) {
     return true;
 }
 
-// This context's device copy of the compiled AIR (uploaded on first use).
+// The device copy of the compiled AIR on this context's GPU (uploaded on first use).
 int air_upload(nhip_ctx* ctx, nhip_air* a, nhip_air::Dev* out) {
     std::lock_guard<std::mutex> g(a->mu);
+    const int device = nhip_internal_device(ctx);
     for (const auto& d : a->devs)
-        if (d.ctx == ctx) {
+        if (d.device == device) {
             *out = d;
             return NHIP_OK;
         }
-    nhip_air::Dev d{ctx, nhip_internal_device(ctx), nullptr, nullptr, nullptr};
+    nhip_air::Dev d{device, nullptr, nullptr, nullptr};
     hipError_t e = hipMalloc(&d.d_prog, a->prog.size() * sizeof(OodIns) + 16);
     if (e == hipSuccess) e = hipMalloc(&d.d_prog_off, a->prog_off.size() * 4 + 4);
     if (e == hipSuccess) e = hipMalloc(&d.d_consts, a->consts.size() * sizeof(Xfe) + 24);
