@@ -31,7 +31,7 @@ import enum
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
-from .stark import Air, Claim, Stark, verify_batch as _gpu_verify_batch
+from .stark import Air, Claim, Group, Stark, verify_batch as _gpu_verify_batch, verify_batch_group
 
 MOCK_VALID = (0,)    # MockProofBehavior::ValidMock.encode()
 MOCK_INVALID = (1,)  # MockProofBehavior::InvalidMock.encode()
@@ -56,7 +56,8 @@ def is_invalid_mock(proof) -> bool:
 
 
 class Verifier:
-    """GPU-backed `verify` for one device: the AIR descriptor and Stark parameters are fixed."""
+    """GPU-backed `verify`: the AIR descriptor and Stark parameters are fixed.  `ctx` is one GPU's
+    Context, or a Group (every GPU of the node from one process: each batch is split over them)."""
 
     def __init__(self, ctx, air: Air, stark: Optional[Stark] = None):
         self.ctx, self.air = ctx, air
@@ -68,7 +69,11 @@ class Verifier:
     def verify_batch(self, pairs: Sequence[Tuple[Claim, object]], network: Network = Network.MAIN) -> List[bool]:
         if network.use_mock_proof():
             return [is_valid_mock(p) for _, p in pairs]
-        return _gpu_verify_batch(self.ctx, self.air, self.stark, list(pairs)) if pairs else []
+        if not pairs:
+            return []
+        if isinstance(self.ctx, Group):
+            return verify_batch_group(self.ctx, self.air, self.stark, list(pairs))[0]
+        return _gpu_verify_batch(self.ctx, self.air, self.stark, list(pairs))
 
 
 def _rev(d: Sequence[int]) -> List[int]:

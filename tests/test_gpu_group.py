@@ -69,3 +69,15 @@ def test_group_from_mask_covers_visible_devices():
     import neptune_hip.stark as NS
     with NS.Group(mask=0) as g:
         assert len(g) == torch.cuda.device_count()
+
+
+def test_verifier_mirror_over_a_group(ctx):
+    """verifier.rs-shaped mirror (`Verifier.verify_batch`, one call per ProofCollection /
+    mempool batch) backed by a group instead of one context: same verdicts."""
+    import neptune_hip.stark as NS
+    from neptune_hip.verifier import Verifier
+    air_w, pairs, expect = _batch(0x77, 2)
+    air = NS.Air([int(w) for w in air_w])
+    claims = [(NS.Claim(*c), p) for c, p in pairs]
+    with NS.Group([ctx.device, ctx.device]) as g:
+        assert Verifier(g, air).verify_batch(claims) == expect == Verifier(ctx, air).verify_batch(claims)
