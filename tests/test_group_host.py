@@ -32,3 +32,24 @@ def test_group_without_device_is_an_error():
         NS.Group([0, 0])
     with pytest.raises(L.NhipError):
         NS.Group(mask=0)
+
+
+def test_group_entry_points_reject_bad_arguments():
+    """C-ABI argument checks of the group entry points (host only): null outputs, zero members,
+    null arrays with n > 0 are NHIP_ERR_ARG; null handles are harmless."""
+    import ctypes
+    import neptune_hip._lib as L
+    lib = L.load()
+    member = (ctypes.c_uint32 * 1)()
+    assert lib.nhip_group_shard(None, 0, 1, None) == L.NHIP_OK
+    assert lib.nhip_group_shard(None, 1, 1, member) == L.NHIP_ERR_ARG
+    p = (L.Proof * 1)()
+    assert lib.nhip_group_shard(p, 1, 0, member) == L.NHIP_ERR_ARG
+    assert lib.nhip_group_shard(p, 1, 1, None) == L.NHIP_ERR_ARG
+    assert lib.nhip_group_create(None, 0, None) == L.NHIP_ERR_ARG
+    assert lib.nhip_group_init(0, None) == L.NHIP_ERR_ARG
+    assert lib.nhip_group_size(None) == 0
+    assert lib.nhip_group_member(None, 0) is None
+    lib.nhip_group_destroy(None)
+    v = np.zeros(1, dtype=np.uint8)
+    assert lib.nhip_group_verify_batch(None, None, None, None, None, 0, v, None) == L.NHIP_ERR_ARG
