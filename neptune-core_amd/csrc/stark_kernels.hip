@@ -875,9 +875,25 @@ __global__ void __launch_bounds__(256) k_fri(const uint64_t* __restrict__ words,
     }
     const Xfe snum = block_sum_xfe(num, red);
     const Xfe sden = block_sum_xfe(den, red);
+    // the last polynomial at t, in parallel instead of a one-lane Horner chain: lane c takes
+    // coef_c * t^c (t^c from the t^(2^j) table), then a block sum (field values: the order of
+    // the sum does not change the result)
+    __shared__ Xfe tpow[32];
+    const uint32_t pbits = d.last_poly_n ? 32 - __clz(d.last_poly_n) : 0;
     if (tid == 0) {
-        Xfe h = x_zero();
-        for (uint32_t c = d.last_poly_n; c-- > 0;) h = x_add(x_mul(h, t), ld_xfe_canon(words, d.last_poly_off + 3ull * c));
+        Xfe q = t;
+        for (uint32_t j = 0; j < pbits; ++j, q = x_mul(q, q)) tpow[j] = q;
+    }
+    __syncthreads();
+    Xfe hp = x_zero();
+    for (uint32_t c = tid; c < d.last_poly_n; c += blockDim.x) {
+        Xfe pw = x_one();
+        for (uint32_t j = 0; (c >> j) != 0; ++j)
+            if ((c >> j) & 1u) pw = x_mul(pw, tpow[j]);
+        hp = x_add(hp, x_mul(pw, ld_xfe_canon(words, d.last_poly_off + 3ull * c)));
+    }
+    const Xfe h = block_sum_xfe(hp, red);
+    if (tid == 0) {
         if (lflag || x_is_zero(sden)) f |= FAIL_ZERO_INVERSE;
         else if (!x_eq(h, x_mul(snum, x_inv(sden)))) f |= FAIL_FRI_EVAL;
         if (!d.last_poly_degree_ok) f |= FAIL_FRI_DEGREE;
