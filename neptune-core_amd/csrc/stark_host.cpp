@@ -698,7 +698,7 @@ int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
     const uint64_t M = w[1], A = w[2], K = w[3], NN = w[4];
     const uint64_t nc[4] = {w[5], w[6], w[7], w[8]};
     const uint64_t C = nc[0] + nc[1] + nc[2] + nc[3];
-    if (M > (1u << 20) || A > (1u << 20) || K < 3 || K > (1u << 20) || NN > (1u << 24) || C > (1u << 24)) return NHIP_ERR_ARG;
+    if (M > (1u << 20) || A > (1u << 20) || K < 16 || K > (1u << 20) || NN > (1u << 24) || C > (1u << 24)) return NHIP_ERR_ARG;
     if (n != 9 + 4 * NN + C) return NHIP_ERR_ARG;
     nhip_air* a = new (std::nothrow) nhip_air();
     if (!a) return NHIP_ERR_OOM;
@@ -717,7 +717,7 @@ int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
         bool ok = true;
         if (op == AIR_INPUT) {
             const uint64_t lim = x == IN_MAIN_CURR || x == IN_MAIN_NEXT ? M
-                                 : (x == IN_AUX_CURR || x == IN_AUX_NEXT ? A : (x == IN_CHALLENGE ? K + 3 : 0));
+                                 : (x == IN_AUX_CURR || x == IN_AUX_NEXT ? A : (x == IN_CHALLENGE ? K + 4 : 0));
             ok = x <= IN_CHALLENGE && y < lim;
             nd.a = (uint32_t)x;
             nd.b = (uint32_t)y;

@@ -667,6 +667,34 @@ __device__ Xfe block_sum_xfe(Xfe v, Xfe* sh) {
     return r;
 }
 
+// ------------------------------------------------------------------ Challenges::new
+// triton-air 1.0 ChallengeId indices of the sampled indeterminates the derived challenges use
+// (public design, unpinned; oracle/stark_ref.py derive_challenges)
+static constexpr uint32_t CH_COMPRESS_PROGRAM_DIGEST = 0, CH_STANDARD_INPUT = 1, CH_STANDARD_OUTPUT = 2,
+                          CH_LOOKUP_TABLE_PUBLIC = 15;
+
+__device__ __forceinline__ Xfe shfl_xor_xfe(Xfe v, int m) {
+    return {(uint64_t)__shfl_xor((long long)v.c0, m), (uint64_t)__shfl_xor((long long)v.c1, m),
+            (uint64_t)__shfl_xor((long long)v.c2, m)};
+}
+
+// EvalArg::compute_terminal(symbols[0..n), initial 1, c) on one full wave: lane j folds the chunk
+// [j ch, (j + 1) ch) by Horner, scales it by c^(n - chunk end), and the wave sums the chunks plus
+// c^n (the initial 1).  Same value as the sequential fold; n / 64 + ~2 log2 n products per lane.
+template <class Sym>
+__device__ Xfe eval_terminal_wave(uint32_t n, Xfe c, Sym sym) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t ch = (n + 63u) / 64u;
+    const uint32_t lo = min(n, lane * ch), hi = min(n, lo + ch);
+    Xfe h = x_zero();
+    for (uint32_t i = lo; i < hi; ++i) h = x_add(x_mul(h, c), x_lift(sym(i)));
+    Xfe t = hi > lo ? x_mul(h, x_pow(c, n - hi)) : x_zero();
+    if (lane == 0) t = x_add(t, x_pow(c, n));
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) t = x_add(t, shfl_xor_xfe(t, m));
+    return t;
+}
+
 // ------------------------------------------------------------------ OOD: AIR + quotient identity
 // One workgroup per proof.  The compiled AIR program (OodIns, stark.hpp) runs level by level:
 // OOD-row inputs are loaded into LDS slots, each ADD/SUB/MUL writes its value (XFE) to a reusable
@@ -683,7 +711,7 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Xfe* red = reinterpret_cast<Xfe*>(smem);              // 256
     Xfe* zinv = red + 256;                                 // 4
-    Xfe* chal_derived = zinv + 4;                          // 4 (3 used)
+    Xfe* chal_derived = zinv + 4;                          // 4 (Challenges::new)
     Xfe* misc = chal_derived + 4;                          // 4 (1 used: z - w^-1)
     uint32_t& zero_flag = *reinterpret_cast<uint32_t*>(misc + 4);
     Xfe* val = reinterpret_cast<Xfe*>(smem + AIR_LDS_HEADER);
@@ -713,21 +741,26 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
         const Xfe cons = x_sub(zph, x_one());
         if (x_is_zero(cons)) atomicOr(&zero_flag, 1u);
         zinv[1] = x_inv(cons);
-    } else if (tid == 192) {
-        // derived challenges: compressed program digest, input / output evaluation arguments
-        const Xfe c0 = ld_xfe_raw(xs, xb + 3ull * (sl.chal + 0));
-        const Xfe c1 = ld_xfe_raw(xs, xb + 3ull * (sl.chal + 1));
-        const Xfe c2 = ld_xfe_raw(xs, xb + 3ull * (sl.chal + 2));
-        Xfe comp = x_zero();
-        for (int q = 0; q < 5; ++q) comp = x_add(x_mul(comp, c0), x_lift(to_mont(words[d.claim_digest_off + q])));
-        Xfe ein = x_one();
-        for (uint32_t q = 0; q < d.claim_in_n; ++q) ein = x_add(x_mul(ein, c1), x_lift(to_mont(words[d.claim_in_off + q])));
-        Xfe eout = x_one();
-        for (uint32_t q = 0; q < d.claim_out_n; ++q)
-            eout = x_add(x_mul(eout, c2), x_lift(to_mont(words[d.claim_out_off + q])));
-        chal_derived[0] = comp;
-        chal_derived[1] = ein;
-        chal_derived[2] = eout;
+    } else if (tid >= 192) {
+        // Challenges::new: the 4 derived challenges in ChallengeId order, each an EvalArg terminal
+        // folded from 1 with its named sampled indeterminate (wave 3, lane-parallel)
+        auto chal = [&](uint32_t i) { return ld_xfe_raw(xs, xb + 3ull * (sl.chal + i)); };
+        const Xfe ein = eval_terminal_wave(d.claim_in_n, chal(CH_STANDARD_INPUT),
+                                           [&](uint32_t i) { return to_mont(words[d.claim_in_off + i]); });
+        const Xfe eout = eval_terminal_wave(d.claim_out_n, chal(CH_STANDARD_OUTPUT),
+                                            [&](uint32_t i) { return to_mont(words[d.claim_out_off + i]); });
+        const Xfe lut = eval_terminal_wave(256u, chal(CH_LOOKUP_TABLE_PUBLIC), [&](uint32_t i) {
+            const uint64_t y = i + 1;  // tip5::LOOKUP_TABLE[i] = (i + 1)^3 - 1 mod 257
+            return to_mont((y * y % 257u * y % 257u + 256u) % 257u);
+        });
+        const Xfe comp = eval_terminal_wave(5u, chal(CH_COMPRESS_PROGRAM_DIGEST),
+                                            [&](uint32_t i) { return to_mont(words[d.claim_digest_off + i]); });
+        if (tid == 192) {
+            chal_derived[0] = ein;
+            chal_derived[1] = eout;
+            chal_derived[2] = lut;
+            chal_derived[3] = comp;
+        }
     }
     __syncthreads();
     if (tid == 0) zinv[2] = x_mul(misc[0], zinv[1]);

@@ -351,7 +351,7 @@ static int verify_one(const params_t* pp, const air_t* air, const claim_t* cl, c
     uint64_t* w = malloc((len ? len : 1) * 8);
     stream_t* ps = calloc(1, sizeof(stream_t));
     xfe* vals = malloc(air->n_nodes * sizeof(xfe) + 8);
-    xfe* smp = malloc((air->num_sampled + 3 + air->n_cons + M + A + Q + 3 + 64) * sizeof(xfe));
+    xfe* smp = malloc((air->num_sampled + 4 + air->n_cons + M + A + Q + 3 + 64) * sizeof(xfe));
     uint64_t* dig = malloc(k * 5 * 8 + 8);
     uint64_t* cw_dig = NULL;
     if (!w || !ps || !vals || !smp || !dig) goto out;
@@ -390,19 +390,26 @@ static int verify_one(const params_t* pp, const air_t* air, const claim_t* cl, c
     if (!main_root) goto out;
     xfe* chal = smp;
     sp_sample_scalars(&ps->sp, air->num_sampled, chal);
-    if (air->num_sampled < 3) goto out;
-    {   /* derive_challenges */
-        xfe comp = X0, ein = X1, eout = X1;
-        for (int i = 0; i < 5; ++i) comp = xadd(xmul(comp, chal[0]), xlift(cl->digest[i] % P));
+    if (air->num_sampled < 16) goto out;
+    {   /* Challenges::new (stark_ref.derive_challenges): EvalArg terminals folded from 1 with the
+           named indeterminates (ChallengeId 0, 1, 2, 15), appended in ChallengeId order: input,
+           output, lookup-table public (over tip5::LOOKUP_TABLE), compressed program digest */
+        xfe ein = X1, eout = X1, lut = X1, comp = X1;
         for (size_t i = 0; i < cl->input_len; ++i) ein = xadd(xmul(ein, chal[1]), xlift(cl->input[i] % P));
         for (size_t i = 0; i < cl->output_len; ++i) eout = xadd(xmul(eout, chal[2]), xlift(cl->output[i] % P));
-        chal[air->num_sampled] = comp;
-        chal[air->num_sampled + 1] = ein;
-        chal[air->num_sampled + 2] = eout;
+        for (uint64_t x = 0; x < 256; ++x) {
+            const uint64_t y = x + 1;
+            lut = xadd(xmul(lut, chal[15]), xlift((y * y % 257u * y % 257u + 256u) % 257u));
+        }
+        for (int i = 0; i < 5; ++i) comp = xadd(xmul(comp, chal[0]), xlift(cl->digest[i] % P));
+        chal[air->num_sampled] = ein;
+        chal[air->num_sampled + 1] = eout;
+        chal[air->num_sampled + 2] = lut;
+        chal[air->num_sampled + 3] = comp;
     }
     const item_t* aux_root = dequeue(ps, MERKLE_ROOT);
     if (!aux_root) goto out;
-    xfe* quot_w = chal + air->num_sampled + 3;
+    xfe* quot_w = chal + air->num_sampled + 4;
     sp_sample_scalars(&ps->sp, air->n_cons, quot_w);
     const item_t* quot_root = dequeue(ps, MERKLE_ROOT);
     if (!quot_root) goto out;
@@ -441,7 +448,7 @@ static int verify_one(const params_t* pp, const air_t* air, const claim_t* cl, c
                 else if (kind == 1 && x < A) v = xld(ac->pay + 3 * x);
                 else if (kind == 2 && x < M) v = xld(mn->pay + 3 * x);
                 else if (kind == 3 && x < A) v = xld(an->pay + 3 * x);
-                else if (kind == 4 && x < air->num_sampled + 3) v = chal[x];
+                else if (kind == 4 && x < air->num_sampled + 4) v = chal[x];
                 else goto out;
                 break;
             }

@@ -361,7 +361,7 @@ class AirCircuit:
     """Straight-line XFE circuit over OOD row values and challenges.  nodes[i] = (op, a, b, c) with
     OP_INPUT: a = input kind, b = index;  OP_CONST: (a, b, c) = XFE;  ADD/SUB/MUL: node ids a, b.
     constraints: node ids grouped by type in triton order (initial, consistency, transition,
-    terminal).  num_sampled challenges are squeezed; 3 more are derived from the claim."""
+    terminal).  num_sampled challenges are squeezed; 4 more are derived (derive_challenges)."""
 
     def __init__(self, num_main, num_aux, num_sampled, nodes, constraints_by_type):
         self.num_main, self.num_aux, self.num_sampled = num_main, num_aux, num_sampled
@@ -374,7 +374,7 @@ class AirCircuit:
 
     @property
     def num_challenges(self):
-        return self.num_sampled + 3
+        return self.num_sampled + NUM_DERIVED_CHALLENGES
 
     @classmethod
     def from_words(cls, w: Sequence[int]) -> "AirCircuit":
@@ -420,21 +420,40 @@ class AirCircuit:
         return [[vals[i] for i in cs] for cs in self.constraints]
 
 
+# triton-air 1.0 `ChallengeId` (public design; unpinned offline): the sampled indeterminates that
+# Challenges::new reads, and the derived challenges it appends after the SAMPLE_COUNT = 59 sampled
+# ones, in ChallengeId order (StandardInputTerminal, StandardOutputTerminal,
+# LookupTablePublicTerminal, CompressedProgramDigest).
+CH_COMPRESS_PROGRAM_DIGEST_INDETERMINATE = 0
+CH_STANDARD_INPUT_INDETERMINATE = 1
+CH_STANDARD_OUTPUT_INDETERMINATE = 2
+CH_LOOKUP_TABLE_PUBLIC_INDETERMINATE = 15
+NUM_DERIVED_CHALLENGES = 4
+CHALLENGE_SAMPLE_COUNT = 59
+
+
+def eval_arg_terminal(symbols, challenge, initial=X_ONE):
+    """EvalArg::compute_terminal: fold running -> challenge * running + symbol, from
+    EvalArg::default_initial() = 1."""
+    acc = initial
+    for s in symbols:
+        acc = xadd(xmul(acc, challenge), lift(int(s) % P))
+    return acc
+
+
 def derive_challenges(sampled, claim) -> List[Tuple[int, int, int]]:
-    """Challenges::new(sampled, claim): sampled ++ [compressed program digest, input evaluation
-    argument, output evaluation argument] (triton-style derivation; exact formulas unpinned)."""
+    """Challenges::new(sampled, claim) (triton-vm 1.0 public design, unpinned): sampled ++
+    [input terminal, output terminal, lookup-table public terminal, compressed program digest],
+    each an evaluation argument folded from 1 with its named indeterminate; the lookup terminal runs
+    over twenty-first's tip5::LOOKUP_TABLE."""
+    if len(sampled) <= CH_LOOKUP_TABLE_PUBLIC_INDETERMINATE:
+        raise VerifyError("too few sampled challenges")
     digest, _version, inp, out = claim
-    ch0, ch1, ch2 = sampled[0], sampled[1], sampled[2]
-    comp = X_ZERO
-    for d in digest:
-        comp = xadd(xmul(comp, ch0), lift(d))
-    ein = X_ONE
-    for x in inp:
-        ein = xadd(xmul(ein, ch1), lift(x))
-    eout = X_ONE
-    for x in out:
-        eout = xadd(xmul(eout, ch2), lift(x))
-    return list(sampled) + [comp, ein, eout]
+    ein = eval_arg_terminal(inp, sampled[CH_STANDARD_INPUT_INDETERMINATE])
+    eout = eval_arg_terminal(out, sampled[CH_STANDARD_OUTPUT_INDETERMINATE])
+    lut = eval_arg_terminal(T.LOOKUP_TABLE, sampled[CH_LOOKUP_TABLE_PUBLIC_INDETERMINATE])
+    comp = eval_arg_terminal(digest, sampled[CH_COMPRESS_PROGRAM_DIGEST_INDETERMINATE])
+    return list(sampled) + [ein, eout, lut, comp]
 
 
 class _SplitMix:
@@ -467,7 +486,7 @@ class SynthRecipe:
         self.combos: List[dict] = []         # combination constraints
 
 
-def synth_air(params: StarkParams, num_sampled: int = 63, seed: int = 0x5EED, num_constraints: Optional[int] = None):
+def synth_air(params: StarkParams, num_sampled: int = CHALLENGE_SAMPLE_COUNT, seed: int = 0x5EED, num_constraints: Optional[int] = None):
     """Deterministic synthetic AIR with params' column counts (see module doc)."""
     rng = _SplitMix(seed)
     M, A = params.num_main, params.num_aux
@@ -529,12 +548,14 @@ def synth_air(params: StarkParams, num_sampled: int = 63, seed: int = 0x5EED, nu
                                    lin_coef=lin_coef, node=nid))
         base_by_type[ctype].append(len(recipe.targets) - 1)
         main_targets.append(t)
-    # aux targets: challenge-weighted products; the last 3 bind the claim through derived challenges
+    # aux targets: challenge-weighted products; the last 4 bind the claim (and the lookup table)
+    # through the derived challenges
     aux_targets: List[int] = []
+    nd = NUM_DERIVED_CHALLENGES
     for j in range(A):
-        if j >= A - 3:
+        if j >= A - nd:
             ctype = C_TERM
-            factors = [(INPUT_CHALLENGE, num_sampled + (j - (A - 3)))]
+            factors = [(INPUT_CHALLENGE, num_sampled + (j - (A - nd)))]
             coef = X_ONE
             lin, lin_coef = None, X_ZERO
         else:

@@ -95,7 +95,7 @@ def test_air_descriptor_validation():
     import neptune_hip.stark as NS
     from neptune_hip import NhipError
     params = S.StarkParams(num_main=24, num_aux=9, num_collinearity_checks=8)
-    air, _ = S.synth_air(params, num_sampled=8, seed=7)
+    air, _ = S.synth_air(params, num_sampled=16, seed=7)
     w = air.to_words()
     NS.Air(w)
     bad = list(w)
