@@ -530,7 +530,7 @@ def main():
         # wall time, against the VALU peak
         "tip5_valu_frac": perms_job * K / elapsed * TIP5_VALU_OPS_PER_PERM / (VALU_PEAK_LANE_OPS * world),
         # per sub-batch (each sub-batch's phases are timed by HIP events on its own two streams)
-        "phase_ms": {k[3:]: round(avg[k] / P, 4) for k in ("ms_fiat_shamir", "ms_row_hash", "ms_merkle",
+        "phase_ms": {k[3:]: round(avg[k] / P, 4) for k in ("ms_device_decode", "ms_fiat_shamir", "ms_row_hash", "ms_merkle",
                                                             "ms_merkle_hash", "ms_ood_air", "ms_fri", "ms_deep",
                                                             "ms_device_total")},
         "host_prepare_ms": {"decode": sum(x["ms_decode"] for x in st0), "upload": sum(x["ms_upload"] for x in st0),

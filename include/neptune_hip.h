@@ -135,7 +135,7 @@ typedef struct {
     uint64_t num_proofs, proof_words;
     uint64_t tip5_perms_static;  /* Fiat-Shamir + row hashing (from the proof shapes) */
     uint64_t tip5_perms_merkle;  /* authentication-structure hash_pairs performed (device-counted) + last-codeword trees */
-    double ms_decode, ms_upload;  /* host */
+    double ms_decode, ms_upload;  /* host: layout + staging copy (+ DMA issue), then the wait for the uploads */
     double ms_fiat_shamir, ms_row_hash, ms_merkle, ms_ood_air, ms_fri, ms_deep, ms_device_total; /* device */
     double ms_merkle_hash;          /* the per-level hash_pair launches inside ms_merkle */
     uint64_t merkle_hash_launches;  /* number of those launches (one per tree level) */
@@ -143,6 +143,7 @@ typedef struct {
      * run k_mp_hash_wide): summed kernel time, launch count, permutations they performed */
     double ms_mp_hash_kernel;
     uint64_t mp_hash_kernel_launches, mp_hash_kernel_perms;
+    double ms_device_decode;        /* k_decode: the proof-stream walk on the device (every run) */
 } nhip_stats;
 
 typedef struct nhip_air nhip_air;
@@ -155,11 +156,19 @@ int nhip_air_info(const nhip_air *air, uint32_t *num_nodes, uint32_t *num_levels
 /* Host-only structural decode (no GPU needed): 1 = decodes, 0 = malformed, < 0 = bad argument. */
 int nhip_proof_decodes(const nhip_air *air, const nhip_stark_params *params, const nhip_claim *claim,
                        const nhip_proof *proof);
-/* One-shot: decode, upload, verify, verdicts[n]. */
+/* Pinned host memory for proofs: proofs whose words lie in a range from nhip_host_alloc or
+ * nhip_host_register are DMA'd straight from it (no staging copy); adjacent proofs of one range
+ * go as one copy.  Any other host memory works too, through the context's pinned staging. */
+int nhip_host_alloc(size_t bytes, void **out);
+int nhip_host_free(void *p);
+int nhip_host_register(void *p, size_t bytes);
+int nhip_host_unregister(void *p);
+/* One-shot: upload, decode (on the device), verify, verdicts[n]. */
 int nhip_verify_batch(nhip_ctx *ctx, nhip_air *air, const nhip_stark_params *params, const nhip_claim *claims,
                       const nhip_proof *proofs, size_t n, uint8_t *verdicts, nhip_stats *stats);
-/* Device-resident form: prepare (host decode + one upload), run (device phases only) any number
- * of times, read stats / the Fiat-Shamir transcript of one proof, destroy. */
+/* Device-resident form: prepare (stage + one upload of the raw proof words), run (every device
+ * phase, starting with the proof-stream decode) any number of times, read stats / the
+ * Fiat-Shamir transcript of one proof, destroy. */
 int nhip_batch_prepare(nhip_ctx *ctx, nhip_air *air, const nhip_stark_params *params, const nhip_claim *claims,
                        const nhip_proof *proofs, size_t n, nhip_batch **out);
 /* Refill an idle batch in place with new proofs (same semantics as prepare; its streams,

@@ -132,13 +132,18 @@ int nhip_group_verify_batch(nhip_group* g, nhip_air* air, const nhip_stark_param
         };
         // one host thread per busy member (member 0 on the calling thread); a thread that cannot be
         // started runs its shard on the calling thread afterwards
+        // (both vectors are reserved up front: no allocation, hence no throw, once a thread runs)
         std::vector<std::thread> threads;
         std::vector<size_t> inline_members;
+        threads.reserve(M);
+        inline_members.reserve(M);
         for (size_t m = 1; m < M; ++m) {
             if (idx[m].empty()) continue;
             try {
                 threads.emplace_back(run, m);
             } catch (const std::system_error&) {
+                inline_members.push_back(m);
+            } catch (const std::bad_alloc&) {
                 inline_members.push_back(m);
             }
         }

@@ -4,6 +4,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "proof_codec.hpp"
 #include "stark.hpp"
 #include "xfe.hpp"
 
@@ -54,12 +55,28 @@ struct MpPlan {
     uint32_t levels;
 };
 
+// One proof of a batch as staged for k_decode: its raw words and its staged claim encoding in the
+// batch word buffer, and the padded height the host sized the batch's scratch with (from the
+// proof header; SHAPE_NONE = malformed header).
+struct ProofIn {
+    uint64_t off, len;
+    uint64_t claim_off;
+    uint32_t claim_in_n, claim_out_n;
+    uint32_t sized_log2_ph, pad;
+};
+
+// device counters of a run (zeroed per run, read back with the verdicts)
+enum : uint32_t { CNT_MP_SKIPPED = 0, CNT_PERMS_STATIC = 1, CNT_PERMS_LCW = 2, CNT_N = 4 };
+
 struct StarkBatchDev {
     uint32_t n_proofs, max_R;
     StarkDims dims;
+    Dims D;
+    uint32_t fs_stride, xs_stride;  // per-proof Fiat-Shamir program slots / sample areas (k_decode)
+    const ProofIn* in;
     const uint64_t* words;
-    const ProofDesc* desc;
-    const FsOp* ops;
+    ProofDesc* desc;
+    FsOp* ops;
     uint64_t* xs;
     uint32_t* idx;
     uint64_t* dig;
@@ -67,10 +84,10 @@ struct StarkBatchDev {
     uint64_t* xdom;        // [n_proofs][k] round-0 FRI domain point of each check (raw), k_fri -> k_deep
     uint64_t* lcw;         // [n_proofs][max_lcw][5] last-codeword Merkle tree nodes (heap order)
     uint32_t max_lcw;      // max last-codeword length (power of two)
-    uint32_t* fail;
-    const uint32_t* fail_init;  // decode-time failure bits (FAIL_DECODE), constant across runs
+    uint32_t* fail;                    // set by k_decode (FAIL_DECODE or 0), then ORed by every check
     uint8_t* verdicts;
-    unsigned long long* perm_counter;  // multiproof hash ops skipped (trees whose authentication structure failed)
+    unsigned long long* counters;      // CNT_*: multiproof ops skipped (trees whose authentication
+                                       // structure failed), decoded permutation counts
     MpPlan mp;
     const uint64_t* mp_cap_host;  // host: op capacity per level (launch sizes)
     const OodIns* air_prog;        // compiled AIR (OodIns per level)
@@ -81,9 +98,9 @@ struct StarkBatchDev {
     size_t air_lds_bytes;
 };
 
-// events: 0 start | fs | rows | mp plan | mp hash levels | mp roots | ood | fri | deep | 9 verdicts
-// 10: main stream at the aux-chain release point, 11: aux stream after that wait
-static constexpr int STARK_EVENTS = 12;
+// events: 0 start (after k_decode) | fs | rows | mp plan | mp hash levels | mp roots | ood | fri | deep | 9 verdicts
+// 10: main stream at the aux-chain release point, 11: aux stream after that wait, 12: before k_decode
+static constexpr int STARK_EVENTS = 13;
 struct StarkPhaseTimer {
     hipEvent_t ev[STARK_EVENTS];
     uint32_t mp_hash_launches;

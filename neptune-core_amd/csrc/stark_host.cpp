@@ -32,429 +32,64 @@ using namespace nhip;
 namespace {
 
 constexpr uint64_t P = GL_P;
-constexpr size_t OUT_HDR = 16;  // pinned readback: [skipped ops u64 | pad | plan counters | verdicts]
+constexpr size_t OUT_HDR = CNT_N * 8;  // pinned readback: [device counters | plan counters | verdicts]
 // hash levels launched before the OOD / FRI / DEEP chain is released (NHIP_AUX_AFTER_LEVEL
 // overrides); tuned on MI355X
 constexpr uint32_t AUX_AFTER_LEVEL_DEFAULT = 0;
 
-enum ItemKind : uint32_t {
-    MERKLE_ROOT = 0, OOD_MAIN_ROW, OOD_AUX_ROW, OOD_QUOT_SEGMENTS, AUTH_STRUCTURE, MAIN_ROWS, AUX_ROWS,
-    LOG2_PADDED_HEIGHT, QUOT_SEGMENTS_ELEMENTS, FRI_CODEWORD, FRI_POLYNOMIAL, FRI_RESPONSE, N_KINDS
-};
-
-struct Item {
-    uint32_t kind;
-    uint64_t lo, hi;        // item words [lo, hi) (starting at the discriminant), absolute
-    uint64_t payload;       // first payload element (after counts)
-    uint64_t n;             // element count (dynamic kinds) / value (Log2PaddedHeight)
-    // FRI response only
-    uint64_t leaves_off, leaves_n, auth_off, auth_n;
-};
-
-inline uint32_t log2u(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
-
-struct Dims {
-    StarkDims d;
-    uint32_t expansion;
-};
-
-uint32_t fri_num_rounds(const Dims& D, uint64_t fri_len) {
-    const uint64_t dim = fri_len / D.expansion;
-    const uint32_t max_rounds = dim > 1 ? 64u - (uint32_t)__builtin_clzll(dim - 1) : 0u;
-    const uint32_t all = log2u(D.d.num_checks);
-    return max_rounds > all + 1 ? max_rounds - (all + 1) : 0u;
-}
-
-// Decode one ProofItem occupying words[lo, hi).  Returns false on any malformation.
-bool decode_item(const uint64_t* w, uint64_t lo, uint64_t hi, const Dims& D, Item& it) {
-    if (lo >= hi) return false;
-    it = Item{};
-    it.kind = (uint32_t)(w[lo] < N_KINDS ? w[lo] : N_KINDS);
-    it.lo = lo;
-    it.hi = hi;
-    const uint64_t len = hi - lo;
-    const StarkDims& d = D.d;
-    switch (it.kind) {
-        case MERKLE_ROOT: it.payload = lo + 1; return len == 1 + 5;
-        case OOD_MAIN_ROW: it.payload = lo + 1; return len == 1 + 3ull * d.num_main;
-        case OOD_AUX_ROW: it.payload = lo + 1; return len == 1 + 3ull * d.num_aux;
-        case OOD_QUOT_SEGMENTS: it.payload = lo + 1; return len == 1 + 3ull * d.num_quot_seg;
-        case LOG2_PADDED_HEIGHT:
-            if (len != 2) return false;
-            it.n = w[lo + 1];
-            return it.n < (1ull << 32);
-        case N_KINDS: return false;
-        default: break;
-    }
-    // dynamically sized payload: [kind, blen, body(blen)]
-    if (len < 2) return false;
-    const uint64_t blen = w[lo + 1];
-    if (blen != len - 2) return false;
-    const uint64_t b0 = lo + 2;
-    if (it.kind == FRI_RESPONSE) {
-        // FriResponse { auth_structure, revealed_leaves } encoded fields-reversed:
-        // [len(rl), n_leaves, leaves.., len(au), n_auth, digests..]
-        if (blen < 1) return false;
-        const uint64_t lrl = w[b0];
-        if (lrl < 1 || 1 + lrl > blen) return false;
-        const uint64_t nl = w[b0 + 1];
-        if (nl > (lrl - 1) / 3 || 3 * nl != lrl - 1) return false;
-        it.leaves_off = b0 + 2;
-        it.leaves_n = nl;
-        const uint64_t pa = b0 + 1 + lrl;
-        if (pa >= b0 + blen) return false;
-        const uint64_t lau = w[pa];
-        if (lau < 1 || 1 + lrl + 1 + lau != blen) return false;
-        const uint64_t na = w[pa + 1];
-        if (na > (lau - 1) / 5 || 5 * na != lau - 1) return false;
-        it.auth_off = pa + 2;
-        it.auth_n = na;
-        return true;
-    }
-    uint64_t width = 0;
-    switch (it.kind) {
-        case AUTH_STRUCTURE: width = 5; break;
-        case MAIN_ROWS: width = d.num_main; break;
-        case AUX_ROWS: width = 3ull * d.num_aux; break;
-        case QUOT_SEGMENTS_ELEMENTS: width = 3ull * d.num_quot_seg; break;
-        case FRI_CODEWORD: width = 3; break;
-        case FRI_POLYNOMIAL: width = 3; break;
-        default: return false;
-    }
-    if (blen < 1) return false;
-    const uint64_t n = w[b0];
-    if (width == 0 || n > (blen - 1) / width || n * width != blen - 1) return false;
-    it.n = n;
-    it.payload = b0 + 1;
-    return true;
-}
-
+// What the host knows of a batch: its layout in the device word buffer and the scratch sizes,
+// from the proof lengths and the padded height each proof header declares.  Everything else (the
+// proof-stream walk, descriptors, Fiat-Shamir programs, decode failures) is k_decode's, every run.
 struct HostBatch {
-    Dims D;
-    std::vector<ProofDesc> desc;
-    std::vector<FsOp> ops;
-    std::vector<uint32_t> fail;
-    uint64_t words_total = 0;  // proof words + staged claim encodings, uploaded to dev.words
-    uint64_t xs_total = 0, idx_total = 0;
-    uint32_t max_R = 0, max_last_cw = 1;
-    uint64_t perms_static = 0;  // FS + row hashing (multiproof Merkle hashes are counted on device)
-    uint64_t perms_lcw = 0;     // last-codeword Merkle trees (hashed with the multiproof levels)
-    uint64_t proof_words = 0;
+    Dims D{};
+    uint32_t n = 0;
+    uint64_t proof_words = 0;   // proof region [0, proof_words) of the word buffer
+    uint64_t words_total = 0;   // + the staged claim encodings
+    uint32_t max_R = 0, max_last_cw = 1, levels = 0;
+    uint32_t fs_stride = 0, xs_stride = 0;
+    uint64_t perms_static = 0, perms_lcw = 0;  // device-counted, per run
 };
 
-uint64_t absorb_perms(uint64_t len) { return len / 10 + 1; }
+uint64_t claim_words(const nhip_claim& c) { return (uint64_t)c.output_len + c.input_len + 10; }
 
-// words one proof occupies in the batch buffer: the proof, then its staged claim encoding
-uint64_t staged_words(const nhip_claim& claim, const nhip_proof& proof) {
-    return proof.len + claim.output_len + claim.input_len + 10;
+// The claim's BFieldCodec encoding (pinned layout, new_claim.rs:38-100):
+// [out_n + 1, out_n, out.., in_n + 1, in_n, in.., version, digest(5)]
+void encode_claim(const nhip_claim& claim, uint64_t* c) {
+    *c++ = claim.output_len + 1;
+    *c++ = claim.output_len;
+    for (size_t i = 0; i < claim.output_len; ++i) *c++ = claim.output[i] % P;
+    *c++ = claim.input_len + 1;
+    *c++ = claim.input_len;
+    for (size_t i = 0; i < claim.input_len; ++i) *c++ = claim.input[i] % P;
+    *c++ = claim.version;
+    for (int i = 0; i < 5; ++i) *c++ = claim.program_digest[i] % P;
 }
 
-// What decoding one proof produces; merged into the HostBatch in proof order.
-struct ProofOut {
-    ProofDesc pd{};
-    std::vector<FsOp> ops;  // this proof's Fiat-Shamir program (absolute word offsets)
-    uint32_t fail = 0;
-    uint64_t perms = 0, perms_lcw = 0;
-};
-
-// Stage proof p at words[base, base + staged_words) (canonical: BFieldElement::new reduces) and
-// decode it into its descriptor; on malformation mark FAIL_DECODE and leave a benign desc.
-// Independent per proof: nhip_batch_prepare runs it on several host threads.
-void decode_proof(const Dims& D, const nhip_claim& claim, const nhip_proof& proof, uint64_t* words,
-                  uint64_t base, ProofOut& out) {
-    const StarkDims& d = D.d;
-    ProofDesc pd{};
-    uint32_t fail = 0;
-    const uint64_t len = proof.len;
-    {
-        uint64_t* dst = words + base;
-        const uint64_t* src = proof.words;
-        for (uint64_t i = 0; i < len; ++i) {
-            const uint64_t v = src[i];
-            dst[i] = v >= P ? v - P : v;
-        }
-    }
-    // stage the claim encoding (pinned layout): [out_n+1, out_n, out.., in_n+1, in_n, in.., version, digest]
-    const uint64_t cbase = base + len;
-    {
-        uint64_t* c = words + cbase;
-        *c++ = claim.output_len + 1;
-        *c++ = claim.output_len;
-        for (size_t i = 0; i < claim.output_len; ++i) *c++ = claim.output[i] % P;
-        *c++ = claim.input_len + 1;
-        *c++ = claim.input_len;
-        for (size_t i = 0; i < claim.input_len; ++i) *c++ = claim.input[i] % P;
-        *c++ = claim.version;
-        for (int i = 0; i < 5; ++i) *c++ = claim.program_digest[i] % P;
-    }
-    const uint64_t clen = claim.output_len + claim.input_len + 10;
-    pd.claim_out_off = cbase + 2;
-    pd.claim_out_n = (uint32_t)claim.output_len;
-    pd.claim_in_off = cbase + 2 + claim.output_len + 2;
-    pd.claim_in_n = (uint32_t)claim.input_len;
-    pd.claim_digest_off = cbase + clen - 5;
-
-    const uint64_t* w = words;
-    std::vector<Item> items;
-    bool ok = len >= 2 && w[base] == len - 1;
-    if (ok) {
-        const uint64_t n_items = w[base + 1];
-        uint64_t pos = base + 2;
-        const uint64_t end = base + len;
-        for (uint64_t i = 0; ok && i < n_items; ++i) {
-            if (pos >= end) { ok = false; break; }
-            const uint64_t ln = w[pos++];
-            if (ln > end - pos) { ok = false; break; }
-            Item it;
-            ok = decode_item(w, pos, pos + ln, D, it);
-            items.push_back(it);
-            pos += ln;
-        }
-        ok = ok && pos == end;
-    }
-    // dequeue order of Stark::verify
-    uint32_t R = 0;
-    if (ok) {
-        size_t q = 0;
-        auto take = [&](uint32_t kind) -> const Item* {
-            if (!ok || q >= items.size() || items[q].kind != kind) { ok = false; return nullptr; }
-            return &items[q++];
-        };
-        const Item* lph = take(LOG2_PADDED_HEIGHT);
-        if (ok && lph->n > LOG2_PH_MAX) ok = false;
-        uint32_t log2_ph = 0, log2_T = 0, log2_N = 0;
-        if (ok) {
-            log2_ph = (uint32_t)lph->n;
-            const uint64_t ph = 1ull << log2_ph;
-            const uint64_t need = ph + d.num_trace_randomizers;
-            uint64_t T = 1;
-            while (T < need) T <<= 1;
-            log2_T = log2u(T);
-            log2_N = log2_T + d.log2_expansion;
-            R = fri_num_rounds(D, 1ull << log2_N);
-            if (R > MAX_FRI_ROUNDS || log2_N > 32) ok = false;
-        }
-        const Item* mr = take(MERKLE_ROOT);
-        const Item* ar = take(MERKLE_ROOT);
-        const Item* qr = take(MERKLE_ROOT);
-        const Item* mc = take(OOD_MAIN_ROW);
-        const Item* ac = take(OOD_AUX_ROW);
-        const Item* mn = take(OOD_MAIN_ROW);
-        const Item* an = take(OOD_AUX_ROW);
-        const Item* qs = take(OOD_QUOT_SEGMENTS);
-        const Item* fr[MAX_FRI_ROUNDS + 1] = {};
-        for (uint32_t r = 0; ok && r <= R; ++r) fr[r] = take(MERKLE_ROOT);
-        const Item* cw = take(FRI_CODEWORD);
-        const Item* poly = take(FRI_POLYNOMIAL);
-        const Item* resp[MAX_FRI_ROUNDS + 1] = {};
-        for (uint32_t r = 0; ok && r <= R; ++r) resp[r] = take(FRI_RESPONSE);
-        const Item* mrows = take(MAIN_ROWS);
-        const Item* mauth = take(AUTH_STRUCTURE);
-        const Item* arows = take(AUX_ROWS);
-        const Item* aauth = take(AUTH_STRUCTURE);
-        const Item* qrows = take(QUOT_SEGMENTS_ELEMENTS);
-        const Item* qauth = take(AUTH_STRUCTURE);
-        if (ok && q != items.size()) ok = false;  // items left
-        const uint32_t k = d.num_checks;
-        if (ok) {
-            for (uint32_t r = 0; r <= R; ++r)
-                if (resp[r]->leaves_n != k) ok = false;
-            if (mrows->n != k || arows->n != k || qrows->n != k) ok = false;
-            if (cw->n != (1ull << (log2_N - R))) ok = false;
-        }
-        if (ok) {
-            pd.log2_ph = log2_ph;
-            pd.log2_T = log2_T;
-            pd.log2_N = log2_N;
-            pd.R = R;
-            pd.main_root = mr->payload;
-            pd.aux_root = ar->payload;
-            pd.quot_root = qr->payload;
-            pd.ood_mc = mc->payload;
-            pd.ood_ac = ac->payload;
-            pd.ood_mn = mn->payload;
-            pd.ood_an = an->payload;
-            pd.ood_qs = qs->payload;
-            for (uint32_t r = 0; r <= R; ++r) {
-                pd.fri_root[r] = fr[r]->payload;
-                pd.fri[r].auth_off = resp[r]->auth_off;
-                pd.fri[r].auth_n = (uint32_t)resp[r]->auth_n;
-                pd.fri[r].leaves_off = resp[r]->leaves_off;
-                pd.fri[r].leaves_n = (uint32_t)resp[r]->leaves_n;
-            }
-            pd.last_cw_off = cw->payload;
-            pd.last_cw_n = (uint32_t)cw->n;
-            pd.last_poly_off = poly->payload;
-            pd.last_poly_n = (uint32_t)poly->n;
-            // degree of the last polynomial (highest non-zero coefficient) vs the FRI bound
-            int64_t deg = -1;
-            for (uint64_t c = 0; c < poly->n; ++c) {
-                const uint64_t* x = w + poly->payload + 3 * c;
-                if (x[0] | x[1] | x[2]) deg = (int64_t)c;
-            }
-            const uint64_t first_max = (1ull << log2_N) / D.expansion - 1;
-            const uint64_t last_max = first_max >> R;
-            pd.last_poly_degree_ok = deg <= (int64_t)last_max ? 1u : 0u;
-            pd.main_rows_off = mrows->payload;
-            pd.aux_rows_off = arows->payload;
-            pd.quot_rows_off = qrows->payload;
-            pd.main_auth_off = mauth->payload;
-            pd.main_auth_n = (uint32_t)mauth->n;
-            pd.aux_auth_off = aauth->payload;
-            pd.aux_auth_n = (uint32_t)aauth->n;
-            pd.quot_auth_off = qauth->payload;
-            pd.quot_auth_n = (uint32_t)qauth->n;
-            pd.rows_n = k;
-            // Fiat-Shamir program (order of Stark::verify + Fri::verify)
-            std::vector<FsOp>& ops = out.ops;
-            uint64_t perms = 0;
-            auto absorb = [&](uint64_t off, uint64_t n) {
-                ops.push_back(FsOp{FS_ABSORB, (uint32_t)n, off});
-                perms += absorb_perms(n);
-            };
-            auto squeeze = [&](uint32_t n) {
-                ops.push_back(FsOp{FS_SQUEEZE_X, n, 0});
-                perms += (3ull * n + 9) / 10;
-            };
-            auto absorb_item = [&](const Item* it) { absorb(it->lo, it->hi - it->lo); };
-            absorb(cbase, clen);
-            absorb_item(mr);
-            squeeze(d.num_sampled);
-            absorb_item(ar);
-            squeeze(d.num_constraints);
-            absorb_item(qr);
-            squeeze(1);
-            absorb_item(mc);
-            absorb_item(ac);
-            absorb_item(mn);
-            absorb_item(an);
-            absorb_item(qs);
-            squeeze(d.num_main + d.num_aux + d.num_quot_seg + d.num_deep);
-            for (uint32_t r = 0; r <= R; ++r) {
-                absorb_item(fr[r]);
-                if (r < R) squeeze(1);
-            }
-            ops.push_back(FsOp{FS_SAMPLE_IDX, k, 1ull << log2_N});
-            perms += (k + 9) / 10;
-            squeeze(1);
-            pd.fs_op_n = (uint32_t)ops.size();
-            // rows + last codeword tree
-            perms += (uint64_t)k * (absorb_perms(d.num_main) + absorb_perms(3ull * d.num_aux) +
-                                    absorb_perms(3ull * d.num_quot_seg));
-            out.perms = perms;
-            out.perms_lcw = cw->n - 1;  // last-codeword tree, hashed by k_mp_hash
-        }
-    }
-    if (!ok) {
-        fail |= FAIL_DECODE;
-        pd = ProofDesc{};
-        pd.claim_out_off = cbase + 2;
-        pd.claim_in_off = cbase + 2 + claim.output_len + 2;
-        pd.claim_digest_off = cbase + clen - 5;
-        out.ops.clear();
-        out.perms = out.perms_lcw = 0;
-    }
-    out.pd = pd;
-    out.fail = fail;
-}
-
-// Append one decoded proof to the batch (serial, in proof order): global Fiat-Shamir program
-// offsets, sample / index areas, batch maxima and permutation counts.
-void merge_proof(HostBatch& B, ProofOut& o, uint64_t proof_len) {
-    ProofDesc pd = o.pd;
-    pd.fs_op_off = (uint32_t)B.ops.size();
-    B.ops.insert(B.ops.end(), o.ops.begin(), o.ops.end());
-    const SampleLayout sl = SampleLayout::of(B.D.d, pd.R);
-    pd.xs_off = B.xs_total;
-    pd.n_xs = sl.total;
-    B.xs_total += sl.total;
-    pd.idx_off = B.idx_total;
-    B.idx_total += B.D.d.num_checks;
-    if (pd.R > B.max_R) B.max_R = pd.R;
-    if (pd.last_cw_n > B.max_last_cw) B.max_last_cw = pd.last_cw_n;
-    B.perms_static += o.perms;
-    B.perms_lcw += o.perms_lcw;
-    B.proof_words += proof_len;
-    B.desc.push_back(pd);
-    B.fail.push_back(o.fail);
-}
-
-// Host threads for decoding (NHIP_HOST_THREADS overrides; at most 16, the GPU box's CPU share).
-unsigned host_threads(size_t n) {
+// Host threads for staging copies (NHIP_HOST_THREADS overrides; at most 16, the GPU box's CPU
+// share).
+unsigned host_threads(uint64_t bytes) {
     unsigned t = std::thread::hardware_concurrency();
     if (const char* e = std::getenv("NHIP_HOST_THREADS")) t = (unsigned)std::strtoul(e, nullptr, 10);
     t = std::max(1u, std::min(t, 16u));
-    return n < 32 ? 1u : std::min<unsigned>(t, (unsigned)(n / 8));
+    return bytes < (8ull << 20) ? 1u : t;
 }
 
-// Decode proofs [0, n) into words (staged at bases[i]) on up to `threads` threads.
-void decode_all(const Dims& D, const nhip_claim* claims, const nhip_proof* proofs, size_t n, uint64_t* words,
-                const std::vector<uint64_t>& bases, std::vector<ProofOut>& outs, unsigned threads) {
-    std::atomic<size_t> next{0};
-    auto work = [&]() {
-        constexpr size_t CHUNK = 4;
-        for (size_t a; (a = next.fetch_add(CHUNK)) < n;)
-            for (size_t i = a; i < std::min(n, a + CHUNK); ++i)
-                decode_proof(D, claims[i], proofs[i], words, bases[i], outs[i]);
-    };
-    if (threads <= 1) {
-        work();
-        return;
+// Pinned host ranges handed out by nhip_host_alloc / registered by nhip_host_register: proofs that
+// live in one are DMA'd to the device straight from the caller's memory (no staging copy).
+struct PinnedRanges {
+    std::mutex mu;
+    std::vector<std::pair<uintptr_t, size_t>> r;  // (start, bytes)
+    bool contains(const void* p, size_t bytes) {
+        const uintptr_t a = (uintptr_t)p;
+        std::lock_guard<std::mutex> g(mu);
+        for (const auto& x : r)
+            if (a >= x.first && a + bytes <= x.first + x.second && a + bytes >= a) return true;
+        return false;
     }
-    std::vector<std::thread> pool;
-    try {
-        for (unsigned t = 1; t < threads; ++t) pool.emplace_back(work);
-    } catch (const std::system_error&) {
-        // fewer threads than asked: the ones running (and this one) take the remaining proofs
-    }
-    work();
-    for (auto& th : pool) th.join();
-}
-
-// decode_all with the upload overlapped: the proofs are cut into chunks of ~CHUNK_WORDS staged
-// words; worker threads decode in proof order while this thread hands each finished chunk to
-// `ready(first_word, n_words)` (an async DMA), so the copy of chunk c runs under the decode of
-// c + 1.  Returns false when no worker thread could be started (the caller then decodes and
-// copies in one piece).
-template <class Ready>
-bool decode_all_streamed(const Dims& D, const nhip_claim* claims, const nhip_proof* proofs, size_t n,
-                         uint64_t* words, const std::vector<uint64_t>& bases, uint64_t words_total,
-                         std::vector<ProofOut>& outs, unsigned threads, Ready&& ready) {
-    constexpr uint64_t CHUNK_WORDS = 8ull << 20;  // 64 MB
-    std::vector<size_t> cut{0};                   // chunk c = proofs [cut[c], cut[c+1])
-    for (size_t i = 1; i < n; ++i)
-        if (bases[i] - bases[cut.back()] >= CHUNK_WORDS) cut.push_back(i);
-    cut.push_back(n);
-    const size_t nc = cut.size() - 1;
-    std::vector<size_t> chunk_of(n);
-    std::unique_ptr<std::atomic<size_t>[]> left(new std::atomic<size_t>[nc]);
-    for (size_t c = 0; c < nc; ++c) {
-        left[c].store(cut[c + 1] - cut[c]);
-        for (size_t i = cut[c]; i < cut[c + 1]; ++i) chunk_of[i] = c;
-    }
-    std::atomic<size_t> next{0};
-    auto work = [&]() {
-        constexpr size_t STEP = 4;
-        for (size_t a; (a = next.fetch_add(STEP)) < n;)
-            for (size_t i = a; i < std::min(n, a + STEP); ++i) {
-                decode_proof(D, claims[i], proofs[i], words, bases[i], outs[i]);
-                left[chunk_of[i]].fetch_sub(1, std::memory_order_release);
-            }
-    };
-    std::vector<std::thread> pool;
-    try {
-        for (unsigned t = 0; t < threads; ++t) pool.emplace_back(work);
-    } catch (const std::system_error&) {
-    }
-    if (pool.empty()) return false;
-    for (size_t c = 0; c < nc; ++c) {
-        while (left[c].load(std::memory_order_acquire) != 0)
-            std::this_thread::sleep_for(std::chrono::microseconds(20));
-        const uint64_t w0 = bases[cut[c]], w1 = c + 1 < nc ? bases[cut[c + 1]] : words_total;
-        ready(w0, w1 - w0);
-    }
-    for (auto& th : pool) th.join();
-    return true;
+};
+PinnedRanges& pinned() {
+    static PinnedRanges p;
+    return p;
 }
 
 }  // namespace
@@ -523,20 +158,18 @@ struct nhip_batch {
     // device buffers
     void* dmem = nullptr;
     StarkBatchDev dev{};
-    uint32_t* d_fail_init = nullptr;
-    uint64_t* d_perm_counter = nullptr;
     StarkPhaseTimer tm{};
     hipStream_t main = nullptr;  // hashing chain (rows -> Merkle levels -> roots -> verdicts)
     hipStream_t aux = nullptr;   // latency-bound chain (Fiat-Shamir -> plan -> OOD -> FRI -> DEEP)
-    uint8_t* h_out = nullptr;    // pinned: [perm counter (8 B) | verdicts (n B)]
+    uint8_t* h_out = nullptr;    // pinned: [device counters | plan counters | verdicts (n B)]
     size_t dmem_bytes = 0, h_out_bytes = 0;  // owned allocations (refill reuses them when they fit)
     void* dwords = nullptr;                  // proof words (owned unless borrowed from the scratch)
     size_t dwords_bytes = 0;
     bool timed = false, in_flight = false;
     struct {
-        double fs, rows, plan, hash, roots, ood, fri, deep, total;
+        double decode, fs, rows, plan, hash, roots, ood, fri, deep, total;
     } ph{};
-    double decode_ms = 0, upload_ms = 0;
+    double stage_ms = 0, upload_ms = 0;
     uint64_t merkle_perms = 0;
     std::vector<uint64_t> mp_cap;  // multiproof op capacity per level
 };
@@ -574,7 +207,7 @@ bool dims_from(const nhip_stark_params* sp, const nhip_air* air, Dims& D) {
     if (deep_lds_bytes(d) > 160 * 1024 - 8192) return false;
     // the last FRI codeword has at most 2^(floor(log2 k) + 1 + log2 expansion) XFEs; bound its
     // Merkle-tree scratch (n x max_len digests)
-    if ((1ull << (log2u(d.num_checks) + 1 + d.log2_expansion)) > 4096) return false;
+    if ((1ull << (log2_u64(d.num_checks) + 1 + d.log2_expansion)) > 4096) return false;
     return true;
 }
 
@@ -784,15 +417,20 @@ int nhip_proof_decodes(const nhip_air* air, const nhip_stark_params* sp, const n
                        const nhip_proof* proof) {
     Dims D{};
     if (!claim || !proof || (proof->len && !proof->words) || !dims_from(sp, air, D)) return -NHIP_ERR_ARG;
-    std::vector<uint64_t> words(staged_words(*claim, *proof));
-    ProofOut o;
-    decode_proof(D, *claim, *proof, words.data(), 0, o);
-    return o.fail ? 0 : 1;
+    // the same walk k_decode runs, straight on the caller's words (proof_codec.hpp)
+    ProofDesc pd;
+    FsOp ops[fs_ops_for(MAX_FRI_ROUNDS)];
+    uint64_t perms, perms_lcw;
+    const ClaimLoc cl{0, (uint32_t)claim->input_len, (uint32_t)claim->output_len};
+    return decode_stream(proof->words, 0, proof->len, cl, D, pd, ops, perms, perms_lcw) ? 0 : 1;
 }
 
 namespace {
-// Decode + upload a batch.  reuse == nullptr: a new batch (*out); otherwise `reuse` is refilled
-// in place (same streams and events; its device memory reused when large enough).
+// Stage + upload a batch: proof words (raw; k_decode walks them on the device every run) and
+// the staged claim encodings into the batch word buffer, the per-proof ProofIn records, and the
+// scratch sized from the padded height each proof header declares.  reuse == nullptr: a new batch
+// (*out); otherwise `reuse` is refilled in place (same streams and events; its device memory reused
+// when large enough).
 int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
                   const nhip_proof* proofs, size_t n, nhip_batch** out, VerifyScratch* scr,
                   nhip_batch* reuse = nullptr) {
@@ -801,9 +439,11 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     if (!reuse) *out = nullptr;
     Dims D{};
     if (!dims_from(sp, air, D)) return NHIP_ERR_ARG;
+    if (n > 0xFFFFFFFFull) return NHIP_ERR_ARG;
     for (size_t i = 0; i < n; ++i)
         if ((proofs[i].len && !proofs[i].words) || (claims[i].input_len && !claims[i].input) ||
-            (claims[i].output_len && !claims[i].output))
+            (claims[i].output_len && !claims[i].output) || claims[i].input_len > 0xFFFFFFFFull ||
+            claims[i].output_len > 0xFFFFFFFFull)
             return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
     (void)hipSetDevice(nhip_internal_device(ctx));
@@ -827,24 +467,44 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     b->H = HostBatch{};
     HostBatch& H = b->H;
     H.D = D;
-    H.desc.reserve(n);
-    H.fail.reserve(n);
-    // stage every proof (+ claim encoding) straight into the context's pinned staging buffer
-    // (pinned once per context and reused: not part of the decode time), on several host
-    // threads, then merge the descriptors in proof order
-    std::vector<uint64_t> bases(n);
+    H.n = (uint32_t)n;
+    const auto t0 = std::chrono::steady_clock::now();
+    // ---- layout and scratch sizes: proof words back to back, then the claim encodings; the
+    // padded height each proof declares (its first item, 5 header words) sizes the multiproof plan,
+    // the sample areas and the Fiat-Shamir program slots.  k_decode re-reads it and rejects a proof
+    // whose walk disagrees (never happens for one buffer; guards the scratch bounds).
+    std::vector<ProofIn> pin(n);
+    std::vector<ProofShape> shp(n);
+    uint64_t cur = 0;
     for (size_t i = 0; i < n; ++i) {
-        bases[i] = H.words_total;
-        H.words_total += staged_words(claims[i], proofs[i]);
+        pin[i].off = cur;
+        pin[i].len = proofs[i].len;
+        cur += proofs[i].len;
     }
-    std::vector<uint64_t> pageable;
-    uint64_t* words = (uint64_t*)nhip_internal_staging(ctx, H.words_total * 8 + 8);
-    if (!words) {
-        pageable.resize(H.words_total + 1);
-        words = pageable.data();
+    H.proof_words = cur;
+    for (size_t i = 0; i < n; ++i) {
+        pin[i].claim_off = cur;
+        pin[i].claim_in_n = (uint32_t)claims[i].input_len;
+        pin[i].claim_out_n = (uint32_t)claims[i].output_len;
+        cur += claim_words(claims[i]);
     }
-    // device buffer for the proof words (grow-only; its own allocation, so that it can be filled
-    // while the rest of the batch's sizes are still being decoded)
+    H.words_total = cur;
+    for (size_t i = 0; i < n; ++i) {
+        uint64_t lph = 0;
+        ProofShape s{};
+        if (header_log2_ph(proofs[i].words, proofs[i].len, lph) && shape_of(D, lph, s)) {
+            pin[i].sized_log2_ph = s.log2_ph;
+            shp[i] = s;
+            H.max_R = std::max(H.max_R, s.R);
+            H.levels = std::max(H.levels, s.log2_N);
+            H.max_last_cw = std::max(H.max_last_cw, 1u << (s.log2_N - s.R));
+        } else {
+            pin[i].sized_log2_ph = SHAPE_NONE;
+        }
+    }
+    H.fs_stride = fs_ops_for(H.max_R);
+    H.xs_stride = SampleLayout::of(D.d, H.max_R).total;
+    // ---- device word buffer (grow-only; its own allocation)
     const size_t wbytes = H.words_total * 8 + 8;
     {
         void** dw = scr ? &scr->dwords : &b->dwords;
@@ -866,26 +526,92 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     hipStream_t st = nhip_internal_stream(ctx);
     uint64_t* d_words = (uint64_t*)b->dwords;
     hipError_t e = hipSuccess;
-    auto t0 = std::chrono::steady_clock::now();
+    auto dma = [&](uint64_t dst_word, const uint64_t* src, uint64_t nw) {
+        if (e == hipSuccess && nw) e = hipMemcpyAsync(d_words + dst_word, src, nw * 8, hipMemcpyHostToDevice, st);
+    };
+    // ---- upload.  Proofs in pinned caller memory (nhip_host_alloc / nhip_host_register) are
+    // DMA'd as they lie, adjacent ones as one copy; the others are copied into the context's
+    // pinned staging (same layout as the device buffer) by host threads, ~64 MB chunks in proof
+    // order, each chunk's DMA issued as soon as its copies are done.  The claim encodings go
+    // through the staging too.
     {
-        std::vector<ProofOut> outs(n);
-        const unsigned threads = host_threads(n);
-        bool streamed = false;
-        if (threads > 1 && words != pageable.data())
-            streamed = decode_all_streamed(D, claims, proofs, n, words, bases, H.words_total, outs, threads,
-                                           [&](uint64_t w0, uint64_t nw) {
-                                               if (e == hipSuccess && nw)
-                                                   e = hipMemcpyAsync(d_words + w0, words + w0, nw * 8,
-                                                                      hipMemcpyHostToDevice, st);
-                                           });
-        if (!streamed) {
-            decode_all(D, claims, proofs, n, words, bases, outs, threads);
-            if (H.words_total) e = hipMemcpyAsync(d_words, words, H.words_total * 8, hipMemcpyHostToDevice, st);
+        std::vector<uint8_t> direct(n, 0);
+        for (size_t i = 0; i < n; ++i)
+            direct[i] = proofs[i].len && pinned().contains(proofs[i].words, proofs[i].len * 8) ? 1 : 0;
+        for (size_t i = 0; i < n;) {  // direct segments first: the DMA engine starts right away
+            if (!direct[i]) {
+                ++i;
+                continue;
+            }
+            size_t j = i + 1;
+            while (j < n && direct[j] && proofs[j].words == proofs[j - 1].words + proofs[j - 1].len) ++j;
+            dma(pin[i].off, proofs[i].words, pin[j - 1].off + pin[j - 1].len - pin[i].off);
+            i = j;
         }
-        for (size_t i = 0; i < n; ++i) merge_proof(H, outs[i], proofs[i].len);
+        std::vector<uint64_t> pageable;
+        uint64_t* stage = (uint64_t*)nhip_internal_staging(ctx, wbytes);
+        if (!stage) {
+            pageable.resize(H.words_total + 1);
+            stage = pageable.data();
+        }
+        for (size_t i = 0; i < n; ++i) encode_claim(claims[i], stage + pin[i].claim_off);
+        std::vector<size_t> todo;  // staged proofs, in order
+        uint64_t staged_bytes = 0;
+        for (size_t i = 0; i < n; ++i)
+            if (!direct[i] && proofs[i].len) todo.push_back(i), staged_bytes += proofs[i].len * 8;
+        constexpr uint64_t CHUNK_WORDS = 8ull << 20;  // 64 MB
+        std::vector<size_t> cut{0};                   // chunk c = todo[cut[c] .. cut[c + 1])
+        for (size_t q = 1; q < todo.size(); ++q)
+            if (pin[todo[q]].off - pin[todo[cut.back()]].off >= CHUNK_WORDS) cut.push_back(q);
+        cut.push_back(todo.size());
+        const size_t nc = todo.empty() ? 0 : cut.size() - 1;
+        std::unique_ptr<std::atomic<size_t>[]> left(new std::atomic<size_t>[nc + 1]);
+        std::vector<size_t> chunk_of(todo.size());
+        for (size_t c = 0; c < nc; ++c) {
+            left[c].store(cut[c + 1] - cut[c]);
+            for (size_t q = cut[c]; q < cut[c + 1]; ++q) chunk_of[q] = c;
+        }
+        std::atomic<size_t> next{0};
+        auto work = [&]() {
+            for (size_t q; (q = next.fetch_add(1)) < todo.size();) {
+                const size_t i = todo[q];
+                std::memcpy(stage + pin[i].off, proofs[i].words, proofs[i].len * 8);
+                left[chunk_of[q]].fetch_sub(1, std::memory_order_release);
+            }
+        };
+        std::vector<std::thread> pool;
+        const unsigned threads = host_threads(staged_bytes);
+        if (threads > 1 && stage != pageable.data()) {
+            pool.reserve(threads);
+            for (unsigned t = 0; t < threads; ++t) {
+                try {
+                    pool.emplace_back(work);
+                } catch (const std::system_error&) {
+                    break;  // fewer threads: the running ones (and this one, below) take the rest
+                }
+            }
+        }
+        if (pool.empty()) work();
+        // DMA each chunk once copied: its staged proofs, adjacent ones as one copy
+        for (size_t c = 0; c < nc; ++c) {
+            while (left[c].load(std::memory_order_acquire) != 0) {
+                if (pool.empty()) break;
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
+            }
+            for (size_t q = cut[c]; q < cut[c + 1];) {
+                size_t r = q + 1;
+                while (r < cut[c + 1] && todo[r] == todo[r - 1] + 1) ++r;
+                const size_t i0 = todo[q], i1 = todo[r - 1];
+                dma(pin[i0].off, stage + pin[i0].off, pin[i1].off + pin[i1].len - pin[i0].off);
+                q = r;
+            }
+        }
+        for (auto& th : pool) th.join();
+        dma(H.proof_words, stage + H.proof_words, H.words_total - H.proof_words);
+        if (stage == pageable.data() && e == hipSuccess) e = hipStreamSynchronize(st);  // pageable source
     }
-    auto t1 = std::chrono::steady_clock::now();
-    b->decode_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    const auto t1 = std::chrono::steady_clock::now();
+    b->stage_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (e != hipSuccess) {
         (void)hipStreamSynchronize(st);
         if (scr) b->dwords = nullptr;
@@ -893,14 +619,20 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     }
     nhip_air::Dev adev{};
     int rc = air_upload(ctx, air, &adev);
-    if (rc) return fail_out(rc);
+    if (rc) {
+        (void)hipStreamSynchronize(st);
+        return fail_out(rc);
+    }
     {
         static std::mutex attrs_mu;
         static uint64_t attrs_set = 0;  // devices whose kernel attributes are set
         std::lock_guard<std::mutex> attrs_lock(attrs_mu);
         const int adevice = nhip_internal_device(ctx);
         if (adevice >= 64 || !((attrs_set >> adevice) & 1u)) {
-            if (stark_set_kernel_attributes() != hipSuccess) return fail_out(NHIP_ERR_HIP);
+            if (stark_set_kernel_attributes() != hipSuccess) {
+                (void)hipStreamSynchronize(st);
+                return fail_out(NHIP_ERR_HIP);
+            }
             if (adevice < 64) attrs_set |= 1ull << adevice;
         }
     }
@@ -908,17 +640,15 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     // multiproof op capacity per (level, shard): a tree of height h has at most min(k, 2^(h-1-l))
     // parents at level l; shard = proof index % MP_SHARDS
     const uint32_t tpp = 4 + H.max_R;
-    uint32_t levels = 0;
-    for (size_t i = 0; i < n; ++i)
-        if (!(H.fail[i] & FAIL_DECODE)) levels = std::max(levels, H.desc[i].log2_N);
+    const uint32_t levels = H.levels;
     std::vector<uint64_t> mp_scap((size_t)levels * MP_SHARDS, 0), mp_sbase((size_t)levels * MP_SHARDS, 0);
     b->mp_cap.assign(levels, 0);
     for (size_t i = 0; i < n; ++i) {
-        if (H.fail[i] & FAIL_DECODE) continue;
-        const ProofDesc& pd = H.desc[i];
+        if (pin[i].sized_log2_ph == SHAPE_NONE) continue;
+        const ProofShape& s = shp[i];
         const uint32_t sh = (uint32_t)(i % MP_SHARDS);
-        for (uint32_t t = 0; t < 4 + pd.R; ++t) {
-            const uint32_t h = t < 4 ? pd.log2_N : pd.log2_N - (t - 4);
+        for (uint32_t t = 0; t < 4 + s.R; ++t) {
+            const uint32_t h = t < 4 ? s.log2_N : s.log2_N - (t - 4);
             for (uint32_t l = 0; l < h; ++l)
                 mp_scap[(size_t)l * MP_SHARDS + sh] += std::min<uint64_t>(k, 1ull << std::min(h - 1 - l, 40u));
         }
@@ -930,32 +660,34 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
             mp_total += mp_scap[(size_t)l * MP_SHARDS + q];
             b->mp_cap[l] += mp_scap[(size_t)l * MP_SHARDS + q];
         }
-    const size_t sz[] = {8,  // (slot 0 unused: the proof words have their own allocation)
-                         std::max<size_t>(1, n) * sizeof(ProofDesc),
-                         H.ops.size() * sizeof(FsOp) + 8,
-                         H.xs_total * 24 + 8,
-                         H.idx_total * 4 + 8,
-                         std::max<size_t>(1, n) * 3 * k * 40,
-                         std::max<size_t>(1, n) * 9 * 8,
-                         std::max<size_t>(1, n) * 4,
-                         std::max<size_t>(1, n) * 4,
-                         std::max<size_t>(1, n),
-                         8,
+    const size_t N1 = std::max<size_t>(1, n);
+    const size_t sz[] = {8,  // (slot 0 unused: the words have their own allocation)
+                         N1 * sizeof(ProofDesc),
+                         N1 * H.fs_stride * sizeof(FsOp),
+                         N1 * H.xs_stride * 24,
+                         N1 * k * 4,
+                         N1 * 3 * k * 40,
+                         N1 * 9 * 8,
+                         N1 * 4,
+                         N1 * sizeof(ProofIn),
+                         N1,
+                         CNT_N * 8,
                          mp_total * 16 + 16,
                          mp_total * 40 + 40,
                          (size_t)levels * MP_SHARDS * 8 + 8,
                          (size_t)levels * MP_SHARDS * 8 + 8,
                          (size_t)levels * MP_SHARDS * 4 + 4,
-                         std::max<size_t>(1, n) * tpp * sizeof(MpRoot),
-                         std::max<size_t>(1, n) * (1 + H.max_R) * k * 8,
-                         std::max<size_t>(1, n) * (1 + H.max_R) * 4,
-                         std::max<size_t>(1, n) * k * 8,
-                         std::max<size_t>(1, n) * H.max_last_cw * 40};
+                         N1 * tpp * sizeof(MpRoot),
+                         N1 * (1 + H.max_R) * k * 8,
+                         N1 * (1 + H.max_R) * 4,
+                         N1 * k * 8,
+                         N1 * H.max_last_cw * 40};
     constexpr int NBUF = sizeof(sz) / sizeof(sz[0]);
     size_t total = 0;
-    for (size_t s : sz) total += al(s);
+    for (size_t x : sz) total += al(x);
     if (scr) {  // grow-only device scratch of the context
         if (scr->dmem_bytes < total) {
+            (void)hipStreamSynchronize(st);
             if (scr->dmem) (void)hipFree(scr->dmem);
             scr->dmem = nullptr;
             scr->dmem_bytes = 0;
@@ -964,6 +696,7 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         }
         b->dmem = scr->dmem;
     } else if (b->dmem_bytes < total) {  // new batch, or a refill that no longer fits
+        (void)hipStreamSynchronize(st);
         if (b->dmem) (void)hipFree(b->dmem);
         b->dmem = nullptr;
         b->dmem_bytes = 0;
@@ -972,6 +705,7 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         if (e == hipSuccess) b->dmem_bytes = want;
     }
     if (e != hipSuccess) {
+        (void)hipStreamSynchronize(st);
         if (scr) b->dmem = nullptr;
         return fail_out(hipfail(e));
     }
@@ -981,34 +715,36 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         ptr[i] = p;
         p += al(sz[i]);
     }
-    if (n) e = hipMemcpyAsync(ptr[1], H.desc.data(), n * sizeof(ProofDesc), hipMemcpyHostToDevice, st);
-    if (e == hipSuccess && !H.ops.empty())
-        e = hipMemcpyAsync(ptr[2], H.ops.data(), H.ops.size() * sizeof(FsOp), hipMemcpyHostToDevice, st);
-    if (e == hipSuccess && n) e = hipMemcpyAsync(ptr[8], H.fail.data(), n * 4, hipMemcpyHostToDevice, st);
+    if (n) e = hipMemcpyAsync(ptr[8], pin.data(), n * sizeof(ProofIn), hipMemcpyHostToDevice, st);
     if (e == hipSuccess && levels)
         e = hipMemcpyAsync(ptr[13], mp_sbase.data(), mp_sbase.size() * 8, hipMemcpyHostToDevice, st);
     if (e == hipSuccess && levels)
         e = hipMemcpyAsync(ptr[14], mp_scap.data(), mp_scap.size() * 8, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    auto t2 = std::chrono::steady_clock::now();
+    {
+        const hipError_t es = hipStreamSynchronize(st);  // the sources are host vectors / the staging
+        if (e == hipSuccess) e = es;
+    }
+    const auto t2 = std::chrono::steady_clock::now();
     b->upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
     if (e != hipSuccess) return fail_out(hipfail(e));
     StarkBatchDev& dv = b->dev;
     dv.n_proofs = (uint32_t)n;
     dv.max_R = H.max_R;
     dv.dims = D.d;
+    dv.D = D;
+    dv.fs_stride = H.fs_stride;
+    dv.xs_stride = H.xs_stride;
     dv.words = d_words;
-    dv.desc = (const ProofDesc*)ptr[1];
-    dv.ops = (const FsOp*)ptr[2];
+    dv.desc = (ProofDesc*)ptr[1];
+    dv.ops = (FsOp*)ptr[2];
     dv.xs = (uint64_t*)ptr[3];
     dv.idx = (uint32_t*)ptr[4];
     dv.dig = (uint64_t*)ptr[5];
     dv.ood = (uint64_t*)ptr[6];
     dv.fail = (uint32_t*)ptr[7];
-    b->d_fail_init = (uint32_t*)ptr[8];
+    dv.in = (const ProofIn*)ptr[8];
     dv.verdicts = (uint8_t*)ptr[9];
-    b->d_perm_counter = (uint64_t*)ptr[10];
-    dv.perm_counter = (unsigned long long*)ptr[10];
+    dv.counters = (unsigned long long*)ptr[10];
     dv.mp.ops = (uint64_t*)ptr[11];
     dv.mp.arena = (uint64_t*)ptr[12];
     dv.mp.shard_base = (const uint64_t*)ptr[13];
@@ -1021,7 +757,6 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     dv.xdom = (uint64_t*)ptr[19];
     dv.lcw = (uint64_t*)ptr[20];
     dv.max_lcw = H.max_last_cw;
-    dv.fail_init = b->d_fail_init;
     dv.mp_cap_host = b->mp_cap.data();
     dv.air_prog = adev.d_prog;
     dv.air_prog_off = adev.d_prog_off;
@@ -1111,14 +846,13 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
     hipStream_t st = b->main;
     const uint32_t n = b->dev.n_proofs;
     hipError_t e = hipSuccess;
-    if (n) e = hipMemcpyAsync(b->dev.fail, b->d_fail_init, n * 4, hipMemcpyDeviceToDevice, st);
     const size_t cnt_bytes = (size_t)b->dev.mp.levels * MP_SHARDS * 4;
-    if (e == hipSuccess) e = hipMemsetAsync(b->d_perm_counter, 0, 8, st);
+    e = hipMemsetAsync(b->dev.counters, 0, CNT_N * 8, st);
     if (e == hipSuccess && cnt_bytes) e = hipMemsetAsync(b->dev.mp.counter, 0, cnt_bytes, st);
     if (e != hipSuccess) return hipfail(e);
     e = launch_stark_phases(b->dev, st, b->aux, &b->tm);
     if (e != hipSuccess) return hipfail(e);
-    if (e == hipSuccess) e = hipMemcpyAsync(b->h_out, b->d_perm_counter, 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(b->h_out, b->dev.counters, CNT_N * 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess && cnt_bytes) e = hipMemcpyAsync(b->h_out + OUT_HDR, b->dev.mp.counter, cnt_bytes, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess && n) e = hipMemcpyAsync(b->h_out + OUT_HDR + cnt_bytes, b->dev.verdicts, n, hipMemcpyDeviceToHost, st);
     if (e != hipSuccess) return hipfail(e);
@@ -1136,16 +870,19 @@ int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* al
     if (e != hipSuccess) return hipfail(e);
     const uint32_t n = b->dev.n_proofs;
     // Merkle permutations: multiproof ops reserved by the plan (per level and shard) minus the ops of
-    // trees whose authentication structure failed, plus the last-codeword trees
+    // trees whose authentication structure failed, plus the last-codeword trees; the sponge + row
+    // permutations of the proofs k_decode accepted
     const size_t cnt_n = (size_t)b->dev.mp.levels * MP_SHARDS;
-    uint64_t skipped = 0, reserved = 0;
-    std::memcpy(&skipped, b->h_out, 8);
+    uint64_t cnt[CNT_N], reserved = 0;
+    std::memcpy(cnt, b->h_out, sizeof(cnt));
     for (size_t i = 0; i < cnt_n; ++i) {
         uint32_t c;
         std::memcpy(&c, b->h_out + OUT_HDR + 4 * i, 4);
         reserved += c;
     }
-    b->merkle_perms = reserved - skipped + b->H.perms_lcw;
+    b->H.perms_static = cnt[CNT_PERMS_STATIC];
+    b->H.perms_lcw = cnt[CNT_PERMS_LCW];
+    b->merkle_perms = reserved - cnt[CNT_MP_SKIPPED] + b->H.perms_lcw;
     // phases overlap (two streams): each is timed from the event its inputs wait on
     auto el = [&](int a, int c) {
         float ms = 0.f;
@@ -1153,6 +890,7 @@ int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* al
         return (double)ms;
     };
     if (n) {
+        b->ph.decode = el(12, 0);
         b->ph.fs = el(0, 1);
         b->ph.rows = el(0, 2);
         b->ph.plan = el(1, 3);
@@ -1161,7 +899,7 @@ int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* al
         b->ph.ood = el(11, 6);
         b->ph.fri = el(6, 7);
         b->ph.deep = el(7, 8);
-        b->ph.total = el(0, 9);
+        b->ph.total = el(12, 9);
     }
     const uint8_t* v = b->h_out + OUT_HDR + cnt_n * 4;
     if (verdicts && n) std::memcpy(verdicts, v, n);
@@ -1184,7 +922,7 @@ int nhip_batch_stats(const nhip_batch* b, nhip_stats* s) {
     std::memset(s, 0, sizeof(*s));
     s->num_proofs = b->dev.n_proofs;
     s->proof_words = b->H.proof_words;
-    s->ms_decode = b->decode_ms;
+    s->ms_decode = b->stage_ms;
     s->ms_upload = b->upload_ms;
     s->ms_fiat_shamir = b->ph.fs;
     s->ms_row_hash = b->ph.rows;
@@ -1194,8 +932,8 @@ int nhip_batch_stats(const nhip_batch* b, nhip_stats* s) {
     s->ms_ood_air = b->ph.ood;
     s->ms_fri = b->ph.fri;
     s->ms_deep = b->ph.deep;
-    s->ms_device_total = 0;
     s->ms_device_total = b->ph.total;
+    s->ms_device_decode = b->ph.decode;
     s->tip5_perms_static = b->H.perms_static;
     s->tip5_perms_merkle = b->merkle_perms;
     // every Merkle hash launch (k_mp_hash + the 16-lane-row k_mp_hash_wide): back to back on the
@@ -1212,11 +950,13 @@ int nhip_batch_transcript(nhip_ctx* ctx, const nhip_batch* b, size_t proof, uint
     std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
     (void)hipSetDevice(b->device);
     hipStream_t st = nhip_internal_stream(ctx);
-    const ProofDesc& pd = b->H.desc[proof];
+    ProofDesc pd{};
+    hipError_t e = hipMemcpyAsync(&pd, b->dev.desc + proof, sizeof(pd), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hipfail(e);
     const size_t nx = pd.n_xs;
     if (n_xfe) *n_xfe = nx;
     std::vector<uint64_t> raw(nx * 3);
-    hipError_t e = hipSuccess;
     if (nx) e = hipMemcpyAsync(raw.data(), b->dev.xs + pd.xs_off * 3, nx * 24, hipMemcpyDeviceToHost, st);
     std::vector<uint32_t> ix(b->dev.dims.num_checks);
     if (e == hipSuccess)
@@ -1248,6 +988,58 @@ void nhip_batch_destroy(nhip_batch* b) {
     if (b->dmem) (void)hipFree(b->dmem);
     if (b->dwords) (void)hipFree(b->dwords);
     delete b;
+}
+
+int nhip_host_alloc(size_t bytes, void** out) {
+    if (!out) return NHIP_ERR_ARG;
+    *out = nullptr;
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return NHIP_ERR_OOM;
+    try {
+        std::lock_guard<std::mutex> g(pinned().mu);
+        pinned().r.emplace_back((uintptr_t)p, bytes);
+    } catch (const std::bad_alloc&) {
+        (void)hipHostFree(p);
+        return NHIP_ERR_OOM;
+    }
+    *out = p;
+    return NHIP_OK;
+}
+
+static bool pinned_forget(void* p) {
+    std::lock_guard<std::mutex> g(pinned().mu);
+    auto& r = pinned().r;
+    for (size_t i = 0; i < r.size(); ++i)
+        if (r[i].first == (uintptr_t)p) {
+            r.erase(r.begin() + (ptrdiff_t)i);
+            return true;
+        }
+    return false;
+}
+
+int nhip_host_free(void* p) {
+    if (!p) return NHIP_OK;
+    if (!pinned_forget(p)) return NHIP_ERR_ARG;
+    return hipfail(hipHostFree(p));
+}
+
+int nhip_host_register(void* p, size_t bytes) {
+    if (!p || !bytes) return NHIP_ERR_ARG;
+    const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterPortable);
+    if (e != hipSuccess) return hipfail(e);
+    try {
+        std::lock_guard<std::mutex> g(pinned().mu);
+        pinned().r.emplace_back((uintptr_t)p, bytes);
+    } catch (const std::bad_alloc&) {
+        (void)hipHostUnregister(p);
+        return NHIP_ERR_OOM;
+    }
+    return NHIP_OK;
+}
+
+int nhip_host_unregister(void* p) {
+    if (!p || !pinned_forget(p)) return NHIP_ERR_ARG;
+    return hipfail(hipHostUnregister(p));
 }
 
 int nhip_verify_batch(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,

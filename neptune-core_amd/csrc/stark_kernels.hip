@@ -6,6 +6,7 @@
 #include <cstdlib>
 
 #include "kernels.hpp"
+#include "proof_codec.hpp"
 #include "stark.hpp"
 #include "tip5_device.hpp"
 #include "xfe.hpp"
@@ -31,66 +32,72 @@ __device__ __forceinline__ uint64_t root_of_unity(uint32_t log2n) {
     return b_pow(to_mont(7), (GL_P - 1) >> log2n);
 }
 
-// ------------------------------------------------------------------ Fiat-Shamir replay
-// One lane per proof replays the proof's sponge program: pad_and_absorb_all of the claim and of
-// every Fiat-Shamir item, squeezes for sample_scalars, sample_indices (skip BFieldElement::MAX,
-// `value as u32 % bound`).
-__global__ void __launch_bounds__(64) k_fs_replay(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
-                                                  const FsOp* __restrict__ ops, uint32_t n_proofs,
-                                                  uint64_t* __restrict__ xs, uint32_t* __restrict__ idx_out,
-                                                  const uint32_t* __restrict__ fail) {
-    __shared__ Tip5Lds lds;
-    tip5_lds_init(lds);
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_proofs || fail[p]) return;
-    const ProofDesc& d = desc[p];
-    uint64_t s[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) s[k] = 0;
-    uint64_t xcur = d.xs_off * 3;  // word cursor into xs
-    uint64_t icur = d.idx_off;
-    for (uint32_t o = 0; o < d.fs_op_n; ++o) {
-        const FsOp op = ops[d.fs_op_off + o];
-        if (op.kind == FS_ABSORB) {
-            const uint64_t* __restrict__ src = words + op.arg;
-            const uint32_t len = op.n;
-            uint32_t pos = 0;
-            for (; pos + TIP5_RATE <= len; pos += TIP5_RATE) {
-#pragma unroll
-                for (int k = 0; k < TIP5_RATE; ++k) s[k] = to_mont(src[pos + k]);
-                tip5_permute_raw(s, lds.lut);
-            }
-            const uint32_t rem = len - pos;
-#pragma unroll
-            for (int k = 0; k < TIP5_RATE; ++k) {
-                const uint32_t kk = (uint32_t)k;
-                s[k] = kk < rem ? to_mont(src[pos + kk]) : (kk == rem ? MONT_ONE : 0ull);
-            }
-            tip5_permute_raw(s, lds.lut);
-        } else if (op.kind == FS_SQUEEZE_X) {
-            const uint32_t nwords = 3 * op.n;
-            for (uint32_t f = 0; f < nwords; f += TIP5_RATE) {
-#pragma unroll
-                for (int k = 0; k < TIP5_RATE; ++k)
-                    if (f + (uint32_t)k < nwords) xs[xcur + f + k] = s[k];
-                tip5_permute_raw(s, lds.lut);
-            }
-            xcur += nwords;
-        } else {  // FS_SAMPLE_IDX
-            const uint64_t bound = op.arg;
-            uint32_t got = 0;
-            while (got < op.n) {
-                uint64_t out[TIP5_RATE];
-#pragma unroll
-                for (int k = 0; k < TIP5_RATE; ++k) out[k] = from_mont(s[k]);
-                tip5_permute_raw(s, lds.lut);
-                for (int k = 0; k < TIP5_RATE && got < op.n; ++k) {
-                    if (out[k] != GL_P - 1) idx_out[icur + got++] = (uint32_t)((out[k] & 0xFFFFFFFFull) % bound);
-                }
-            }
-            icur += op.n;
+// ------------------------------------------------------------------ proof-stream decode
+// One wave per proof: lane 0 walks the proof stream (decode_stream, proof_codec.hpp: the item
+// headers form a dependent chain of ~20-70 wave-uniform loads), writing the descriptor into LDS and
+// the Fiat-Shamir program into the proof's slot; the wave then scans the last FRI polynomial for
+// its degree (lane-parallel: a prover can pad it with zero coefficients) and copies the descriptor
+// out.  Every run of a batch decodes again from the raw words in HBM, so the device phases never
+// depend on host-side parsing.  fail[p] is (re)initialised here: FAIL_DECODE or 0.
+__global__ void __launch_bounds__(64) k_decode(const uint64_t* __restrict__ words, const ProofIn* __restrict__ in,
+                                               uint32_t n_proofs, Dims D, uint32_t fs_stride, uint32_t xs_stride,
+                                               ProofDesc* __restrict__ desc, FsOp* __restrict__ ops,
+                                               uint32_t* __restrict__ fail, unsigned long long* __restrict__ counters) {
+    __shared__ ProofDesc spd;
+    __shared__ uint32_t sfail;
+    __shared__ int sdeg;
+    const uint32_t p = blockIdx.x, lane = threadIdx.x;
+    if (p >= n_proofs) return;
+    const ProofIn pin = in[p];
+    if (lane == 0) {
+        uint64_t perms = 0, perms_lcw = 0;
+        const ClaimLoc cl{pin.claim_off, pin.claim_in_n, pin.claim_out_n};
+        uint32_t f = decode_stream(words, pin.off, pin.len, cl, D, spd, ops + (uint64_t)p * fs_stride, perms, perms_lcw);
+        if (!f && spd.log2_ph != pin.sized_log2_ph) {  // capacity guard: the batch was sized from the header
+            f = FAIL_DECODE;
+            spd = ProofDesc{};
+            claim_offsets(spd, cl);
         }
+        if (!f) {
+            atomicAdd(counters + CNT_PERMS_STATIC, (unsigned long long)perms);
+            atomicAdd(counters + CNT_PERMS_LCW, (unsigned long long)perms_lcw);
+        }
+        sfail = f;
+        sdeg = -1;
     }
+    __syncthreads();
+    const uint32_t f = sfail;
+    if (!f) {
+        // highest non-zero coefficient, 64 coefficients per step from the top (lane 0 = highest)
+        int deg = -1;
+        for (uint32_t hi = spd.last_poly_n; hi > 0; hi = hi > 64 ? hi - 64 : 0) {
+            bool nz = false;
+            if (lane < hi) {
+                const uint64_t* x = words + spd.last_poly_off + 3ull * (hi - 1 - lane);
+                nz = (canon(x[0]) | canon(x[1]) | canon(x[2])) != 0;
+            }
+            const uint64_t b = __ballot(nz);
+            if (b) {
+                deg = (int)(hi - (uint32_t)__ffsll((unsigned long long)b));
+                break;
+            }
+        }
+        if (lane == 0) sdeg = deg;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        if (!f) last_poly_finish(spd, sdeg, D);
+        const SampleLayout sl = SampleLayout::of(D.d, spd.R);
+        spd.fs_op_off = p * fs_stride;
+        spd.xs_off = (uint64_t)p * xs_stride;
+        spd.n_xs = f ? 0u : sl.total;
+        spd.idx_off = (uint64_t)p * D.d.num_checks;
+        fail[p] = f;
+    }
+    __syncthreads();
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(&spd);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(desc + p);
+    for (uint32_t i = lane; i < sizeof(ProofDesc) / 8; i += 64) dst[i] = src[i];
 }
 
 // Same program on the 16-lane "wide" Tip5 (one proof per DPP row, PAIR = false: ~10x lower
@@ -504,7 +511,7 @@ __device__ __forceinline__ void lcw_node(const uint64_t* __restrict__ words, con
 __global__ void __launch_bounds__(256) k_mp_hash(const uint64_t* __restrict__ words, const uint64_t* __restrict__ dig,
                                                  MpPlan plan, uint32_t lvl, uint32_t mp_blocks,
                                                  const ProofDesc* __restrict__ desc, uint32_t n_proofs,
-                                                 const uint32_t* __restrict__ fail_init, LcwTree lcw) {
+                                                 const uint32_t* __restrict__ fail, LcwTree lcw) {
     __shared__ Tip5Lds t5;
     __shared__ uint64_t s_base[MP_SHARDS + 1];
     __shared__ uint32_t s_cnt[MP_SHARDS];
@@ -525,7 +532,7 @@ __global__ void __launch_bounds__(256) k_mp_hash(const uint64_t* __restrict__ wo
         const uint32_t per = lcw.max_len >> (lvl + 1);
         const uint64_t q = (uint64_t)(blockIdx.x - mp_blocks) * blockDim.x + threadIdx.x;
         const uint32_t p = (uint32_t)(q / per), i = (uint32_t)(q % per);
-        if (p < n_proofs && !(fail_init[p] & FAIL_DECODE)) {
+        if (p < n_proofs && !(fail[p] & FAIL_DECODE)) {  // FAIL_DECODE is final once k_decode ran
             const ProofDesc& d = desc[p];
             const uint32_t L = d.last_cw_n;
             if (i < (L >> (lvl + 1))) {
@@ -617,12 +624,11 @@ __global__ void __launch_bounds__(256) k_mp_hash_wide(const uint64_t* __restrict
 // Lanes n_records.. check the last codeword's Merkle root, one per proof.
 __global__ void k_mp_roots(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                            const uint64_t* __restrict__ dig, MpPlan plan, uint32_t n_records, uint32_t trees_per_proof,
-                           uint32_t k, uint32_t* __restrict__ fail, uint32_t n_proofs,
-                           const uint32_t* __restrict__ fail_init, LcwTree lcw) {
+                           uint32_t k, uint32_t* __restrict__ fail, uint32_t n_proofs, LcwTree lcw) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_records) {
         const uint32_t p = i - n_records;
-        if (p >= n_proofs || (fail_init[p] & FAIL_DECODE)) return;
+        if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
         const ProofDesc& d = desc[p];
         uint64_t v[5];
         lcw_node(words, d, lcw.nodes + (uint64_t)p * lcw.max_len * 5, 1, d.last_cw_n, v);
@@ -1131,7 +1137,11 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     const uint32_t k = b.dims.num_checks;
     const uint32_t tpp = 4 + b.max_R;
     auto mark = [&](int i, hipStream_t s) { (void)hipEventRecord(tm->ev[i], s); };
-    // fork: the aux stream starts after everything already queued on st (fail-bit reset etc.)
+    // proof-stream decode of every proof (descriptors, Fiat-Shamir programs, fail words)
+    mark(12, st);
+    hipLaunchKernelGGL(k_decode, dim3(n), dim3(64), 0, st, b.words, b.in, n, b.D, b.fs_stride, b.xs_stride, b.desc,
+                       b.ops, b.fail, b.counters);
+    // fork: the aux stream starts after everything already queued on st (counter reset, decode)
     mark(0, st);
     (void)hipStreamWaitEvent(sa, tm->ev[0], 0);
     // ---- aux stream: latency-bound chain
@@ -1147,10 +1157,10 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     mark(1, sa);
     if (k <= 128)
         hipLaunchKernelGGL(k_mp_plan<128>, dim3(n, 1 + b.max_R), dim3(128), 0, sa, b.words, b.desc, n, k, tpp, b.dig,
-                           b.idx, b.mp, b.fail, b.perm_counter);
+                           b.idx, b.mp, b.fail, b.counters + CNT_MP_SKIPPED);
     else
         hipLaunchKernelGGL(k_mp_plan<256>, dim3(n, 1 + b.max_R), dim3(256), 0, sa, b.words, b.desc, n, k, tpp, b.dig,
-                           b.idx, b.mp, b.fail, b.perm_counter);
+                           b.idx, b.mp, b.fail, b.counters + CNT_MP_SKIPPED);
     mark(3, sa);
     // ---- main stream: VALU-bound hashing
     {
@@ -1199,7 +1209,7 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
                                b.dig, b.mp, l);
         else
             hipLaunchKernelGGL(k_mp_hash, dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, b.words, b.dig, b.mp, l,
-                               mp_blocks, b.desc, n, b.fail_init, lcw);
+                               mp_blocks, b.desc, n, b.fail, lcw);
         ++launches;
     }
     if (!aux_started) launch_aux_chain();
@@ -1207,7 +1217,7 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     mark(4, st);
     const uint32_t nrec = n * tpp;
     hipLaunchKernelGGL(k_mp_roots, dim3((nrec + n + 255) / 256), dim3(256), 0, st, b.words, b.desc, b.dig, b.mp, nrec,
-                       tpp, k, b.fail, n, b.fail_init, lcw);
+                       tpp, k, b.fail, n, lcw);
     mark(5, st);
     (void)hipStreamWaitEvent(st, tm->ev[8], 0);  // join the aux chain
     hipLaunchKernelGGL(k_verdicts, dim3((n + 255) / 256), dim3(256), 0, st, b.fail, n, b.verdicts);

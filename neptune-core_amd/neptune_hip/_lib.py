@@ -50,7 +50,8 @@ class Stats(ctypes.Structure):
                 ("ms_ood_air", ctypes.c_double), ("ms_fri", ctypes.c_double), ("ms_deep", ctypes.c_double),
                 ("ms_device_total", ctypes.c_double), ("ms_merkle_hash", ctypes.c_double),
                 ("merkle_hash_launches", ctypes.c_uint64), ("ms_mp_hash_kernel", ctypes.c_double),
-                ("mp_hash_kernel_launches", ctypes.c_uint64), ("mp_hash_kernel_perms", ctypes.c_uint64)]
+                ("mp_hash_kernel_launches", ctypes.c_uint64), ("mp_hash_kernel_perms", ctypes.c_uint64),
+                ("ms_device_decode", ctypes.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -105,6 +106,10 @@ SIGNATURES = {
     "nhip_proof_from_be_bytes": ([ctypes.c_void_p, _sz, ctypes.c_void_p, _sz, ctypes.POINTER(_sz)], ctypes.c_int),
     "nhip_proof_to_be_bytes": ([ctypes.c_void_p, _sz, ctypes.c_void_p], ctypes.c_int),
     "nhip_claim_hash": ([_vp, ctypes.POINTER(Claim), _u64p], ctypes.c_int),
+    "nhip_host_alloc": ([_sz, ctypes.POINTER(_vp)], ctypes.c_int),
+    "nhip_host_free": ([_vp], ctypes.c_int),
+    "nhip_host_register": ([_vp, _sz], ctypes.c_int),
+    "nhip_host_unregister": ([_vp], ctypes.c_int),
     "nhip_pow_mast_commit": ([_vp, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "nhip_pow_preprocess": ([_vp, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                              ctypes.POINTER(_vp)], ctypes.c_int),

@@ -385,7 +385,7 @@ static int verify_one(const params_t* pp, const air_t* air, const claim_t* cl, c
         const uint32_t all = log2u(k);
         R = max_rounds > all + 1 ? max_rounds - (all + 1) : 0u;
     }
-    if (R > 40) goto out;
+    if (R > 26 || log2_N > 31) goto out;  /* descriptor bound; sample_indices' u32 upper bound */
     const item_t* main_root = dequeue(ps, MERKLE_ROOT);
     if (!main_root) goto out;
     xfe* chal = smp;

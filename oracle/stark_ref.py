@@ -45,6 +45,7 @@ from field_ref import (P, X_ONE, X_ZERO, Domain, GENERATOR, barycentric_evaluate
 EXT = 3
 DIGEST_LEN = 5
 CURRENT_VERSION = 0  # triton_vm::proof::CURRENT_VERSION (new_claim.rs:97); value unpinned
+MAX_FRI_ROUNDS = 26
 
 
 class VerifyError(Exception):
@@ -703,6 +704,9 @@ def _verify(params, air, claim, proof_words, transcript):
     ph = 1 << log2_ph
     fri_dom = params.fri_domain(ph)
     tree_h = int(math.log2(fri_dom.length))
+    # sample_indices takes a u32 upper bound; the descriptors hold at most 26 FRI rounds
+    if tree_h > 31 or params.fri_num_rounds(fri_dom.length) > MAX_FRI_ROUNDS:
+        raise VerifyError("FRI domain too large")
     main_root = ps.dequeue(MERKLE_ROOT)
     sampled = ps.sample_scalars(air.num_sampled, "challenges")
     challenges = derive_challenges(sampled, claim)
@@ -820,6 +824,8 @@ def structure_ok(params: StarkParams, proof_words: Sequence[int]) -> bool:
     ph = 1 << items[0][1]
     N = params.fri_domain(ph).length
     R = params.fri_num_rounds(N)
+    if N > (1 << 31) or R > MAX_FRI_ROUNDS:
+        return False
     if [k for k, _ in items] != expected_kinds(R):
         return False
     k = params.num_collinearity_checks
