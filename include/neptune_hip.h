@@ -191,6 +191,23 @@ int nhip_batch_transcript(nhip_ctx *ctx, const nhip_batch *batch, size_t proof, 
                           uint32_t *idx_out, size_t idx_cap, uint32_t *fail_bits, size_t *n_xfe);
 void nhip_batch_destroy(nhip_batch *batch);
 
+/* ---- coalescing queue for concurrent single-proof callers ---------------------------------
+ * The reference calls triton_vm::verify once per proof from many tokio tasks at once
+ * (verifier.rs:60-63; e.g. peer_loop.rs:1342 per peer transaction).  nhip_queue_verify is that
+ * call: blocking, thread-safe, nhip_verify_batch semantics for its own proofs; a worker thread
+ * gathers the proofs of every caller waiting at the time (up to max_batch proofs, at most
+ * max_wait_us after the oldest arrival) into one device batch, with the next batch collected while
+ * the current one runs.  max_batch 0 = 4096. */
+typedef struct nhip_queue nhip_queue;
+int nhip_queue_create(nhip_ctx *ctx, nhip_air *air, const nhip_stark_params *params, uint32_t max_batch,
+                      uint32_t max_wait_us, nhip_queue **out);
+int nhip_queue_verify(nhip_queue *queue, const nhip_claim *claims, const nhip_proof *proofs, size_t n,
+                      uint8_t *verdicts);
+/* batches launched and proofs verified so far */
+int nhip_queue_stats(const nhip_queue *queue, uint64_t *batches, uint64_t *proofs);
+/* Drains the pending requests, then stops the worker. */
+void nhip_queue_destroy(nhip_queue *queue);
+
 /* ---- several GPUs from one process --------------------------------------
  * neptune-core is one process; its batch callers (proof_collection.rs:342-388,
  * state/mod.rs:2226-2272, peer_loop.rs:315-323) end in n calls of triton_vm::verify at

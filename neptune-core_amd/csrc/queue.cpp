@@ -1,0 +1,220 @@
+// Coalescing verification queue (include/neptune_hip.h, nhip_queue_*).
+//
+// The reference verifies one proof per call: `verify(claim, proof, network)` hops onto tokio's
+// blocking pool and runs `triton_vm::verify` there (neptune-core/src/protocol/proof_abstractions/
+// verifier.rs:60-63), called concurrently from many tasks, e.g. one per peer transaction
+// (application/loops/peer_loop.rs:1342 -> Transaction::is_valid).  One GPU verify of a single
+// proof is latency-bound (~1.7 ms, almost all of it the sequential Fiat-Shamir sponge), so
+// serializing such calls would cap a context at ~500 proofs/s.  The queue gathers concurrent
+// callers' proofs into one batch instead ("the internal queue may coalesce small
+// calls into batches"): a worker thread takes every pending request (up to max_batch proofs, after
+// at most max_wait_us from the oldest arrival), stages them into one of two nhip_batch slots, and
+// launches it; while that batch runs on the device the next one is collected, so the device sees
+// back-to-back batches whose size follows the load.  Each caller blocks until its own verdicts are
+// written, with nhip_verify_batch semantics (0 = reject; a non-zero return is an infrastructure
+// fault, never "accept").
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <new>
+#include <system_error>
+#include <thread>
+#include <vector>
+
+#include "../../include/neptune_hip.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+struct Req {
+    const nhip_claim* claims;
+    const nhip_proof* proofs;
+    size_t n;
+    uint8_t* verdicts;
+    Clock::time_point arrived;
+    int rc = NHIP_OK;
+    bool done = false;
+};
+
+}  // namespace
+
+struct nhip_queue {
+    nhip_ctx* ctx = nullptr;
+    nhip_air* air = nullptr;
+    nhip_stark_params params{};
+    size_t max_batch = 0;
+    std::chrono::microseconds max_wait{0};
+    std::mutex mu;
+    std::condition_variable cv_in, cv_out;
+    std::deque<Req*> pending;
+    size_t pending_proofs = 0;
+    bool stop = false;
+    std::thread worker;
+    // two batch slots: one runs on the device while the next is collected and staged
+    nhip_batch* slot[2] = {nullptr, nullptr};
+    std::vector<Req*> in_slot[2];
+    bool in_flight[2] = {false, false};
+    std::vector<nhip_claim> claims;
+    std::vector<nhip_proof> proofs;
+    std::vector<uint8_t> verdicts;
+    std::atomic<uint64_t> n_batches{0}, n_proofs{0};
+
+    void deliver(std::vector<Req*>& reqs, int rc, const uint8_t* v) {
+        std::lock_guard<std::mutex> g(mu);
+        size_t off = 0;
+        for (Req* r : reqs) {
+            r->rc = rc;
+            if (!rc && r->n) std::memcpy(r->verdicts, v + off, r->n);
+            off += r->n;
+            r->done = true;
+        }
+        reqs.clear();
+        cv_out.notify_all();
+    }
+
+    void finish(int s) {
+        if (!in_flight[s]) return;
+        in_flight[s] = false;
+        size_t n = 0;
+        for (Req* r : in_slot[s]) n += r->n;
+        verdicts.assign(n ? n : 1, 0);
+        const int rc = nhip_batch_wait(ctx, slot[s], verdicts.data(), nullptr);
+        deliver(in_slot[s], rc, verdicts.data());
+    }
+
+    // stage + launch the requests in in_slot[s]
+    void launch(int s) {
+        claims.clear();
+        proofs.clear();
+        for (Req* r : in_slot[s])
+            for (size_t i = 0; i < r->n; ++i) {
+                claims.push_back(r->claims[i]);
+                proofs.push_back(r->proofs[i]);
+            }
+        int rc = slot[s] ? nhip_batch_refill(ctx, slot[s], air, &params, claims.data(), proofs.data(), claims.size())
+                         : nhip_batch_prepare(ctx, air, &params, claims.data(), proofs.data(), claims.size(), &slot[s]);
+        if (!rc) rc = nhip_batch_launch(ctx, slot[s]);
+        if (rc) {
+            deliver(in_slot[s], rc, nullptr);
+            return;
+        }
+        in_flight[s] = true;
+        ++n_batches;
+        n_proofs += claims.size();
+    }
+
+    void run() {
+        int s = 0;
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            if (pending.empty()) {
+                if (in_flight[s ^ 1]) {  // nothing new: complete the batch on the device first
+                    lk.unlock();
+                    finish(s ^ 1);
+                    lk.lock();
+                    continue;
+                }
+                cv_in.wait(lk, [&] { return stop || !pending.empty(); });
+                if (pending.empty()) break;  // stop, drained
+            }
+            // coalescing window from the oldest request's arrival, ended early by a full batch
+            const Clock::time_point deadline = pending.front()->arrived + max_wait;
+            cv_in.wait_until(lk, deadline, [&] { return stop || pending_proofs >= max_batch; });
+            size_t taken = 0;
+            while (!pending.empty() && (taken == 0 || taken + pending.front()->n <= max_batch)) {
+                Req* r = pending.front();
+                pending.pop_front();
+                pending_proofs -= r->n;
+                taken += r->n;
+                in_slot[s].push_back(r);
+            }
+            lk.unlock();
+            try {
+                launch(s);
+            } catch (const std::bad_alloc&) {
+                deliver(in_slot[s], NHIP_ERR_OOM, nullptr);
+            }
+            finish(s ^ 1);
+            s ^= 1;
+            lk.lock();
+        }
+        lk.unlock();
+        finish(s ^ 1);
+        finish(s);
+    }
+};
+
+extern "C" {
+
+int nhip_queue_create(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* params, uint32_t max_batch,
+                      uint32_t max_wait_us, nhip_queue** out) {
+    if (!ctx || !air || !params || !out) return NHIP_ERR_ARG;
+    *out = nullptr;
+    nhip_queue* q = new (std::nothrow) nhip_queue();
+    if (!q) return NHIP_ERR_OOM;
+    q->ctx = ctx;
+    q->air = air;
+    q->params = *params;
+    q->max_batch = max_batch ? max_batch : 4096;
+    q->max_wait = std::chrono::microseconds(max_wait_us);
+    try {
+        q->worker = std::thread([q] { q->run(); });
+    } catch (const std::system_error&) {
+        delete q;
+        return NHIP_ERR_HIP;
+    }
+    *out = q;
+    return NHIP_OK;
+}
+
+int nhip_queue_verify(nhip_queue* q, const nhip_claim* claims, const nhip_proof* proofs, size_t n,
+                      uint8_t* verdicts) {
+    if (!q || (n && (!claims || !proofs || !verdicts))) return NHIP_ERR_ARG;
+    if (n == 0) return NHIP_OK;
+    // argument errors stay this caller's: checked here, before the proofs join a shared batch
+    for (size_t i = 0; i < n; ++i)
+        if ((proofs[i].len && !proofs[i].words) || (claims[i].input_len && !claims[i].input) ||
+            (claims[i].output_len && !claims[i].output) || claims[i].input_len > 0xFFFFFFFFull ||
+            claims[i].output_len > 0xFFFFFFFFull)
+            return NHIP_ERR_ARG;
+    Req r{claims, proofs, n, verdicts, Clock::now()};
+    std::unique_lock<std::mutex> lk(q->mu);
+    if (q->stop) return NHIP_ERR_ARG;
+    try {
+        q->pending.push_back(&r);
+    } catch (const std::bad_alloc&) {
+        return NHIP_ERR_OOM;
+    }
+    q->pending_proofs += n;
+    q->cv_in.notify_one();
+    q->cv_out.wait(lk, [&] { return r.done; });
+    return r.rc;
+}
+
+int nhip_queue_stats(const nhip_queue* q, uint64_t* batches, uint64_t* proofs) {
+    if (!q) return NHIP_ERR_ARG;
+    if (batches) *batches = q->n_batches.load();
+    if (proofs) *proofs = q->n_proofs.load();
+    return NHIP_OK;
+}
+
+void nhip_queue_destroy(nhip_queue* q) {
+    if (!q) return;
+    {
+        std::lock_guard<std::mutex> g(q->mu);
+        q->stop = true;
+    }
+    q->cv_in.notify_all();
+    q->worker.join();
+    for (nhip_batch* b : q->slot)
+        if (b) nhip_batch_destroy(b);
+    delete q;
+}
+
+}  // extern "C"

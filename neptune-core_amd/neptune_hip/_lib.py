@@ -106,6 +106,11 @@ SIGNATURES = {
     "nhip_proof_from_be_bytes": ([ctypes.c_void_p, _sz, ctypes.c_void_p, _sz, ctypes.POINTER(_sz)], ctypes.c_int),
     "nhip_proof_to_be_bytes": ([ctypes.c_void_p, _sz, ctypes.c_void_p], ctypes.c_int),
     "nhip_claim_hash": ([_vp, ctypes.POINTER(Claim), _u64p], ctypes.c_int),
+    "nhip_queue_create": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.c_uint32, ctypes.c_uint32,
+                           ctypes.POINTER(_vp)], ctypes.c_int),
+    "nhip_queue_verify": ([_vp, _vp, _vp, _sz, _vp], ctypes.c_int),
+    "nhip_queue_stats": ([_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+    "nhip_queue_destroy": ([_vp], None),
     "nhip_host_alloc": ([_sz, ctypes.POINTER(_vp)], ctypes.c_int),
     "nhip_host_free": ([_vp], ctypes.c_int),
     "nhip_host_register": ([_vp, _sz], ctypes.c_int),

@@ -183,6 +183,78 @@ def verify(ctx, air: Air, stark: Stark, claim: Claim, proof: Sequence[int]) -> b
     return verify_batch(ctx, air, stark, [(claim, proof)])[0]
 
 
+class Queue:
+    """Coalescing verifier for concurrent callers (``nhip_queue``): ``verify(claim, proof)`` from
+    any number of threads; the proofs of callers waiting at the same time are verified in one
+    device batch (ctypes releases the GIL during the blocking C call)."""
+
+    def __init__(self, ctx, air: Air, stark: Stark, max_batch: int = 0, max_wait_us: int = 200):
+        self.ctx, self.air, self.stark = ctx, air, stark
+        h = ctypes.c_void_p()
+        params = stark.c()
+        check(ctx.lib.nhip_queue_create(ctx.handle, air.handle, ctypes.byref(params), max_batch, max_wait_us,
+                                        ctypes.byref(h)), "nhip_queue_create")
+        self.handle = h.value
+
+    def verify_many(self, pairs: Sequence[Tuple[Claim, Sequence[int]]]) -> List[bool]:
+        m = _Marshal([c for c, _ in pairs], [p for _, p in pairs])
+        v = np.zeros(max(m.n, 1), dtype=np.uint8)
+        check(self.ctx.lib.nhip_queue_verify(self.handle, m.claims, m.proofs, m.n, v.ctypes.data), "nhip_queue_verify")
+        return [bool(x) for x in v[:m.n]]
+
+    def verify(self, claim: Claim, proof: Sequence[int]) -> bool:
+        return self.verify_many([(claim, proof)])[0]
+
+    def stats(self):
+        b, p = ctypes.c_uint64(), ctypes.c_uint64()
+        check(self.ctx.lib.nhip_queue_stats(self.handle, ctypes.byref(b), ctypes.byref(p)), "nhip_queue_stats")
+        return {"batches": b.value, "proofs": p.value}
+
+    def close(self):
+        if self.handle:
+            self.ctx.lib.nhip_queue_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class PinnedProofs:
+    """Proofs copied back to back into one pinned host buffer (``nhip_host_alloc``): batches
+    staged from them are DMA'd straight from this memory (no staging copy).  ``views`` are the
+    proofs as numpy arrays over the pinned buffer."""
+
+    def __init__(self, proofs: Sequence[Sequence[int]]):
+        self.lib = _lib.load()
+        arrs = [np.asarray(p, dtype=np.uint64) for p in proofs]
+        total = sum(a.size for a in arrs)
+        h = ctypes.c_void_p()
+        check(self.lib.nhip_host_alloc(max(total, 1) * 8, ctypes.byref(h)), "nhip_host_alloc")
+        self.ptr = h.value
+        buf = (ctypes.c_uint64 * max(total, 1)).from_address(self.ptr)
+        self.flat = np.frombuffer(buf, dtype=np.uint64, count=max(total, 1))
+        self.views, off = [], 0
+        for a in arrs:
+            self.flat[off:off + a.size] = a
+            self.views.append(self.flat[off:off + a.size])
+            off += a.size
+
+    def close(self):
+        if self.ptr:
+            self.views, self.flat = [], None
+            self.lib.nhip_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Group:
     """Several GPUs (or several contexts on one GPU) from one process: ``nhip_group``.
     ``Group([0, 1, 2, 3])`` or ``Group(mask=0)`` (every visible device)."""
