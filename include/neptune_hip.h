@@ -153,6 +153,9 @@ void nhip_stark_params_default(nhip_stark_params *out);
 int nhip_air_create(const uint64_t *words, size_t n_words, nhip_air **out);
 void nhip_air_destroy(nhip_air *air);
 int nhip_air_info(const nhip_air *air, uint32_t *num_nodes, uint32_t *num_levels, uint32_t *num_constraints);
+/* The OOD evaluator's value slots (liveness-allocated): those in LDS, and those past the LDS budget
+ * (~6K XFEs), which live in a per-proof global area (an AIR of triton-air's size class). */
+int nhip_air_slots(const nhip_air *air, uint32_t *lds_slots, uint32_t *global_slots);
 /* Host-only structural decode (no GPU needed): 1 = decodes, 0 = malformed, < 0 = bad argument. */
 int nhip_proof_decodes(const nhip_air *air, const nhip_stark_params *params, const nhip_claim *claim,
                        const nhip_proof *proof);

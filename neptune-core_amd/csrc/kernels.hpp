@@ -27,6 +27,8 @@ hipError_t launch_absolute_index_sets(const uint64_t* d_digests, const uint64_t*
 
 // ---- batched STARK verifier (stark_kernels.hip)
 static constexpr uint32_t AIR_LDS_HEADER = (256 + 4 + 4 + 4) * 24 + 16;  // red, zinv, derived, misc, flag
+static constexpr uint32_t AIR_LDS_BUDGET = 160 * 1024 - 8192;              // k_ood_air dynamic LDS cap
+static constexpr uint32_t AIR_LDS_SLOTS_MAX = (AIR_LDS_BUDGET - AIR_LDS_HEADER) / 24;
 
 // Level-synchronous Merkle multiproof plan (see k_mp_plan in stark_kernels.hip).  Ops of level l
 // live in MP_SHARDS shards (shard = proof index % MP_SHARDS) so the per-level slot reservations of
@@ -96,6 +98,9 @@ struct StarkBatchDev {
     const Xfe* air_consts;         // constant table (raw Montgomery)
     uint4 air_cons_off;            // constraint-type boundaries
     size_t air_lds_bytes;
+    uint32_t air_lds_slots;        // slots held in LDS
+    uint32_t air_gslot_n;          // slots past the LDS budget, per proof, in air_gslots
+    Xfe* air_gslots;               // [n_proofs][air_gslot_n]
 };
 
 // events: 0 start (after k_decode) | fs | rows | mp plan | mp hash levels | mp roots | ood | fri | deep | 9 verdicts

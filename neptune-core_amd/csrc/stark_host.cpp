@@ -410,6 +410,15 @@ int nhip_air_info(const nhip_air* a, uint32_t* num_nodes, uint32_t* num_levels, 
     return NHIP_OK;
 }
 
+// Slots of the compiled AIR program: held in LDS, and past the LDS budget (global memory).
+int nhip_air_slots(const nhip_air* a, uint32_t* lds_slots, uint32_t* global_slots) {
+    if (!a) return NHIP_ERR_ARG;
+    const uint32_t l = std::min<uint32_t>(a->slots, AIR_LDS_SLOTS_MAX);
+    if (lds_slots) *lds_slots = l;
+    if (global_slots) *global_slots = a->slots - l;
+    return NHIP_OK;
+}
+
 // Host-only structural check (no GPU): 1 if the proof stream decodes with the expected item
 // sequence and counts, else 0.  Used by CPU tests of the decoder and by callers that want to
 // reject garbage before touching a device.
@@ -681,7 +690,9 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
                          N1 * (1 + H.max_R) * k * 8,
                          N1 * (1 + H.max_R) * 4,
                          N1 * k * 8,
-                         N1 * H.max_last_cw * 40};
+                         N1 * H.max_last_cw * 40,
+                         // OOD slots past the LDS budget (an AIR larger than ~6K live XFEs)
+                         N1 * (size_t)(air->slots - std::min<uint32_t>(air->slots, AIR_LDS_SLOTS_MAX)) * 24 + 24};
     constexpr int NBUF = sizeof(sz) / sizeof(sz[0]);
     size_t total = 0;
     for (size_t x : sz) total += al(x);
@@ -763,9 +774,10 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     dv.air_n_levels = (uint32_t)air->prog_off.size() - 1;
     dv.air_consts = adev.d_consts;
     dv.air_cons_off = air->cons_off;
-    dv.air_lds_bytes = AIR_LDS_HEADER + (size_t)air->slots * 24;
-    if (dv.air_lds_bytes > 160 * 1024 - 8192)
-        return fail_out(NHIP_ERR_ARG);  // AIR too large for the single-workgroup LDS evaluator
+    dv.air_lds_slots = std::min<uint32_t>(air->slots, AIR_LDS_SLOTS_MAX);
+    dv.air_gslot_n = air->slots - dv.air_lds_slots;
+    dv.air_gslots = (Xfe*)ptr[21];
+    dv.air_lds_bytes = AIR_LDS_HEADER + (size_t)dv.air_lds_slots * 24;
     *out = b;
     return NHIP_OK;
 }

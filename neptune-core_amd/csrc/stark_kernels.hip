@@ -712,7 +712,8 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
                                                  const uint32_t* __restrict__ prog_off, uint32_t n_levels,
                                                  const Xfe* __restrict__ consts, uint4 cons_type_off,
                                                  const uint64_t* __restrict__ xs, uint64_t* __restrict__ ood_out,
-                                                 uint32_t* __restrict__ fail) {
+                                                 uint32_t* __restrict__ fail, uint32_t lds_slots,
+                                                 Xfe* __restrict__ gslots, uint32_t gslot_n) {
     // all LDS in the dynamic region (16-B aligned carve, no static __shared__ in front of it)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Xfe* red = reinterpret_cast<Xfe*>(smem);              // 256
@@ -722,6 +723,11 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
     uint32_t& zero_flag = *reinterpret_cast<uint32_t*>(misc + 4);
     Xfe* val = reinterpret_cast<Xfe*>(smem + AIR_LDS_HEADER);
     const uint32_t p = blockIdx.x, tid = threadIdx.x;
+    // slots [0, lds_slots) live in LDS, the rest (an AIR larger than the LDS budget) in this
+    // proof's global slot area; the slot allocator reuses low slots first, so the hot ones stay in
+    // LDS.  The barrier after each level orders the global writes for the workgroup as well.
+    Xfe* gval = gslots + (uint64_t)p * gslot_n;
+    auto slot = [&](uint32_t s) -> Xfe& { return s < lds_slots ? val[s] : gval[s - lds_slots]; };
     if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
     const ProofDesc& d = desc[p];
     const SampleLayout sl = SampleLayout::of(dims, d.R);
@@ -774,7 +780,7 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
     const uint32_t offs[5] = {0u, cons_type_off.x, cons_type_off.y, cons_type_off.z, cons_type_off.w};
     auto fetch = [&](uint32_t ref) -> Xfe {
         const uint32_t t = ref >> 30;
-        if (t == 0) return val[ref];
+        if (t == 0) return slot(ref);
         if (t == 1) return consts[ref & 0x3FFFFFFFu];
         const uint32_t kind = (ref >> 27) & 7u, i = ref & 0x7FFFFFFu;
         switch (kind) {
@@ -797,10 +803,10 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
                 const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.quot_w + c));
                 acc = x_add(acc, x_mul(w, x_mul(fetch(ins.a), zinv[t])));
             } else if (ins.op == OOD_LOAD) {
-                val[ins.dst] = fetch(ins.a);
+                slot(ins.dst) = fetch(ins.a);
             } else {
                 const Xfe x = fetch(ins.a), y = fetch(ins.b);
-                val[ins.dst] = ins.op == OOD_ADD ? x_add(x, y) : (ins.op == OOD_SUB ? x_sub(x, y) : x_mul(x, y));
+                slot(ins.dst) = ins.op == OOD_ADD ? x_add(x, y) : (ins.op == OOD_SUB ? x_sub(x, y) : x_mul(x, y));
             }
         }
         __syncthreads();
@@ -1179,7 +1185,8 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         (void)hipStreamWaitEvent(sa, tm->ev[10], 0);
         mark(11, sa);
         hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(256), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims, b.air_prog,
-                           b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs, b.ood, b.fail);
+                           b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs, b.ood, b.fail,
+                           b.air_lds_slots, b.air_gslots, b.air_gslot_n);
         mark(6, sa);
         hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
         mark(7, sa);
@@ -1226,7 +1233,7 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
 }
 
 hipError_t stark_set_kernel_attributes() {
-    hipError_t e = hipFuncSetAttribute((const void*)k_ood_air, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
+    hipError_t e = hipFuncSetAttribute((const void*)k_ood_air, hipFuncAttributeMaxDynamicSharedMemorySize, AIR_LDS_BUDGET);
     if (e != hipSuccess) return e;
     e = hipFuncSetAttribute((const void*)k_deep, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
     if (e != hipSuccess) return e;

@@ -15,16 +15,7 @@
 //   state[0..10]; padding appends a single 1 then zeros to a multiple of 10.
 #pragma once
 #include "goldilocks.hpp"
-#include "mont_asm.hpp"
 #include "tip5_constants.h"
-
-// 1: the x^7 S-box uses the hand-interleaved asm Montgomery products of mont_asm.hpp (16 VALU
-// instructions per product, no s_nop); 0 (default): the C mont_mul_n.  Measured on MI355X the asm
-// form issues 1.7% fewer VALU instructions per permutation (SQ_INSTS_VALU) yet runs 3% slower
-// (k_mtree_verify 4.58 vs 4.74e9 perms/s; full batch 6.33 vs 6.05 ms), so it stays off.
-#ifndef NHIP_MM_ASM
-#define NHIP_MM_ASM 0
-#endif
 
 namespace nhip {
 
@@ -87,14 +78,7 @@ __device__ __forceinline__ uint64_t pow7(uint64_t x) {
 #endif
 template <int G>
 __device__ __forceinline__ void pow7_mul(const uint64_t* a, const uint64_t* b, uint64_t* out) {
-#if NHIP_MM_ASM
-    static_assert(G == 3 || G == 4 || G == 6, "asm widths generated by tools/gen_mont_asm.py");
-    if constexpr (G == 3) mont_mul3_asm(a, b, out);
-    else if constexpr (G == 4) mont_mul4_asm(a, b, out);
-    else mont_mul6_asm(a, b, out);
-#else
     mont_mul_n<G>(a, b, out);
-#endif
 }
 
 __device__ __forceinline__ void pow7_12(uint64_t* x) {

@@ -103,6 +103,7 @@ SIGNATURES = {
     "nhip_air_destroy": ([_vp], None),
     "nhip_air_info": ([_vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                        ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+    "nhip_air_slots": ([_vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
     "nhip_proof_from_be_bytes": ([ctypes.c_void_p, _sz, ctypes.c_void_p, _sz, ctypes.POINTER(_sz)], ctypes.c_int),
     "nhip_proof_to_be_bytes": ([ctypes.c_void_p, _sz, ctypes.c_void_p], ctypes.c_int),
     "nhip_claim_hash": ([_vp, ctypes.POINTER(Claim), _u64p], ctypes.c_int),
@@ -184,6 +185,8 @@ def load() -> ctypes.CDLL:
                             "(or __graft_entry__.build()); there is no CPU fallback")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (args, res) in SIGNATURES.items():
+            if os.environ.get("NHIP_LIB") and not hasattr(lib, name):
+                continue  # an older build loaded for an A/B comparison
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = res

@@ -62,7 +62,10 @@ class Air:
     def info(self):
         a, b, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
         check(self.lib.nhip_air_info(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "air_info")
-        return {"nodes": a.value, "levels": b.value, "constraints": c.value}
+        lds, glob = ctypes.c_uint32(), ctypes.c_uint32()
+        check(self.lib.nhip_air_slots(self.handle, ctypes.byref(lds), ctypes.byref(glob)), "air_slots")
+        return {"nodes": a.value, "levels": b.value, "constraints": c.value, "lds_slots": lds.value,
+                "global_slots": glob.value}
 
     def __del__(self):
         try:

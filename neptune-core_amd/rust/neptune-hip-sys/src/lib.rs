@@ -158,6 +158,7 @@ extern "C" {
     pub fn nhip_air_destroy(air: *mut nhip_air);
     pub fn nhip_air_info(air: *const nhip_air, num_nodes: *mut u32, num_levels: *mut u32,
                          num_constraints: *mut u32) -> c_int;
+    pub fn nhip_air_slots(air: *const nhip_air, lds_slots: *mut u32, global_slots: *mut u32) -> c_int;
     pub fn nhip_proof_decodes(air: *const nhip_air, params: *const nhip_stark_params,
                               claim: *const nhip_claim, proof: *const nhip_proof) -> c_int;
     pub fn nhip_host_alloc(bytes: usize, out: *mut *mut c_void) -> c_int;

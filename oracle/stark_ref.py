@@ -600,6 +600,54 @@ def synth_air(params: StarkParams, num_sampled: int = CHALLENGE_SAMPLE_COUNT, se
     return air, recipe
 
 
+def bloat_air(air: AirCircuit, target_nodes: int, seed: int = 0xB10A7, max_degree: int = 4) -> AirCircuit:
+    """The same AIR (every constraint has the same value on every input) as a circuit of about
+    `target_nodes` nodes, for tests of the evaluator at triton-air's size class (~600 constraints
+    over ~20-30k nodes after degree lowering).  Each constraint C becomes C + sum_t (m_t - m_t'),
+    where m_t and m_t' are one random monomial of degree <= max_degree over OOD-row inputs and
+    challenges, multiplied in two different orders: identically zero, so the synthetic prover's
+    quotients (from the recipe) still satisfy it, but every term is real work for the verifier
+    (loads, products, a subtraction, an accumulation)."""
+    rng = _SplitMix(seed)
+    nodes = list(air.nodes)
+    cache = {t: i for i, t in enumerate(nodes)}
+
+    def node(t):
+        if t not in cache:
+            cache[t] = len(nodes)
+            nodes.append(t)
+        return cache[t]
+
+    kinds = [(INPUT_MAIN_CURR, air.num_main), (INPUT_AUX_CURR, air.num_aux), (INPUT_MAIN_NEXT, air.num_main),
+             (INPUT_AUX_NEXT, air.num_aux), (INPUT_CHALLENGE, air.num_challenges)]
+
+    def rand_input():
+        k, n = kinds[rng.below(len(kinds))]
+        return node((OP_INPUT, k, rng.below(n), 0))
+
+    def product(fs):
+        acc = fs[0]
+        for f in fs[1:]:
+            acc = node((OP_MUL, acc, f, 0))
+        return acc
+
+    n_cons = air.num_constraints
+    per = max(1, (target_nodes - len(nodes)) // max(1, 6 * n_cons))
+    cons = []
+    for cs in air.constraints:
+        out = []
+        for c in cs:
+            acc = c
+            for _ in range(per):
+                fs = [rand_input() for _ in range(2 + rng.below(max_degree - 1))]
+                rev = fs[::-1] if len(fs) > 2 else [fs[1], fs[0]]
+                diff = node((OP_SUB, product(fs), product(rev), 0))
+                acc = node((OP_ADD, acc, diff, 0))
+            out.append(acc)
+        cons.append(out)
+    return AirCircuit(air.num_main, air.num_aux, air.num_sampled, nodes, cons)
+
+
 # ====================================================================== verifier
 def zerofier_inverses(z, padded_height):
     w = primitive_root_of_unity(padded_height)
