@@ -288,6 +288,56 @@ def tip5_paths(ctx, log2_leaves: int, steps: int):
             "valu_frac": perms_s * TIP5_VALU_OPS_PER_PERM / VALU_PEAK_LANE_OPS, "verdicts_correct": ok}
 
 
+# ------------------------------------------------------------------ proofs arriving in host memory
+def pcie_stream(ctx, gair, stark, claims, proofs, expect, batches: int):
+    """The PCIe-inclusive rate (never `value`): the same batch arriving from host memory, as a node
+    receiving proofs would feed the verifier.  The proofs sit in pinned host memory
+    (nhip_host_alloc), so each refill is a DMA straight from it; two batches alternate refill /
+    launch / wait, so each upload overlaps the other batch's device run.  Beside it the raw
+    host-to-device rate of one copy of the same bytes: the link's measured ceiling."""
+    import neptune_hip.stark as NS
+    pinned = NS.PinnedProofs(proofs)
+    ncl = [NS.Claim(*c) for c in claims]
+    nbytes = sum(len(p) for p in proofs) * 8
+    # raw DMA of the proof bytes, pinned -> device (best of 3)
+    dbuf = ctx.alloc(nbytes)
+    raw = []
+    for _ in range(3):
+        t = time.perf_counter()
+        dbuf.upload(pinned.flat)
+        raw.append(nbytes / (time.perf_counter() - t))
+    dbuf.free()
+    a = NS.Batch(ctx, gair, stark, ncl, pinned.views)
+    b = NS.Batch(ctx, gair, stark, ncl, pinned.views)
+    a.run()
+    ok = True
+    t = time.perf_counter()
+    cur, nxt = a, b
+    cur.refill(ncl, pinned.views)
+    cur.launch()
+    for _ in range(batches - 1):
+        nxt.refill(ncl, pinned.views)
+        v, _ = cur.wait()
+        ok = ok and bool((np.asarray(v, dtype=bool) == expect).all())
+        nxt.launch()
+        cur, nxt = nxt, cur
+    v, _ = cur.wait()
+    dt = time.perf_counter() - t
+    ok = ok and bool((np.asarray(v, dtype=bool) == expect).all())
+    st = a.stats()
+    a.close()
+    b.close()
+    pinned.close()
+    h2d = nbytes * batches / dt
+    peak = max(raw)
+    return {"value": len(proofs) * batches / dt, "unit": "proofs/s", "batches": batches,
+            "proof_bytes_per_batch": nbytes, "h2d_GBps": h2d / 1e9, "h2d_peak_GBps": peak / 1e9,
+            "frac_of_h2d_peak": h2d / peak, "bound": "pcie (host-to-device DMA)",
+            "refill_ms": {"host_stage": st["ms_decode"], "upload_wait": st["ms_upload"]},
+            "verdicts_correct": ok,
+            "measured": f"{batches} batches from pinned host memory, 2 alternating (refill overlaps the other's run)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)

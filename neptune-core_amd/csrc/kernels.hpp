@@ -103,7 +103,7 @@ struct StarkBatchDev {
     Xfe* air_gslots;               // [n_proofs][air_gslot_n]
 };
 
-// events: 0 start (after k_decode) | fs | rows | mp plan | mp hash levels | mp roots | ood | fri | deep | 9 verdicts
+// events: 0 start (after k_decode, aux stream) | fs | rows | mp plan | mp hash levels | mp roots | ood | fri | deep | 9 verdicts
 // 10: main stream at the aux-chain release point, 11: aux stream after that wait, 12: before k_decode
 static constexpr int STARK_EVENTS = 13;
 struct StarkPhaseTimer {

@@ -1143,13 +1143,18 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     const uint32_t k = b.dims.num_checks;
     const uint32_t tpp = 4 + b.max_R;
     auto mark = [&](int i, hipStream_t s) { (void)hipEventRecord(tm->ev[i], s); };
-    // proof-stream decode of every proof (descriptors, Fiat-Shamir programs, fail words)
+    // fork: the aux stream starts after everything already queued on st (counter resets)
     mark(12, st);
-    hipLaunchKernelGGL(k_decode, dim3(n), dim3(64), 0, st, b.words, b.in, n, b.D, b.fs_stride, b.xs_stride, b.desc,
+    (void)hipStreamWaitEvent(sa, tm->ev[12], 0);
+    // proof-stream decode of every proof (descriptors, Fiat-Shamir programs, fail words), on the
+    // aux stream: the Fiat-Shamir replay is the next packet of that queue, so it is dispatched
+    // the moment decode ends, before the row hashing (main stream, waiting on the same event) can
+    // fill the CUs.  Decoding on the main stream instead let k_hash_rows take every wave slot first
+    // and stretched the latency-bound sponge replay 1.6 -> 5.0 ms (config 4, one step in flight).
+    hipLaunchKernelGGL(k_decode, dim3(n), dim3(64), 0, sa, b.words, b.in, n, b.D, b.fs_stride, b.xs_stride, b.desc,
                        b.ops, b.fail, b.counters);
-    // fork: the aux stream starts after everything already queued on st (counter reset, decode)
-    mark(0, st);
-    (void)hipStreamWaitEvent(sa, tm->ev[0], 0);
+    mark(0, sa);
+    (void)hipStreamWaitEvent(st, tm->ev[0], 0);
     // ---- aux stream: latency-bound chain
     // small batches: the sponge replay is the critical path and most SIMDs are idle, so two rows
     // per proof (pair form) for a shorter permutation; large ones: one row per proof (fewer
