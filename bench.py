@@ -2,33 +2,34 @@
 """bench.py — batched STARK verification on MI355X (BASELINE.json metric: STARK proofs verified/s
 + Tip5 permutations/s vs the VALU roofline).
 
-Workload per GPU (BASELINE config 3): 256 synthetic ProofCollections x 8 member proofs with log2
-padded heights {16, 10, 11, 12, 12, 11, 9, 9} = 2,048 STARK verifications with Stark::default()
-parameters (security 160, expansion 4, 80 collinearity checks, 379 main / 88 aux columns, 4
-quotient segments), each through the full verifier: Fiat-Shamir replay, row hashing, Merkle
-multiproofs, out-of-domain AIR evaluation, FRI, DEEP.  5% of the collections carry one flipped word
-(in one member's MainRows payload) and must reject.  The proofs are one accepting synthetic proof per
-padded height from tests/golden/c3_pool.npz (made by tests/golden/make_bench_pool.py), each
-collection member stored separately in HBM.
+Workload (default, BASELINE config 4, the north-star workload): 4,096 transaction proofs with log2
+padded heights drawn uniformly (seed 0xC4) from the ProofCollection member mix {16, 10, 11, 12, 12,
+11, 9, 9}, 1% with one flipped MainRows word (must reject), LPT-sharded over the ranks by estimated
+Tip5 cost, Stark::default() parameters (security 160, expansion 4, 80 collinearity checks, 379 main /
+88 aux columns, 4 quotient segments).  The proofs are the accepting synthetic proofs of
+tests/golden/c3_pool.npz (made by tests/golden/make_bench_pool.py), each stored separately in HBM.
 
-One step = every device phase over one resident batch + the verdict copy back (nhip_batch_launch /
-nhip_batch_wait) and, for N > 1, the batch verdict AND over ranks with one RCCL all-reduce(MIN) —
-the path's only exchange.  Steps are pipelined as a node verifying a stream of
-batches would run them (--inflight 2, default): two resident copies of the batch alternate, step k+1
-is launched before step k is waited on, so one step's latency-bound phases (Fiat-Shamir replay,
-Merkle plan, top Merkle levels) overlap the other's VALU-bound hashing.  Every timed step is
-launched and waited inside the timed region.  Two copies x 2 streams need more than HIP's default 4
-hardware queues per process (streams sharing a queue serialize), so GPU_MAX_HW_QUEUES defaults to 8
-here.  Every rank owns its own 2,048-proof batch (weak scaling).  Host decode +
-upload (nhip_batch_prepare) happens before the timed region and is reported separately.
+One step = whole verification of the rank's batch from its raw proof words in HBM: the proof-stream
+decode on the device (k_decode: ProofStream::try_from + the dequeue order of Stark::verify, every
+step again), Fiat-Shamir replay, row hashing, Merkle multiproofs, OOD AIR evaluation, FRI, DEEP, the
+verdict copy back (nhip_batch_launch / nhip_batch_wait) and, for N > 1, the batch verdict AND over
+ranks with one RCCL all-reduce(MIN) plus the all-gather of the per-proof verdicts (block validation
+needs every transaction's verdict: SURVEY.md §8e).  Steps are pipelined as a node verifying a stream
+of batches runs them (--inflight 2): resident copies alternate, step k+1 is launched before step k
+is waited on, so one step's latency-bound phases overlap the other's VALU-bound hashing; every timed
+step is launched and waited inside the timed region.  Two copies x 2 streams need more than HIP's
+default 4 hardware queues per process, so GPU_MAX_HW_QUEUES defaults to 8 here.
 
-roofline: the dominant kernel, k_mp_hash (the per-level Merkle hash_pair launches), as Tip5
-VALU lane-ops/s against the gfx950 VALU peak, timed over the timed region (sharing the chip with the
-other step in flight); roofline_isolated: the same kernel in steps run one at a time; `tip5_paths` adds the config-2 Tip5 path microbench.
-cpu_baseline: the C restatement of the verifier (oracle/stark_oracle.c), one proof per host thread,
-over a bounded sample of this batch's proofs (the reference, Rust triton-vm, cannot be built here).
+Beside `value` (HBM-resident input, the contract):
+  pcie_inclusive: the same batch arriving from host memory (pinned, DMA'd per refill, two batches
+    alternating) with the host-to-device link's measured ceiling; never `value`.
+  roofline: the dominant kernel, the per-level Merkle hash launches (k_mp_hash), as Tip5 VALU
+    lane-ops/s against the gfx950 VALU peak over the timed region.
+  tip5_paths: the config-2 Tip5 path microbench.
+  cpu_baseline: the C restatement of the verifier (oracle/stark_oracle.c), one proof per host thread,
+    over a bounded sample of this batch's proofs (the reference, Rust triton-vm, cannot be built here).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config {3,4,5}]
        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -42,11 +43,11 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+ISO_STEPS = 5
 # before anything initialises HIP: 2 batches x 2 streams + the context stream (see above); the GPU
 # boxes export HIP's default of 4, which would put two streams on one queue
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
-ISO_STEPS = 5
 sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
 
 P = (1 << 64) - (1 << 32) + 1
@@ -63,13 +64,26 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(kernel: str):
+def latest_profile(config: int):
+    """profiles/LATEST = '<tag> <config>': the committed rocprofv3 PMC passes and the BASELINE
+    config they were taken on (none for another config)."""
+    try:
+        parts = open(os.path.join(ROOT, "profiles", "LATEST")).read().split()
+    except OSError:
+        return None
+    tag, cfg = parts[0], int(parts[1]) if len(parts) > 1 else 3
+    return tag if cfg == config else None
+
+
+def pmc_traffic(kernel: str, config: int):
     """HBM bytes per launch of `kernel` from the latest committed rocprofv3 PMC passes
     (profiles/LATEST -> profiles/<tag>/pmc_{fetch,write}_counter_collection.csv), raw
     (FETCH_SIZE + WRITE_SIZE) x 1024; None when absent."""
     import csv
+    tag = latest_profile(config)
+    if tag is None:
+        return None, None
     try:
-        tag = open(os.path.join(ROOT, "profiles", "LATEST")).read().strip()
         tot = 0.0
         for part, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
             vals = [float(r["Counter_Value"]) for r in
@@ -81,13 +95,15 @@ def pmc_traffic(kernel: str):
         return None, None
 
 
-def pmc_valu_per_step():
+def pmc_valu_per_step(config: int):
     """Wave-level VALU instructions one config-3 step issues, from the latest committed PMC pass
     (profiles/<LATEST>/pmc_valu_counter_collection.csv: SQ_INSTS_VALU summed over a step's
     dispatches, microbench kernels excluded; steps = k_hash_rows dispatches); None when absent."""
     import csv
+    tag = latest_profile(config)
+    if tag is None:
+        return None, None
     try:
-        tag = open(os.path.join(ROOT, "profiles", "LATEST")).read().strip()
         tot, steps = 0.0, 0
         for r in csv.DictReader(open(os.path.join(ROOT, "profiles", tag, "pmc_valu_counter_collection.csv"))):
             k = r["Kernel_Name"]
@@ -100,13 +116,15 @@ def pmc_valu_per_step():
         return None, None
 
 
-def pmc_bytes_per_step():
+def pmc_bytes_per_step(config: int):
     """HBM bytes (raw FETCH_SIZE + WRITE_SIZE, x 1024) one config-3 step moves, summed over the step's
     dispatches in the latest committed PMC passes (microbench and runtime copy kernels excluded;
     steps = k_hash_rows dispatches); None when absent."""
     import csv
+    tag = latest_profile(config)
+    if tag is None:
+        return None, None
     try:
-        tag = open(os.path.join(ROOT, "profiles", "LATEST")).read().strip()
         tot, steps = 0.0, 0
         for part, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
             n_rows = 0
@@ -310,13 +328,14 @@ def pcie_stream(ctx, gair, stark, claims, proofs, expect, batches: int):
     a = NS.Batch(ctx, gair, stark, ncl, pinned.views)
     b = NS.Batch(ctx, gair, stark, ncl, pinned.views)
     a.run()
+    m = NS.marshal(ncl, pinned.views)  # the C arrays, built once (a node's receive loop fills them in place)
     ok = True
     t = time.perf_counter()
     cur, nxt = a, b
-    cur.refill(ncl, pinned.views)
+    cur.refill(None, marshalled=m)
     cur.launch()
     for _ in range(batches - 1):
-        nxt.refill(ncl, pinned.views)
+        nxt.refill(None, marshalled=m)
         v, _ = cur.wait()
         ok = ok and bool((np.asarray(v, dtype=bool) == expect).all())
         nxt.launch()
@@ -342,11 +361,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3, choices=(3, 4, 5),
-                    help="3: 256 ProofCollections (2,048 proofs) per GPU, weak scaling (default); 4: 4,096 mixed "
-                         "proofs over all ranks, strong scaling; 5: 64 proofs at log2 padded height 23 over all "
-                         "ranks, strong scaling")
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=4, choices=(3, 4, 5),
+                    help="4 (default, the north-star workload): 4,096 mixed transaction proofs over all ranks, "
+                         "LPT-sharded, strong scaling; 3: 256 ProofCollections (2,048 proofs) per GPU, weak "
+                         "scaling; 5: 64 proofs at log2 padded height 23 over all ranks, strong scaling")
     ap.add_argument("--proofs", type=int, default=None, help="config 4 / 5 total proofs (4096 / 64)")
     ap.add_argument("--log2-height", type=int, default=23, help="config 5 padded height")
     ap.add_argument("--collections", type=int, default=256)
@@ -355,15 +374,12 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
-    ap.add_argument("--pipeline", type=int, default=1,
-                    help="split the per-GPU batch into this many sub-batches (whole collections) launched "
-                         "back to back on their own streams (measured slower: 2 -> 9.7 ms vs 6.6 ms, probably because the 4 HW "
-                         "queues per process serialize the extra streams; DESIGN.md §3)")
+    ap.add_argument("--stream-batches", type=int, default=6,
+                    help="PCIe-inclusive leg: batches streamed from pinned host memory (0 = skip)")
     ap.add_argument("--inflight", type=int, default=None, choices=(1, 2, 3),
                     help="R > 1: R resident copies of the batch in rotation, up to R steps in flight (step k+1 is "
                          "launched before step k is waited on, so its row hashing fills step k's latency-bound "
-                         "phases). Default: 2 for >= 2,048 proofs per GPU, 3 below (smaller batches are more "
-                         "latency-bound: 512 proofs 205k -> 232k proofs/s, 1,024 307k -> 321k; 2,048 364k -> 354k)")
+                         "phases). Default: 2 for >= 2,048 proofs per GPU, 3 below")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -409,57 +425,38 @@ def main():
     t0 = time.time()
     gair = NS.Air([int(w) for w in air_words])
     stark = NS.Stark.default()
-    unit = len(COLLECTION_HEIGHTS) if args.config == 3 else 1  # split on whole collections
-    n_units = n // unit
-    P = max(1, min(args.pipeline, n_units))
-    cuts = [n_units * i // P * unit for i in range(P + 1)]
-    batches = [NS.Batch(ctx, gair, stark, [NS.Claim(*c) for c in claims[a:b]], proofs[a:b])
-               for a, b in zip(cuts[:-1], cuts[1:])]
-    prep_s = time.time() - t0
-    st0 = [b.stats() for b in batches]
-    log(f"[rank {rank}] batch ready: {n} proofs in {P} sub-batches, {sum(x['proof_words'] for x in st0)} words, "
-        f"prepare {prep_s:.2f}s (decode {sum(x['ms_decode'] for x in st0):.0f} ms, "
-        f"upload {sum(x['ms_upload'] for x in st0):.0f} ms)")
-
+    ncl = [NS.Claim(*c) for c in claims]
     R = args.inflight or (2 if n >= 2048 else 3)
-    ring = [batches] + [[NS.Batch(ctx, gair, stark, [NS.Claim(*c) for c in claims[a:b]], proofs[a:b])
-                         for a, b in zip(cuts[:-1], cuts[1:])] for _ in range(R - 1)]
+    # R resident copies of the raw proof words (each step decodes them on the device again)
+    ring = [NS.Batch(ctx, gair, stark, ncl, proofs) for _ in range(R)]
+    prep_s = time.time() - t0
+    st0 = ring[0].stats()
+    log(f"[rank {rank}] batch ready: {n} proofs x {R} resident copies, {st0['proof_words']} words, "
+        f"prepare {prep_s:.2f}s (host stage {st0['ms_decode']:.0f} ms, upload wait {st0['ms_upload']:.0f} ms)")
+
     launched = []   # ring slots in flight, oldest first
     next_slot = [0]
-
-    def launch_next():
-        for b in ring[next_slot[0]]:
-            b.launch()
-        launched.append(next_slot[0])
-        next_slot[0] = (next_slot[0] + 1) % R
-
-    last_waited = [batches]
     to_launch = [0]  # launches left in the current region: each region starts and ends with nothing in flight
+    gathered = [None]
 
     def run_all():
         # keep up to R steps in flight (one per resident copy), then wait for the oldest
         while to_launch[0] and len(launched) < R:
-            launch_next()
+            ring[next_slot[0]].launch()
+            launched.append(next_slot[0])
+            next_slot[0] = (next_slot[0] + 1) % R
             to_launch[0] -= 1
-        cur = ring[launched.pop(0)]
-        last_waited[0] = cur
-        vs, ok = [], True
-        for b in cur:
-            v, o = b.wait()
-            vs.append(v)
-            ok = ok and o
-        return np.concatenate(vs), ok
-
-
-    gathered = [None]
+        b = ring[launched.pop(0)]
+        v, ok = b.wait()
+        return b, v, ok
 
     def step():
-        v, ok = run_all()
+        b, v, ok = run_all()
         if dist is not None:
             ok = shard.all_ok(ok, dist)  # RCCL all-reduce(MIN) of the batch verdict
             if shards is not None:  # block validation: every rank gets every proof's verdict
                 gathered[0] = shard.gather_verdicts(v, shards, total, dist)
-        return ok
+        return b, v, ok
 
     def barrier_sync():
         ctx.synchronize()
@@ -469,37 +466,34 @@ def main():
             dist.barrier()
 
     to_launch[0] = args.warmup
-    for i in range(args.warmup):
+    for _ in range(args.warmup):
         step()
     barrier_sync()
     acc = {}
     batch_ok = None
+    correct = True
     t_start = time.perf_counter()
-    to_launch[0] = args.steps  # every timed step is launched and waited inside the region
-    for i in range(args.steps):
-        batch_ok = step()
-        for b in last_waited[0]:
-            for k, v in b.stats().items():
-                acc[k] = acc.get(k, 0.0) + v
+    to_launch[0] = args.steps  # every timed step is launched and waited inside the timed region
+    for _ in range(args.steps):
+        b, v, batch_ok = step()
+        correct = correct and bool((np.asarray(v, dtype=bool) == expect).all())
+        if gathered[0] is not None:
+            correct = correct and bool((gathered[0].astype(bool) == expect_all).all())
+        for k, x in b.stats().items():
+            acc[k] = acc.get(k, 0.0) + x
     barrier_sync()
     elapsed = time.perf_counter() - t_start
-
-    to_launch[0] = 1
-    v, _ = run_all()
-    correct = bool((np.asarray(v, dtype=bool) == expect).all())
-    # the same kernels with nothing else on the device: ISO_STEPS steps one at a time (with steps in
-    # flight the hash launches share the chip with the next step's kernels, which stretches them)
-    acc_iso = {}
-    if R > 1:
+    # the same steps one at a time (nothing else on the device): the kernel's own roofline
+    acc_iso, iso_ms = {}, 0.0
+    if R > 1 and ISO_STEPS:
+        t_iso = time.perf_counter()
         for _ in range(ISO_STEPS):
-            for b in batches:
-                b.launch()
-            for b in batches:
-                b.wait()
-                for k, val in b.stats().items():
-                    acc_iso[k] = acc_iso.get(k, 0.0) + val
-    if gathered[0] is not None:
-        correct = correct and bool((gathered[0].astype(bool) == expect_all).all())
+            ring[0].launch()
+            ring[0].wait()
+            for k, x in ring[0].stats().items():
+                acc_iso[k] = acc_iso.get(k, 0.0) + x
+        iso_ms = (time.perf_counter() - t_iso) / ISO_STEPS * 1e3
+
     if dist is not None:
         import torch
         t = torch.tensor([elapsed, 0.0 if correct else 1.0], dtype=torch.float64, device=shard._device_for(dist))
@@ -518,29 +512,41 @@ def main():
     K = args.steps
     avg = {k: v / K for k, v in acc.items()}
     perms = avg["tip5_perms_static"] + avg["tip5_perms_merkle"]
-    # the Merkle hash launches (k_mp_hash, and k_mp_hash_wide for levels of <= 48K ops) run back to
-    # back on the batch's main stream between two HIP events: their summed duration / launch count is
-    # the average launch duration (rocprofv3 cross-check: profiles/<tag>/SUMMARY.md, "Merkle hash
-    # launches" line)
-    traffic, traffic_tag = pmc_traffic("k_mp_hash")
+    step_ms = elapsed / K * 1e3
 
-    def roofline(a, steps, measured):
+    # roofline of the dominant kernel, the Merkle hash launches (k_mp_hash, + k_mp_hash_wide on the
+    # smallest levels): permutations per launch x the analytic VALU lane-ops per permutation / the
+    # average launch duration.  Each launch is timed by the HIP start / stop events of
+    # hipExtLaunchKernel on its stream (the dispatch's own begin / end timestamps, what the
+    # rocprofv3 kernel trace reports per dispatch).  `roofline`: over the timed region, where R
+    # steps are in flight and a launch shares the CUs with the other steps' kernels (so launches of
+    # different steps overlap: launches x average <= R x step time); `roofline_isolated`: the same
+    # launches in ISO_STEPS steps run one at a time after the timed region (launches x average <=
+    # the step time).  kernel_avg_ms_events: the HIP-event span of one step's back-to-back hash
+    # launches / launches (adds the dispatch gaps between levels).
+    traffic, traffic_tag = pmc_traffic("k_mp_hash", args.config)
+
+    def roofline(a, steps, step_ms_, overlap, measured):
         a = {k: v / steps for k, v in a.items()}
         launches = max(a["mp_hash_kernel_launches"], 1.0)
-        kern_avg_s = a["ms_mp_hash_kernel"] / launches / 1e3
+        kern_avg_s = a["ms_mp_hash_exec"] / launches / 1e3
+        kern_avg_ev_s = a["ms_mp_hash_kernel"] / launches / 1e3
         perms_per_launch = a["mp_hash_kernel_perms"] / launches
         achieved = perms_per_launch * TIP5_VALU_OPS_PER_PERM / kern_avg_s if kern_avg_s > 0 else 0.0
+        assert launches * kern_avg_s * 1e3 <= overlap * step_ms_ * 1.0001, (launches, kern_avg_s, step_ms_, overlap)
         return {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
                 "unit": "T VALU lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS, "traffic": traffic,
-                "traffic_unit": "bytes per launch (FETCH_SIZE+WRITE_SIZE, raw; see DESIGN.md §3)",
+                "traffic_unit": "bytes per launch (FETCH_SIZE+WRITE_SIZE, raw; see DESIGN.md §5)",
                 "traffic_profile": traffic_tag, "kernel": "k_mp_hash (+ k_mp_hash_wide on the smallest levels)",
-                "kernel_avg_ms": kern_avg_s * 1e3, "launches_per_step": launches,
-                "perms_per_launch": perms_per_launch, "valu_ops_per_perm": TIP5_VALU_OPS_PER_PERM,
-                # beside the spec peak: the measured integer issue ceiling (1 wave64 instruction per
-                # 4 clocks per SIMD = 64 lane-ops per instruction), DESIGN.md §3
+                "kernel_avg_ms": kern_avg_s * 1e3, "kernel_avg_ms_events": kern_avg_ev_s * 1e3,
+                "launches_per_step": launches, "perms_per_launch": perms_per_launch,
+                "valu_ops_per_perm": TIP5_VALU_OPS_PER_PERM, "step_ms": step_ms_,
+                # beside the spec peak: the measured integer issue ceiling (1 wave64 instruction
+                # per 4 clocks per SIMD = 64 lane-ops per instruction), DESIGN.md §3
                 "measured_ceiling": VALU_ISSUE_CEILING * 64 / 1e12,
                 "frac_of_measured_ceiling": achieved / (VALU_ISSUE_CEILING * 64),
                 "measured": measured}
+
     if args.config == 3:
         workload = (f"BASELINE config 3: {args.collections} ProofCollections x 8 proofs (log2 padded heights "
                     f"{COLLECTION_HEIGHTS}) = {n} STARK verifications per GPU, Stark::default()")
@@ -551,13 +557,13 @@ def main():
         workload = (f"BASELINE config 5: {total} proofs at log2 padded height {args.log2_height} (FRI domain "
                     f"2^{args.log2_height + 3}), sharded over {world} GPU(s), Stark::default()")
     res = {
-        "metric": "STARK proofs verified/s (BASELINE config 3 per GPU) + Tip5 perms/s vs VALU roofline",
+        "metric": "STARK proofs verified/sec (whole node) + Tip5 perms/sec vs VALU roofline",
         "value": total * K / elapsed,
         "unit": "proofs/s",
         "n_gpus": world,
         "steps": K,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / K * 1e3,
+        "ms_per_step": step_ms,
         "higher_is_better": True,
         "scaling": "weak" if args.config == 3 else "strong",
         "vs_baseline": None,
@@ -570,6 +576,10 @@ def main():
                  "column counts"),
         "config": {"workload": workload, "proofs_total": total, "proofs_rank0": n,
                    "parallelism": f"proof-sharded x{world}"},
+        # what one step is: the raw proof words are resident in HBM when the step starts; the step
+        # decodes every proof stream on the device (k_decode) and runs every verifier phase
+        "step": "device proof-stream decode + Fiat-Shamir replay + row hashing + Merkle multiproofs + OOD AIR + "
+                "FRI + DEEP + verdicts back to the host",
         "verdicts_correct": correct,
         "batch_verdict": batch_ok,
         "expected_rejects_rank0": int((~expect).sum()),
@@ -579,42 +589,44 @@ def main():
         # replay, rows, Merkle levels) x the analytic VALU lane-ops per permutation, per second of
         # wall time, against the VALU peak
         "tip5_valu_frac": perms_job * K / elapsed * TIP5_VALU_OPS_PER_PERM / (VALU_PEAK_LANE_OPS * world),
-        # per sub-batch (each sub-batch's phases are timed by HIP events on its own two streams)
-        "phase_ms": {k[3:]: round(avg[k] / P, 4) for k in ("ms_device_decode", "ms_fiat_shamir", "ms_row_hash", "ms_merkle",
-                                                            "ms_merkle_hash", "ms_ood_air", "ms_fri", "ms_deep",
-                                                            "ms_device_total")},
-        "host_prepare_ms": {"decode": sum(x["ms_decode"] for x in st0), "upload": sum(x["ms_upload"] for x in st0),
-                            "total": prep_s * 1e3},
-        "pipeline_sub_batches": P,
+        "phase_ms": {k[3:]: round(avg[k], 4) for k in ("ms_device_decode", "ms_fiat_shamir", "ms_row_hash",
+                                                       "ms_merkle", "ms_merkle_hash", "ms_ood_air", "ms_fri",
+                                                       "ms_deep", "ms_device_total")},
+        "host_prepare_ms": {"stage": st0["ms_decode"], "upload_wait": st0["ms_upload"], "total": prep_s * 1e3},
         "inflight": R,
-        "roofline": roofline(acc, K, f"HIP events over the timed region ({R} step(s) in flight)"),
+        "roofline": roofline(acc, K, step_ms, R, f"timed region, {R} step(s) in flight; per-launch HIP events "
+                                                 f"(hipExtLaunchKernel start/stop)"),
     }
     if acc_iso:
-        res["roofline_isolated"] = roofline(acc_iso, ISO_STEPS, f"{ISO_STEPS} steps one at a time after the timed region")
-    valu_step, valu_tag = pmc_valu_per_step()
-    if args.config == 3 and valu_step:
+        res["roofline_isolated"] = roofline(acc_iso, ISO_STEPS, iso_ms, 1,
+                                            f"{ISO_STEPS} steps one at a time after the timed region; per-launch HIP "
+                                            f"events (hipExtLaunchKernel start/stop)")
+    valu_step, valu_tag = pmc_valu_per_step(args.config)
+    if valu_step:
         # the whole pipeline against the measured VALU issue ceiling: committed PMC instruction
         # count of one step (per GPU) / this run's step time
         res["valu_issue"] = {"wave_instr_per_step": valu_step, "profile": valu_tag,
                              "ceiling_wave_instr_per_s": VALU_ISSUE_CEILING,
                              "frac": valu_step / (elapsed / K) / VALU_ISSUE_CEILING}
     # proof streaming: every proof word is read by the device at least once per step
-    words_step = sum(x["proof_words"] for x in st0)
+    words_step = st0["proof_words"]
     step_s = elapsed / K
     res["hbm"] = {"proof_bytes_per_step": words_step * 8, "achieved_GBps": words_step * 8 / step_s / 1e9,
                   "peak_GBps": HBM_PEAK / 1e9, "frac": words_step * 8 / step_s / HBM_PEAK}
-    bytes_step, bytes_tag = pmc_bytes_per_step()
-    if args.config == 3 and bytes_step:
+    bytes_step, bytes_tag = pmc_bytes_per_step(args.config)
+    if bytes_step:
         res["hbm"].update({"pmc_bytes_per_step": bytes_step, "pmc_GBps": bytes_step / step_s / 1e9,
                            "pmc_frac": bytes_step / step_s / HBM_PEAK, "pmc_profile": bytes_tag})
+    for b in ring:
+        b.close()
+    if rank == 0 and args.stream_batches > 0:
+        res["pcie_inclusive"] = pcie_stream(ctx, gair, stark, claims, proofs, expect, args.stream_batches)
     if rank == 0 and args.paths_log2 > 0:
         res["tip5_paths"] = tip5_paths(ctx, args.paths_log2, 5)
     if cpu is not None:
         res["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(res), flush=True)
-    for b in batches:
-        b.close()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

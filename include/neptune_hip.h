@@ -144,6 +144,9 @@ typedef struct {
     double ms_mp_hash_kernel;
     uint64_t mp_hash_kernel_launches, mp_hash_kernel_perms;
     double ms_device_decode;        /* k_decode: the proof-stream walk on the device (every run) */
+    /* the same hash launches' own durations (dispatch begin / end timestamps of each launch, as the
+     * rocprofv3 kernel trace reports them), summed: ms_mp_hash_kernel minus the gaps between them */
+    double ms_mp_hash_exec;
 } nhip_stats;
 
 typedef struct nhip_air nhip_air;

@@ -67,6 +67,9 @@ struct ProofIn {
     uint32_t sized_log2_ph, pad;
 };
 
+// Merkle hash launches (k_mp_hash / k_mp_hash_wide) timed per launch (start / stop event pairs)
+static constexpr uint32_t MAX_HASH_LAUNCHES = 64;
+
 // device counters of a run (zeroed per run, read back with the verdicts)
 enum : uint32_t { CNT_MP_SKIPPED = 0, CNT_PERMS_STATIC = 1, CNT_PERMS_LCW = 2, CNT_N = 4 };
 
@@ -108,6 +111,7 @@ struct StarkBatchDev {
 static constexpr int STARK_EVENTS = 13;
 struct StarkPhaseTimer {
     hipEvent_t ev[STARK_EVENTS];
+    hipEvent_t lev[2 * MAX_HASH_LAUNCHES];  // per hash launch: dispatch begin / end (nullptr = untimed)
     uint32_t mp_hash_launches;
     uint32_t aux_after_level = 0;  // hash levels launched before the OOD/FRI/DEEP chain is released
 };

@@ -170,6 +170,7 @@ struct nhip_batch {
         double decode, fs, rows, plan, hash, roots, ood, fri, deep, total;
     } ph{};
     double stage_ms = 0, upload_ms = 0;
+    double mp_hash_exec_ms = 0;  // summed dispatch durations of the hash launches
     uint64_t merkle_perms = 0;
     std::vector<uint64_t> mp_cap;  // multiproof op capacity per level
 };
@@ -840,6 +841,12 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
         } else {
             for (int i = 0; i < STARK_EVENTS; ++i)
                 if (hipEventCreate(&b->tm.ev[i]) != hipSuccess) return NHIP_ERR_HIP;
+            for (uint32_t i = 0; i < 2 * MAX_HASH_LAUNCHES; ++i)  // per hash launch (device-resident batches)
+                if (hipEventCreate(&b->tm.lev[i]) != hipSuccess) {
+                    for (uint32_t j = 0; j < i; ++j) (void)hipEventDestroy(b->tm.lev[j]);
+                    for (uint32_t j = 0; j < 2 * MAX_HASH_LAUNCHES; ++j) b->tm.lev[j] = nullptr;
+                    break;  // untimed hash launches: a fault of the timing only
+                }
             if (hipStreamCreateWithFlags(&b->main, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
             if (hipStreamCreateWithFlags(&b->aux, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
         }
@@ -891,6 +898,15 @@ int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* al
         uint32_t c;
         std::memcpy(&c, b->h_out + OUT_HDR + 4 * i, 4);
         reserved += c;
+    }
+    {  // the hash launches' own durations (dispatch begin / end timestamps)
+        double exec = 0;
+        const uint32_t nl = std::min<uint32_t>(b->tm.mp_hash_launches, MAX_HASH_LAUNCHES);
+        for (uint32_t i = 0; i < nl && b->tm.lev[0]; ++i) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, b->tm.lev[2 * i], b->tm.lev[2 * i + 1]) == hipSuccess) exec += ms;
+        }
+        b->mp_hash_exec_ms = exec;
     }
     b->H.perms_static = cnt[CNT_PERMS_STATIC];
     b->H.perms_lcw = cnt[CNT_PERMS_LCW];
@@ -946,6 +962,7 @@ int nhip_batch_stats(const nhip_batch* b, nhip_stats* s) {
     s->ms_deep = b->ph.deep;
     s->ms_device_total = b->ph.total;
     s->ms_device_decode = b->ph.decode;
+    s->ms_mp_hash_exec = b->mp_hash_exec_ms;
     s->tip5_perms_static = b->H.perms_static;
     s->tip5_perms_merkle = b->merkle_perms;
     // every Merkle hash launch (k_mp_hash + the 16-lane-row k_mp_hash_wide): back to back on the
@@ -992,8 +1009,11 @@ void nhip_batch_destroy(nhip_batch* b) {
         delete b;
         return;
     }
-    if (b->timed)
+    if (b->timed) {
         for (int i = 0; i < STARK_EVENTS; ++i) (void)hipEventDestroy(b->tm.ev[i]);
+        for (uint32_t i = 0; i < 2 * MAX_HASH_LAUNCHES; ++i)
+            if (b->tm.lev[i]) (void)hipEventDestroy(b->tm.lev[i]);
+    }
     if (b->main) (void)hipStreamDestroy(b->main);
     if (b->aux) (void)hipStreamDestroy(b->aux);
     if (b->h_out) (void)hipHostFree(b->h_out);

@@ -3,6 +3,8 @@
 // Conventions: the batch word buffer holds canonical u64 field elements (proof words and staged
 // claims); every scratch value written by these kernels (samples, row digests, OOD sums) is a raw
 // Montgomery word.  Each failed check ORs a FailBits bit into fail[proof].
+#include <hip/hip_ext.h>
+
 #include <cstdlib>
 
 #include "kernels.hpp"
@@ -561,7 +563,6 @@ __global__ void __launch_bounds__(256) k_mp_hash(const uint64_t* __restrict__ wo
             }
         }
     }
-    // permutations performed, one atomic per wave (bench / stats: perms per launch)
     if (!work) return;
 #pragma unroll
     for (int q = 10; q < 16; ++q) s[q] = MONT_ONE;
@@ -1216,12 +1217,17 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         const uint32_t lcw_blocks = (uint32_t)((per * n + 255) / 256);
         if (mp_blocks + lcw_blocks == 0) continue;
         const bool wide = lcw_blocks == 0 && cap <= MP_WIDE_MAX_OPS;
+        // hipExtLaunchKernel's start / stop events take the dispatch's own begin / end timestamps
+        // (what the rocprofv3 kernel trace reports): the launch's duration without the dispatch
+        // gap before it, which a plain event pair around back-to-back launches would also hold
+        const bool timed = launches < MAX_HASH_LAUNCHES && tm->lev[0] != nullptr;
+        hipEvent_t e0 = timed ? tm->lev[2 * launches] : nullptr, e1 = timed ? tm->lev[2 * launches + 1] : nullptr;
         if (wide)
-            hipLaunchKernelGGL(k_mp_hash_wide, dim3((unsigned)((cap * 16 + 255) / 256)), dim3(256), 0, st, b.words,
-                               b.dig, b.mp, l);
+            hipExtLaunchKernelGGL(k_mp_hash_wide, dim3((unsigned)((cap * 16 + 255) / 256)), dim3(256), 0, st, e0, e1,
+                                  0, b.words, b.dig, b.mp, l);
         else
-            hipLaunchKernelGGL(k_mp_hash, dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, b.words, b.dig, b.mp, l,
-                               mp_blocks, b.desc, n, b.fail, lcw);
+            hipExtLaunchKernelGGL(k_mp_hash, dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0, e1, 0, b.words,
+                                  b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw);
         ++launches;
     }
     if (!aux_started) launch_aux_chain();

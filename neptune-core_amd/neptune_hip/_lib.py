@@ -51,7 +51,7 @@ class Stats(ctypes.Structure):
                 ("ms_device_total", ctypes.c_double), ("ms_merkle_hash", ctypes.c_double),
                 ("merkle_hash_launches", ctypes.c_uint64), ("ms_mp_hash_kernel", ctypes.c_double),
                 ("mp_hash_kernel_launches", ctypes.c_uint64), ("mp_hash_kernel_perms", ctypes.c_uint64),
-                ("ms_device_decode", ctypes.c_double)]
+                ("ms_device_decode", ctypes.c_double), ("ms_mp_hash_exec", ctypes.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

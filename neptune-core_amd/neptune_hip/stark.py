@@ -102,6 +102,11 @@ class _Marshal:
         self.n = n
 
 
+def marshal(claims: Sequence[Claim], proofs: Sequence[Sequence[int]]):
+    """The C claim / proof arrays over `proofs`' memory (no copy for contiguous uint64 arrays)."""
+    return _Marshal(claims, proofs)
+
+
 class Batch:
     """Device-resident batch: decode + upload once, run the device phases any number of times."""
 
@@ -115,9 +120,11 @@ class Batch:
                                          ctypes.byref(h)), "nhip_batch_prepare")
         self.handle = h.value
 
-    def refill(self, claims: Sequence[Claim], proofs: Sequence[Sequence[int]]) -> None:
-        """Replace the batch's proofs in place (`nhip_batch_refill`; the batch must be idle)."""
-        m = _Marshal(claims, proofs)
+    def refill(self, claims: Sequence[Claim], proofs: Sequence[Sequence[int]] = None, marshalled=None) -> None:
+        """Replace the batch's proofs in place (`nhip_batch_refill`; the batch must be idle).
+        `marshalled`: a `marshal(claims, proofs)` made once and reused (streaming the same buffers
+        again without re-building the C structs in Python)."""
+        m = marshalled if marshalled is not None else _Marshal(claims, proofs)
         params = self.stark.c()
         self.n = 0
         check(self.ctx.lib.nhip_batch_refill(self.ctx.handle, self.handle, self.air.handle, ctypes.byref(params),

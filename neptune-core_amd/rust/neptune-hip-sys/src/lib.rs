@@ -81,6 +81,7 @@ pub struct nhip_stats {
     pub mp_hash_kernel_launches: u64,
     pub mp_hash_kernel_perms: u64,
     pub ms_device_decode: f64,
+    pub ms_mp_hash_exec: f64,
 }
 
 #[repr(C)]

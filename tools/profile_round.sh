@@ -1,17 +1,19 @@
 #!/bin/bash
 # rocprofv3 passes for the bench workload: kernel trace + stats, then separate PMC passes
-# (one counter group per run, never combined with other tracing domains).
+# (one counter group per run, never combined with other tracing domains), each under its own
+# time limit; stops at the first failure.
 # Usage: bash tools/profile_round.sh TAG [bench args...]   (outputs under gpurun_out/prof_TAG/)
-set -e
-TAG=${1:-r01}
+set -o pipefail
+TAG=${1:-r02}
 shift || true
-ARGS=${*:-"--steps 20 --warmup 3 --no-cpu"}
+ARGS=${*:-"--steps 20 --warmup 5 --no-cpu --paths-log2 0 --stream-batches 0"}
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-GPU_MAX_HW_QUEUES=8 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- python3 bench.py $ARGS > $OUT/bench_trace.json 2> $OUT/trace.err
-GPU_MAX_HW_QUEUES=8 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_LDS SQ_INSTS_SALU -d $OUT/pmc_valu -o pmc_valu --output-format csv -- python3 bench.py $ARGS > /dev/null 2> $OUT/pmc_valu.err
-GPU_MAX_HW_QUEUES=8 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -d $OUT/pmc_cycles -o pmc_cycles --output-format csv -- python3 bench.py $ARGS > /dev/null 2> $OUT/pmc_cycles.err
-GPU_MAX_HW_QUEUES=8 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o pmc_fetch --output-format csv -- python3 bench.py $ARGS > /dev/null 2> $OUT/pmc_fetch.err
-GPU_MAX_HW_QUEUES=8 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o pmc_write --output-format csv -- python3 bench.py $ARGS > /dev/null 2> $OUT/pmc_write.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- python3 bench.py $ARGS > $OUT/bench_trace.json 2> $OUT/trace.err || exit 1
+timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_LDS SQ_INSTS_SALU -d $OUT/pmc_valu -o pmc_valu --output-format csv -- python3 bench.py $ARGS > /dev/null 2> $OUT/pmc_valu.err || exit 1
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -d $OUT/pmc_cycles -o pmc_cycles --output-format csv -- python3 bench.py $ARGS > /dev/null 2> $OUT/pmc_cycles.err || exit 1
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o pmc_fetch --output-format csv -- python3 bench.py $ARGS > /dev/null 2> $OUT/pmc_fetch.err || exit 1
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o pmc_write --output-format csv -- python3 bench.py $ARGS > /dev/null 2> $OUT/pmc_write.err || exit 1
+python3 tools/summarize_profile.py $OUT > $OUT/SUMMARY.md
 echo done
