@@ -44,10 +44,6 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 ISO_STEPS = 5
-# before anything initialises HIP: 2 batches x 2 streams + the context stream (see above); the GPU
-# boxes export HIP's default of 4, which would put two streams on one queue
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
 
 P = (1 << 64) - (1 << 32) + 1
@@ -381,11 +377,19 @@ def main():
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
     ap.add_argument("--stream-batches", type=int, default=6,
                     help="PCIe-inclusive leg: batches streamed from pinned host memory (0 = skip)")
-    ap.add_argument("--inflight", type=int, default=None, choices=(1, 2, 3),
+    ap.add_argument("--inflight", type=int, default=None, choices=(1, 2, 3, 4, 5, 6),
                     help="R > 1: R resident copies of the batch in rotation, up to R steps in flight (step k+1 is "
                          "launched before step k is waited on, so its row hashing fills step k's latency-bound "
-                         "phases). Default: 2 for >= 2,048 proofs per GPU, 3 below")
+                         "phases). Default: 2 for >= 4,096 proofs per GPU (2 and 4: 366k proofs/s), 4 below "
+                         "(512 proofs: 243k / 274k / 269k proofs/s with 3 / 4 / 5; 1,024: 300k / 325k / 316k; "
+                         "2,048: 336k / 351k / 344k)")
     args = ap.parse_args()
+    # before anything initialises HIP: R resident batches x 2 streams + the context stream need
+    # their own hardware queues (streams sharing a queue serialize); the GPU boxes export HIP's
+    # default of 4
+    want_q = max(8, 2 * (args.inflight or 4) + 2)
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < want_q:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -431,7 +435,7 @@ def main():
     gair = NS.Air([int(w) for w in air_words])
     stark = NS.Stark.default()
     ncl = [NS.Claim(*c) for c in claims]
-    R = args.inflight or (2 if n >= 2048 else 3)
+    R = args.inflight or (2 if n >= 4096 else 4)
     # R resident copies of the raw proof words (each step decodes them on the device again)
     ring = [NS.Batch(ctx, gair, stark, ncl, proofs) for _ in range(R)]
     prep_s = time.time() - t0
@@ -444,24 +448,28 @@ def main():
     to_launch = [0]  # launches left in the current region: each region starts and ends with nothing in flight
     gathered = [None]
 
-    def run_all():
-        # keep up to R steps in flight (one per resident copy), then wait for the oldest
-        while to_launch[0] and len(launched) < R:
-            ring[next_slot[0]].launch()
-            launched.append(next_slot[0])
-            next_slot[0] = (next_slot[0] + 1) % R
-            to_launch[0] -= 1
-        b = ring[launched.pop(0)]
-        v, ok = b.wait()
-        return b, v, ok
+    def launch_one():
+        ring[next_slot[0]].launch()
+        launched.append(next_slot[0])
+        next_slot[0] = (next_slot[0] + 1) % R
+        to_launch[0] -= 1
 
     def step():
-        b, v, ok = run_all()
+        # keep up to R steps in flight (one per resident copy); wait for the oldest, take its
+        # verdicts and stats, and relaunch its slot at once (before any bookkeeping) so the GPU
+        # never waits on the host between steps
+        while to_launch[0] and len(launched) < R:
+            launch_one()
+        b = ring[launched.pop(0)]
+        v, ok = b.wait()
+        st = b.stats()
+        if to_launch[0]:
+            launch_one()
         if dist is not None:
             ok = shard.all_ok(ok, dist)  # RCCL all-reduce(MIN) of the batch verdict
             if shards is not None:  # block validation: every rank gets every proof's verdict
                 gathered[0] = shard.gather_verdicts(v, shards, total, dist)
-        return b, v, ok
+        return st, v, ok
 
     def barrier_sync():
         ctx.synchronize()
@@ -480,11 +488,11 @@ def main():
     t_start = time.perf_counter()
     to_launch[0] = args.steps  # every timed step is launched and waited inside the timed region
     for _ in range(args.steps):
-        b, v, batch_ok = step()
+        st, v, batch_ok = step()
         correct = correct and bool((np.asarray(v, dtype=bool) == expect).all())
         if gathered[0] is not None:
             correct = correct and bool((gathered[0].astype(bool) == expect_all).all())
-        for k, x in b.stats().items():
+        for k, x in st.items():
             acc[k] = acc.get(k, 0.0) + x
     barrier_sync()
     elapsed = time.perf_counter() - t_start
