@@ -15,6 +15,18 @@
 
 namespace nhip {
 
+// Wave priority of the latency-bound kernels (decode, the Fiat-Shamir sponge, the Merkle plan,
+// the small top Merkle levels, OOD, FRI): their waves share SIMDs with the VALU-bound hashing of
+// the same and the other in-flight steps, and the SIMD arbitrates VALU issue by wave priority,
+// then age.  Raising it lets a dependent chain issue as soon as it can, while the throughput
+// kernels fill the remaining slots.  NHIP_LAT_PRIO (0..3) selects it at build time.
+#ifndef NHIP_LAT_PRIO
+#define NHIP_LAT_PRIO 2
+#endif
+__device__ __forceinline__ void latency_priority() {
+    if constexpr (NHIP_LAT_PRIO > 0) __builtin_amdgcn_s_setprio(NHIP_LAT_PRIO);
+}
+
 
 __device__ __forceinline__ Xfe ld_xfe_canon(const uint64_t* __restrict__ w, uint64_t off) {
     return {to_mont(w[off]), to_mont(w[off + 1]), to_mont(w[off + 2])};
@@ -45,12 +57,43 @@ __global__ void __launch_bounds__(64) k_decode(const uint64_t* __restrict__ word
                                                uint32_t n_proofs, Dims D, uint32_t fs_stride, uint32_t xs_stride,
                                                ProofDesc* __restrict__ desc, FsOp* __restrict__ ops,
                                                uint32_t* __restrict__ fail, unsigned long long* __restrict__ counters) {
+    latency_priority();
     __shared__ ProofDesc spd;
     __shared__ uint32_t sfail;
     __shared__ int sdeg;
+    __shared__ uint32_t sink;
     const uint32_t p = blockIdx.x, lane = threadIdx.x;
     if (p >= n_proofs) return;
     const ProofIn pin = in[p];
+    // The items up to the FRI polynomial have sizes fixed by the padded height the proof declares
+    // (roots, OOD rows, FRI roots, the last codeword), so their positions are known before the
+    // walk: the lanes load their header words in parallel, and lane 0's dependent walk below then
+    // finds them in cache instead of paying one memory round trip per item.  Only a prefetch: a
+    // proof whose items differ is still judged by the walk alone.
+    if (pin.sized_log2_ph != SHAPE_NONE) {
+        ProofShape sh{};
+        if (shape_of(D, pin.sized_log2_ph, sh)) {
+            const StarkDims& d = D.d;
+            const uint32_t t = lane;  // item t's length word sits at pos_t
+            uint64_t pos = pin.off + 2, acc = 0;
+            if (t <= 11u + sh.R) {
+                // pos_t = off + 2 + sum_{j<t} (1 + ln_j)
+                for (uint32_t j = 0; j < t; ++j) {
+                    uint64_t ln;
+                    if (j == 0) ln = 2;
+                    else if (j <= 3 || (j >= 9 && j <= 9 + sh.R)) ln = 6;
+                    else if (j == 4 || j == 6) ln = 1 + 3ull * d.num_main;
+                    else if (j == 5 || j == 7) ln = 1 + 3ull * d.num_aux;
+                    else if (j == 8) ln = 1 + 3ull * d.num_quot_seg;
+                    else ln = 3 + 3ull * (1ull << (sh.log2_N - sh.R));  // the last codeword
+                    pos += 1 + ln;
+                }
+                if (pos + 4 <= pin.off + pin.len)
+                    for (int q = 0; q < 4; ++q) acc ^= words[pos + q];
+            }
+            if (acc == 0x9E3779B97F4A7C15ull) sink = t;  // keeps the loads; practically never taken
+        }
+    }
     if (lane == 0) {
         uint64_t perms = 0, perms_lcw = 0;
         const ClaimLoc cl{pin.claim_off, pin.claim_in_n, pin.claim_out_n};
@@ -114,6 +157,7 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
                                                         const FsOp* __restrict__ ops, uint32_t n_proofs,
                                                         uint64_t* __restrict__ xs, uint32_t* __restrict__ idx_out,
                                                         const uint32_t* __restrict__ fail) {
+    latency_priority();
     __shared__ Tip5Lds lds;
     tip5_lds_init(lds);
     constexpr uint32_t LANES = PAIR ? 32u : 16u;
@@ -321,6 +365,7 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
                                                const uint64_t* __restrict__ dig, const uint32_t* __restrict__ idx_all,
                                                MpPlan plan, uint32_t* __restrict__ fail,
                                                unsigned long long* __restrict__ perm_counter) {
+    latency_priority();
     __shared__ MpPlanLds<B> L;
     const uint32_t p = blockIdx.x, grp = blockIdx.y, tid = threadIdx.x;
     if (p >= n_proofs) return;
@@ -585,6 +630,7 @@ __device__ __forceinline__ uint64_t mp_load_word(uint64_t code, uint32_t e, cons
 
 __global__ void __launch_bounds__(256) k_mp_hash_wide(const uint64_t* __restrict__ words,
                                                       const uint64_t* __restrict__ dig, MpPlan plan, uint32_t lvl) {
+    latency_priority();
     __shared__ Tip5Lds t5;
     __shared__ uint64_t s_base[MP_SHARDS + 1];
     __shared__ uint32_t s_cnt[MP_SHARDS];
@@ -715,6 +761,7 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
                                                  const uint64_t* __restrict__ xs, uint64_t* __restrict__ ood_out,
                                                  uint32_t* __restrict__ fail, uint32_t lds_slots,
                                                  Xfe* __restrict__ gslots, uint32_t gslot_n) {
+    latency_priority();
     // all LDS in the dynamic region (16-B aligned carve, no static __shared__ in front of it)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Xfe* red = reinterpret_cast<Xfe*>(smem);              // 256
@@ -865,6 +912,7 @@ __global__ void __launch_bounds__(256) k_fri(const uint64_t* __restrict__ words,
                                              uint32_t n_proofs, StarkDims dims, const uint64_t* __restrict__ xs,
                                              const uint32_t* __restrict__ idx_all, uint64_t* __restrict__ xdom,
                                              uint32_t* __restrict__ fail) {
+    latency_priority();
     __shared__ Xfe red[256];
     __shared__ uint64_t gsq[33], wsq[33];
     __shared__ uint32_t lflag;
