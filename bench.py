@@ -65,23 +65,25 @@ def log(*a):
 FETCH_CORRECTION = {"FETCH_SIZE": 2.0, "WRITE_SIZE": 1.0}
 
 
-def latest_profile(config: int):
-    """profiles/LATEST = '<tag> <config>': the committed rocprofv3 PMC passes and the BASELINE
-    config they were taken on (none for another config)."""
+def latest_profile(config: int, proofs: int):
+    """profiles/LATEST = '<tag> <config> <proofs per GPU>': the committed rocprofv3 PMC passes and
+    the workload they were taken on (none for another config or per-GPU batch size: the PMC
+    figures are per step of that workload)."""
     try:
         parts = open(os.path.join(ROOT, "profiles", "LATEST")).read().split()
     except OSError:
         return None
     tag, cfg = parts[0], int(parts[1]) if len(parts) > 1 else 3
-    return tag if cfg == config else None
+    n = int(parts[2]) if len(parts) > 2 else None
+    return tag if cfg == config and n in (None, proofs) else None
 
 
-def pmc_traffic(kernel: str, config: int):
+def pmc_traffic(kernel: str, config: int, proofs: int):
     """HBM bytes per launch of `kernel` from the latest committed rocprofv3 PMC passes
     (profiles/LATEST -> profiles/<tag>/pmc_{fetch,write}_counter_collection.csv), raw
     (FETCH_SIZE + WRITE_SIZE) x 1024; None when absent."""
     import csv
-    tag = latest_profile(config)
+    tag = latest_profile(config, proofs)
     if tag is None:
         return None, None
     try:
@@ -96,12 +98,12 @@ def pmc_traffic(kernel: str, config: int):
         return None, None
 
 
-def pmc_valu_per_step(config: int):
+def pmc_valu_per_step(config: int, proofs: int):
     """Wave-level VALU instructions one config-3 step issues, from the latest committed PMC pass
     (profiles/<LATEST>/pmc_valu_counter_collection.csv: SQ_INSTS_VALU summed over a step's
     dispatches, microbench kernels excluded; steps = k_hash_rows dispatches); None when absent."""
     import csv
-    tag = latest_profile(config)
+    tag = latest_profile(config, proofs)
     if tag is None:
         return None, None
     try:
@@ -117,12 +119,12 @@ def pmc_valu_per_step(config: int):
         return None, None
 
 
-def pmc_bytes_per_step(config: int):
+def pmc_bytes_per_step(config: int, proofs: int):
     """HBM bytes (raw FETCH_SIZE + WRITE_SIZE, x 1024) one config-3 step moves, summed over the step's
     dispatches in the latest committed PMC passes (microbench and runtime copy kernels excluded;
     steps = k_hash_rows dispatches); None when absent."""
     import csv
-    tag = latest_profile(config)
+    tag = latest_profile(config, proofs)
     if tag is None:
         return None, None
     try:
@@ -537,7 +539,7 @@ def main():
     # launches in ISO_STEPS steps run one at a time after the timed region (launches x average <=
     # the step time).  kernel_avg_ms_events: the HIP-event span of one step's back-to-back hash
     # launches / launches (adds the dispatch gaps between levels).
-    traffic, traffic_tag = pmc_traffic("k_mp_hash", args.config)
+    traffic, traffic_tag = pmc_traffic("k_mp_hash", args.config, len(proofs))
 
     def roofline(a, steps, step_ms_, overlap, measured):
         a = {k: v / steps for k, v in a.items()}
@@ -614,7 +616,7 @@ def main():
         res["roofline_isolated"] = roofline(acc_iso, ISO_STEPS, iso_ms, 1,
                                             f"{ISO_STEPS} steps one at a time after the timed region; per-launch HIP "
                                             f"events (hipExtLaunchKernel start/stop)")
-    valu_step, valu_tag = pmc_valu_per_step(args.config)
+    valu_step, valu_tag = pmc_valu_per_step(args.config, len(proofs))
     if valu_step:
         # the whole pipeline against the measured VALU issue ceiling: committed PMC instruction
         # count of one step (per GPU) / this run's step time
@@ -626,7 +628,7 @@ def main():
     step_s = elapsed / K
     res["hbm"] = {"proof_bytes_per_step": words_step * 8, "achieved_GBps": words_step * 8 / step_s / 1e9,
                   "peak_GBps": HBM_PEAK / 1e9, "frac": words_step * 8 / step_s / HBM_PEAK}
-    bytes_step, bytes_tag = pmc_bytes_per_step(args.config)
+    bytes_step, bytes_tag = pmc_bytes_per_step(args.config, len(proofs))
     if bytes_step:
         res["hbm"].update({"pmc_bytes_per_step": bytes_step, "pmc_GBps": bytes_step / step_s / 1e9,
                            "pmc_frac": bytes_step / step_s / HBM_PEAK, "pmc_profile": bytes_tag})
