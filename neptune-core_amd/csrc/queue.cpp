@@ -83,9 +83,14 @@ struct nhip_queue {
         in_flight[s] = false;
         size_t n = 0;
         for (Req* r : in_slot[s]) n += r->n;
-        verdicts.assign(n ? n : 1, 0);
-        const int rc = nhip_batch_wait(ctx, slot[s], verdicts.data(), nullptr);
-        deliver(in_slot[s], rc, verdicts.data());
+        int rc = NHIP_OK;
+        try {
+            verdicts.assign(n ? n : 1, 0);
+        } catch (const std::bad_alloc&) {
+            rc = NHIP_ERR_OOM;  // still wait: the slot must be idle before it is refilled
+        }
+        const int wrc = nhip_batch_wait(ctx, slot[s], rc ? nullptr : verdicts.data(), nullptr);
+        deliver(in_slot[s], rc ? rc : wrc, rc ? nullptr : verdicts.data());
     }
 
     // stage + launch the requests in in_slot[s]
