@@ -61,39 +61,9 @@ __global__ void __launch_bounds__(64) k_decode(const uint64_t* __restrict__ word
     __shared__ ProofDesc spd;
     __shared__ uint32_t sfail;
     __shared__ int sdeg;
-    __shared__ uint32_t sink;
     const uint32_t p = blockIdx.x, lane = threadIdx.x;
     if (p >= n_proofs) return;
     const ProofIn pin = in[p];
-    // The items up to the FRI polynomial have sizes fixed by the padded height the proof declares
-    // (roots, OOD rows, FRI roots, the last codeword), so their positions are known before the
-    // walk: the lanes load their header words in parallel, and lane 0's dependent walk below then
-    // finds them in cache instead of paying one memory round trip per item.  Only a prefetch: a
-    // proof whose items differ is still judged by the walk alone.
-    if (pin.sized_log2_ph != SHAPE_NONE) {
-        ProofShape sh{};
-        if (shape_of(D, pin.sized_log2_ph, sh)) {
-            const StarkDims& d = D.d;
-            const uint32_t t = lane;  // item t's length word sits at pos_t
-            uint64_t pos = pin.off + 2, acc = 0;
-            if (t <= 11u + sh.R) {
-                // pos_t = off + 2 + sum_{j<t} (1 + ln_j)
-                for (uint32_t j = 0; j < t; ++j) {
-                    uint64_t ln;
-                    if (j == 0) ln = 2;
-                    else if (j <= 3 || (j >= 9 && j <= 9 + sh.R)) ln = 6;
-                    else if (j == 4 || j == 6) ln = 1 + 3ull * d.num_main;
-                    else if (j == 5 || j == 7) ln = 1 + 3ull * d.num_aux;
-                    else if (j == 8) ln = 1 + 3ull * d.num_quot_seg;
-                    else ln = 3 + 3ull * (1ull << (sh.log2_N - sh.R));  // the last codeword
-                    pos += 1 + ln;
-                }
-                if (pos + 4 <= pin.off + pin.len)
-                    for (int q = 0; q < 4; ++q) acc ^= words[pos + q];
-            }
-            if (acc == 0x9E3779B97F4A7C15ull) sink = t;  // keeps the loads; practically never taken
-        }
-    }
     if (lane == 0) {
         uint64_t perms = 0, perms_lcw = 0;
         const ClaimLoc cl{pin.claim_off, pin.claim_in_n, pin.claim_out_n};
