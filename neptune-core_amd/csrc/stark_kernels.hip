@@ -598,8 +598,19 @@ __device__ __forceinline__ uint64_t mp_load_word(uint64_t code, uint32_t e, cons
     return e < 3 ? to_mont(words[v + e]) : 0ull;  // XFE leaf [c0, c1, c2, 0, 0]
 }
 
+// Word e of a last-codeword tree node v (lcw_node, one word per lane of the row).
+__device__ __forceinline__ uint64_t lcw_node_word(const uint64_t* __restrict__ words, const ProofDesc& d,
+                                                  const uint64_t* __restrict__ mine, uint32_t v, uint32_t L, uint32_t e) {
+    if (v >= L) return e < 3 ? to_mont(words[d.last_cw_off + 3ull * (v - L) + e]) : 0ull;
+    return mine[5ull * v + e];
+}
+
+// Rows [0, mp_rows) take the multiproof ops of level `lvl`; rows past them the level-`lvl` parents of
+// every proof's last-codeword tree (the same mapping as k_mp_hash's lcw blocks, one parent per row).
 __global__ void __launch_bounds__(256) k_mp_hash_wide(const uint64_t* __restrict__ words,
-                                                      const uint64_t* __restrict__ dig, MpPlan plan, uint32_t lvl) {
+                                                      const uint64_t* __restrict__ dig, MpPlan plan, uint32_t lvl,
+                                                      uint64_t mp_rows, const ProofDesc* __restrict__ desc,
+                                                      uint32_t n_proofs, const uint32_t* __restrict__ fail, LcwTree lcw) {
     latency_priority();
     __shared__ Tip5Lds t5;
     __shared__ uint64_t s_base[MP_SHARDS + 1];
@@ -612,29 +623,41 @@ __global__ void __launch_bounds__(256) k_mp_hash_wide(const uint64_t* __restrict
         s_base[MP_SHARDS] = plan.shard_base[(lvl + 1) * MP_SHARDS - 1] + plan.shard_cap[(lvl + 1) * MP_SHARDS - 1];
     tip5_lds_init(t5);  // includes the barrier
     const uint32_t e = threadIdx.x & 15u;
-    const uint64_t g = s_base[0] + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4);
+    const uint64_t row = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
     // every test below is uniform within the 16-lane row (one op per row)
-    bool work = false;
-    uint64_t lc = MPS_NONE, rc = MPS_NONE;
-    if (g < s_base[MP_SHARDS]) {
+    uint64_t s = MONT_ONE;
+    uint64_t* o = nullptr;
+    if (row < mp_rows) {
+        const uint64_t g = s_base[0] + row;
+        if (g >= s_base[MP_SHARDS]) return;
         uint32_t sh = 0;
 #pragma unroll
         for (uint32_t q = 1; q < MP_SHARDS; ++q) sh += g >= s_base[q] ? 1u : 0u;
-        if (g - s_base[sh] < s_cnt[sh]) {
-            lc = plan.ops[2 * g];
-            rc = plan.ops[2 * g + 1];
-            work = lc != MPS_NONE;
-        }
+        if (g - s_base[sh] >= s_cnt[sh]) return;
+        const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
+        if (lc == MPS_NONE) return;  // op of a tree that already failed
+        if (e < 5) s = mp_load_word(lc, e, words, dig, plan.arena);
+        else if (e < 10) s = mp_load_word(rc, e - 5, words, dig, plan.arena);
+        o = plan.arena + 5 * g;
+    } else {
+        const uint32_t per = lcw.max_len >> (lvl + 1);
+        const uint64_t q = row - mp_rows;
+        const uint32_t p = (uint32_t)(q / per), i = (uint32_t)(q % per);
+        if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;  // FAIL_DECODE is final once k_decode ran
+        const ProofDesc& d = desc[p];
+        const uint32_t L = d.last_cw_n;
+        if (i >= (L >> (lvl + 1))) return;
+        const uint32_t v = (L >> (lvl + 1)) + i;
+        uint64_t* mine = lcw.nodes + (uint64_t)p * lcw.max_len * 5;
+        if (e < 5) s = lcw_node_word(words, d, mine, 2 * v, L, e);
+        else if (e < 10) s = lcw_node_word(words, d, mine, 2 * v + 1, L, e - 5);
+        o = mine + 5ull * v;
     }
-    if (!work) return;
     uint64_t rcs[TIP5_ROUNDS];
 #pragma unroll
     for (int r = 0; r < TIP5_ROUNDS; ++r) rcs[r] = c_tip5_rc_raw[r * 16 + e];
-    uint64_t s = MONT_ONE;
-    if (e < 5) s = mp_load_word(lc, e, words, dig, plan.arena);
-    else if (e < 10) s = mp_load_word(rc, e - 5, words, dig, plan.arena);
     s = tip5_permute_wide(s, e, rcs, t5.lut);
-    if (e < 5) plan.arena[5 * g + e] = s;
+    if (e < 5) o[e] = s;
 }
 
 // One lane per (proof, tree): duplicate leaf indices carry equal digests, final node == root.
@@ -1234,15 +1257,15 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         const uint64_t per = b.max_lcw >> (l + 1);
         const uint32_t lcw_blocks = (uint32_t)((per * n + 255) / 256);
         if (mp_blocks + lcw_blocks == 0) continue;
-        const bool wide = lcw_blocks == 0 && cap <= MP_WIDE_MAX_OPS;
+        const bool wide = cap + per * n <= MP_WIDE_MAX_OPS;
         // hipExtLaunchKernel's start / stop events take the dispatch's own begin / end timestamps
         // (what the rocprofv3 kernel trace reports): the launch's duration without the dispatch
         // gap before it, which a plain event pair around back-to-back launches would also hold
         const bool timed = launches < MAX_HASH_LAUNCHES && tm->lev[0] != nullptr;
         hipEvent_t e0 = timed ? tm->lev[2 * launches] : nullptr, e1 = timed ? tm->lev[2 * launches + 1] : nullptr;
         if (wide)
-            hipExtLaunchKernelGGL(k_mp_hash_wide, dim3((unsigned)((cap * 16 + 255) / 256)), dim3(256), 0, st, e0, e1,
-                                  0, b.words, b.dig, b.mp, l);
+            hipExtLaunchKernelGGL(k_mp_hash_wide, dim3((unsigned)(((cap + per * n) * 16 + 255) / 256)), dim3(256), 0,
+                                  st, e0, e1, 0, b.words, b.dig, b.mp, l, cap, b.desc, n, (const uint32_t*)b.fail, lcw);
         else
             hipExtLaunchKernelGGL(k_mp_hash, dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0, e1, 0, b.words,
                                   b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw);
