@@ -36,6 +36,10 @@ static constexpr uint32_t AIR_LDS_SLOTS_MAX = (AIR_LDS_BUDGET - AIR_LDS_HEADER) 
 static constexpr uint32_t MP_SHARDS = 16;
 // levels with at most this many hash ops run the 16-lane-row Tip5 (latency-bound regime)
 static constexpr uint64_t MP_WIDE_MAX_OPS = 48 * 1024;
+// the last levels whose ops (multiproof + last-codeword parents) all fit this many rows are climbed
+// by one workgroup in one launch (k_mp_hash_tail), up to MP_TAIL_LEVELS_MAX levels
+static constexpr uint64_t MP_TAIL_MAX_OPS = 256;
+static constexpr uint32_t MP_TAIL_LEVELS_MAX = 32;
 // batches below this many proofs replay Fiat-Shamir on the two-row pair Tip5 (k_fs_replay_wide):
 // one-collection latency 1.89 -> 1.65 ms, while from 512 proofs on (several steps in flight) the
 // one-row form is 2-3% faster (profiles/r01i/ab_pair.log)

@@ -660,6 +660,83 @@ __global__ void __launch_bounds__(256) k_mp_hash_wide(const uint64_t* __restrict
     if (e < 5) o[e] = s;
 }
 
+// The last levels of a small batch (a few dozen parents each, e.g. one block's proof): one
+// workgroup climbs levels [lvl0, lvl1) itself, 64 rows in flight, with a barrier between levels
+// (all of its waves share one CU and its L1, so a parent written at level l is visible to every
+// wave at level l + 1).  One launch instead of one per level: the ~9 us dispatch gap between
+// dependent launches exceeds the level's own hashing time there.  caps[l - lvl0] = the multiproof
+// rows of level l (its capacity, as the per-level launches use).
+static constexpr uint32_t MP_TAIL_THREADS = 1024;
+struct TailCaps {
+    uint32_t cap[MP_TAIL_LEVELS_MAX];
+};
+
+__global__ void __launch_bounds__(MP_TAIL_THREADS) k_mp_hash_tail(const uint64_t* __restrict__ words,
+                                                                 const uint64_t* __restrict__ dig, MpPlan plan,
+                                                                 uint32_t lvl0, uint32_t lvl1, TailCaps caps,
+                                                                 const ProofDesc* __restrict__ desc, uint32_t n_proofs,
+                                                                 const uint32_t* __restrict__ fail, LcwTree lcw) {
+    latency_priority();
+    __shared__ Tip5Lds t5;
+    __shared__ uint64_t s_base[MP_SHARDS + 1];
+    __shared__ uint32_t s_cnt[MP_SHARDS];
+    tip5_lds_init(t5);
+    const uint32_t e = threadIdx.x & 15u;
+    const uint32_t row0 = threadIdx.x >> 4;
+    constexpr uint32_t ROWS = MP_TAIL_THREADS / 16;
+    uint64_t rcs[TIP5_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < TIP5_ROUNDS; ++r) rcs[r] = c_tip5_rc_raw[r * 16 + e];
+    for (uint32_t lvl = lvl0; lvl < lvl1; ++lvl) {
+        const bool has_mp = lvl < plan.levels;
+        if (has_mp) {
+            if (threadIdx.x < MP_SHARDS) {
+                s_base[threadIdx.x] = plan.shard_base[lvl * MP_SHARDS + threadIdx.x];
+                s_cnt[threadIdx.x] = plan.counter[lvl * MP_SHARDS + threadIdx.x];
+            }
+            if (threadIdx.x == 0)
+                s_base[MP_SHARDS] =
+                    plan.shard_base[(lvl + 1) * MP_SHARDS - 1] + plan.shard_cap[(lvl + 1) * MP_SHARDS - 1];
+        }
+        __syncthreads();  // shard table of this level; parents of the previous level written
+        const uint64_t mp_rows = has_mp ? caps.cap[lvl - lvl0] : 0;
+        const uint32_t per = lcw.max_len >> (lvl + 1);
+        const uint64_t rows = mp_rows + (uint64_t)per * n_proofs;
+        for (uint64_t row = row0; row < rows; row += ROWS) {  // uniform within the 16-lane row
+            uint64_t st = MONT_ONE;
+            uint64_t* o = nullptr;
+            if (row < mp_rows) {
+                const uint64_t g = s_base[0] + row;
+                if (g >= s_base[MP_SHARDS]) continue;
+                uint32_t sh = 0;
+#pragma unroll
+                for (uint32_t q = 1; q < MP_SHARDS; ++q) sh += g >= s_base[q] ? 1u : 0u;
+                if (g - s_base[sh] >= s_cnt[sh]) continue;
+                const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
+                if (lc == MPS_NONE) continue;
+                if (e < 5) st = mp_load_word(lc, e, words, dig, plan.arena);
+                else if (e < 10) st = mp_load_word(rc, e - 5, words, dig, plan.arena);
+                o = plan.arena + 5 * g;
+            } else {
+                const uint64_t q = row - mp_rows;
+                const uint32_t p = (uint32_t)(q / per), i = (uint32_t)(q % per);
+                if (p >= n_proofs || (fail[p] & FAIL_DECODE)) continue;
+                const ProofDesc& d = desc[p];
+                const uint32_t L = d.last_cw_n;
+                if (i >= (L >> (lvl + 1))) continue;
+                const uint32_t v = (L >> (lvl + 1)) + i;
+                uint64_t* mine = lcw.nodes + (uint64_t)p * lcw.max_len * 5;
+                if (e < 5) st = lcw_node_word(words, d, mine, 2 * v, L, e);
+                else if (e < 10) st = lcw_node_word(words, d, mine, 2 * v + 1, L, e - 5);
+                o = mine + 5ull * v;
+            }
+            st = tip5_permute_wide(st, e, rcs, t5.lut);
+            if (e < 5) o[e] = st;
+        }
+        __syncthreads();  // every parent of this level written before the next level reads it
+    }
+}
+
 // One lane per (proof, tree): duplicate leaf indices carry equal digests, final node == root.
 // Lanes n_records.. check the last codeword's Merkle root, one per proof.
 __global__ void k_mp_roots(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
@@ -1247,10 +1324,29 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     const LcwTree lcw{b.lcw, b.max_lcw};
     const uint32_t log2_lcw = 31 - __builtin_clz(b.max_lcw);
     const uint32_t hash_levels = b.mp.levels > log2_lcw ? b.mp.levels : log2_lcw;
+    // first level of the tail climbed in one launch (every level from it on is small)
+    uint32_t tail0 = hash_levels;
+    while (tail0 > 0 && hash_levels - tail0 < MP_TAIL_LEVELS_MAX) {
+        const uint32_t l = tail0 - 1;
+        const uint64_t ops = (l < b.mp.levels ? b.mp_cap_host[l] : 0) + (uint64_t)(b.max_lcw >> (l + 1)) * n;
+        if (ops > MP_TAIL_MAX_OPS) break;
+        --tail0;
+    }
+    if (hash_levels - tail0 < 2) tail0 = hash_levels;  // a single small level: the per-level launch
     for (uint32_t l = 0; l < hash_levels; ++l) {
-        if (!aux_started && l >= tm->aux_after_level) {
+        if (!aux_started && (l >= tm->aux_after_level || l == tail0)) {  // the tail is one workgroup
             launch_aux_chain();
             aux_started = true;
+        }
+        const bool timed = launches < MAX_HASH_LAUNCHES && tm->lev[0] != nullptr;
+        hipEvent_t e0 = timed ? tm->lev[2 * launches] : nullptr, e1 = timed ? tm->lev[2 * launches + 1] : nullptr;
+        if (l == tail0) {
+            TailCaps caps{};
+            for (uint32_t t = l; t < hash_levels; ++t) caps.cap[t - l] = t < b.mp.levels ? (uint32_t)b.mp_cap_host[t] : 0u;
+            hipExtLaunchKernelGGL(k_mp_hash_tail, dim3(1), dim3(MP_TAIL_THREADS), 0, st, e0, e1, 0, b.words, b.dig,
+                                  b.mp, l, hash_levels, caps, b.desc, n, (const uint32_t*)b.fail, lcw);
+            ++launches;
+            break;
         }
         const uint64_t cap = l < b.mp.levels ? b.mp_cap_host[l] : 0;
         const uint32_t mp_blocks = (uint32_t)((cap + 255) / 256);
@@ -1261,8 +1357,6 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         // hipExtLaunchKernel's start / stop events take the dispatch's own begin / end timestamps
         // (what the rocprofv3 kernel trace reports): the launch's duration without the dispatch
         // gap before it, which a plain event pair around back-to-back launches would also hold
-        const bool timed = launches < MAX_HASH_LAUNCHES && tm->lev[0] != nullptr;
-        hipEvent_t e0 = timed ? tm->lev[2 * launches] : nullptr, e1 = timed ? tm->lev[2 * launches + 1] : nullptr;
         if (wide)
             hipExtLaunchKernelGGL(k_mp_hash_wide, dim3((unsigned)(((cap + per * n) * 16 + 255) / 256)), dim3(256), 0,
                                   st, e0, e1, 0, b.words, b.dig, b.mp, l, cap, b.desc, n, (const uint32_t*)b.fail, lcw);
