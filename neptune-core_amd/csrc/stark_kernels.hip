@@ -26,6 +26,11 @@ namespace nhip {
 __device__ __forceinline__ void latency_priority() {
     if constexpr (NHIP_LAT_PRIO > 0) __builtin_amdgcn_s_setprio(NHIP_LAT_PRIO);
 }
+// wave priority of the lane-per-op Merkle level kernel (the level chain is each step's critical
+// path once its sponge replay is done; the row hashing has slack)
+#ifndef NHIP_MP_PRIO
+#define NHIP_MP_PRIO 1
+#endif
 
 
 __device__ __forceinline__ Xfe ld_xfe_canon(const uint64_t* __restrict__ w, uint64_t off) {
@@ -532,6 +537,7 @@ __global__ void __launch_bounds__(256) k_mp_hash(const uint64_t* __restrict__ wo
     __shared__ Tip5Lds t5;
     __shared__ uint64_t s_base[MP_SHARDS + 1];
     __shared__ uint32_t s_cnt[MP_SHARDS];
+    if constexpr (NHIP_MP_PRIO > 0) __builtin_amdgcn_s_setprio(NHIP_MP_PRIO);
     const bool is_lcw = blockIdx.x >= mp_blocks;  // uniform per block
     if (!is_lcw) {
         if (threadIdx.x < MP_SHARDS) {
