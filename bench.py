@@ -375,6 +375,10 @@ def main():
     ap.add_argument("--corrupt-frac", type=float, default=0.05)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--air", default="synthetic", choices=("synthetic", "triton-size"),
+                    help="AIR circuit: the pool's synthetic AIR (505 constraints, 3,151 nodes) or the same "
+                         "constraints bloated to triton-air's size class (~21.7k nodes, stark_ref.bloat_air; "
+                         "identically-zero extra terms, so the same proofs verify)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
     ap.add_argument("--stream-batches", type=int, default=6,
@@ -398,6 +402,11 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     air_words, pool = load_pool()
+    if args.air == "triton-size":
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import stark_ref as S  # AIR descriptor construction only (test-data generator)
+        air_words = np.asarray(S.bloat_air(S.AirCircuit.from_words([int(w) for w in air_words]), 24000).to_words(),
+                               dtype=np.uint64)
     sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
     shards = expect_all = None  # configs 4 / 5: per-proof verdicts are all-gathered every step
     if args.config == 3:
@@ -539,7 +548,7 @@ def main():
     # launches in ISO_STEPS steps run one at a time after the timed region (launches x average <=
     # the step time).  kernel_avg_ms_events: the HIP-event span of one step's back-to-back hash
     # launches / launches (adds the dispatch gaps between levels).
-    traffic, traffic_tag = pmc_traffic("k_mp_hash", args.config, len(proofs))
+    traffic, traffic_tag = pmc_traffic("k_mp_hash", args.config, len(proofs)) if args.air == "synthetic" else (None, None)
 
     def roofline(a, steps, step_ms_, overlap, measured):
         a = {k: v / steps for k, v in a.items()}
@@ -590,7 +599,7 @@ def main():
                  "synthetic: constant-codeword proofs (oracle/stark_prover_const.py), synthetic AIR with triton-vm "
                  "column counts"),
         "config": {"workload": workload, "proofs_total": total, "proofs_rank0": n,
-                   "parallelism": f"proof-sharded x{world}"},
+                   "parallelism": f"proof-sharded x{world}", "air": args.air},
         # what one step is: the raw proof words are resident in HBM when the step starts; the step
         # decodes every proof stream on the device (k_decode) and runs every verifier phase
         "step": "device proof-stream decode + Fiat-Shamir replay + row hashing + Merkle multiproofs + OOD AIR + "
@@ -616,7 +625,7 @@ def main():
         res["roofline_isolated"] = roofline(acc_iso, ISO_STEPS, iso_ms, 1,
                                             f"{ISO_STEPS} steps one at a time after the timed region; per-launch HIP "
                                             f"events (hipExtLaunchKernel start/stop)")
-    valu_step, valu_tag = pmc_valu_per_step(args.config, len(proofs))
+    valu_step, valu_tag = pmc_valu_per_step(args.config, len(proofs)) if args.air == "synthetic" else (None, None)
     if valu_step:
         # the whole pipeline against the measured VALU issue ceiling: committed PMC instruction
         # count of one step (per GPU) / this run's step time
@@ -628,7 +637,7 @@ def main():
     step_s = elapsed / K
     res["hbm"] = {"proof_bytes_per_step": words_step * 8, "achieved_GBps": words_step * 8 / step_s / 1e9,
                   "peak_GBps": HBM_PEAK / 1e9, "frac": words_step * 8 / step_s / HBM_PEAK}
-    bytes_step, bytes_tag = pmc_bytes_per_step(args.config, len(proofs))
+    bytes_step, bytes_tag = pmc_bytes_per_step(args.config, len(proofs)) if args.air == "synthetic" else (None, None)
     if bytes_step:
         res["hbm"].update({"pmc_bytes_per_step": bytes_step, "pmc_GBps": bytes_step / step_s / 1e9,
                            "pmc_frac": bytes_step / step_s / HBM_PEAK, "pmc_profile": bytes_tag})

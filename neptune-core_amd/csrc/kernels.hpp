@@ -26,7 +26,7 @@ hipError_t launch_absolute_index_sets(const uint64_t* d_digests, const uint64_t*
                                       uint32_t* d_dist, hipStream_t st);
 
 // ---- batched STARK verifier (stark_kernels.hip)
-static constexpr uint32_t AIR_LDS_HEADER = (256 + 4 + 4 + 4) * 24 + 16;  // red, zinv, derived, misc, flag
+static constexpr uint32_t AIR_LDS_HEADER = (16 + 4 + 4 + 4) * 24 + 16;  // red (per wave), zinv, derived, misc, flag
 static constexpr uint32_t AIR_LDS_BUDGET = 160 * 1024 - 8192;              // k_ood_air dynamic LDS cap
 static constexpr uint32_t AIR_LDS_SLOTS_MAX = (AIR_LDS_BUDGET - AIR_LDS_HEADER) / 24;
 
@@ -105,6 +105,7 @@ struct StarkBatchDev {
     const Xfe* air_consts;         // constant table (raw Montgomery)
     uint4 air_cons_off;            // constraint-type boundaries
     size_t air_lds_bytes;
+    uint32_t air_block;  // k_ood_air workgroup size (1,024 when the slot area keeps one workgroup per CU)
     uint32_t air_lds_slots;        // slots held in LDS
     uint32_t air_gslot_n;          // slots past the LDS budget, per proof, in air_gslots
     Xfe* air_gslots;               // [n_proofs][air_gslot_n]

@@ -301,6 +301,15 @@ void air_compile(nhip_air* a, const std::vector<uint32_t>& level, uint32_t max_l
     }
     for (size_t c = 0; c < cons.size(); ++c)
         lv_prog[level[cons[c]] + 1].push_back(OodIns{OOD_ACC, ref[cons[c]], (uint32_t)c, 0});
+    // Within a level every instruction is independent (its operands come from earlier levels), so
+    // each level is grouped by kind: a wave then runs one kind of XFE operation instead of the
+    // divergent union of several (a product where any lane multiplies, an add where any lane adds).
+    auto kind_rank = [](uint32_t op) {
+        return op == OOD_LOAD ? 0 : (op == AIR_MUL ? 1 : (op == OOD_ACC ? 3 : 2));
+    };
+    for (auto& lp : lv_prog)
+        std::stable_sort(lp.begin(), lp.end(),
+                         [&](const OodIns& x, const OodIns& y) { return kind_rank(x.op) < kind_rank(y.op); });
     a->prog_off.assign(1, 0);
     for (uint32_t l = 0; l < n_lv; ++l) {
         a->prog.insert(a->prog.end(), lv_prog[l].begin(), lv_prog[l].end());
@@ -779,6 +788,10 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     dv.air_gslot_n = air->slots - dv.air_lds_slots;
     dv.air_gslots = (Xfe*)ptr[21];
     dv.air_lds_bytes = AIR_LDS_HEADER + (size_t)dv.air_lds_slots * 24;
+    // 256 threads per proof: 1,024-thread workgroups for a triton-air-sized circuit (one workgroup
+    // per CU either way, the slot area fills its LDS) ran the 256-proof evaluation 0.248 -> 0.213 ms
+    // alone but took the wave slots the concurrent hashing needs (config 4: 354k -> 305k proofs/s)
+    dv.air_block = 256u;
     *out = b;
     return NHIP_OK;
 }

@@ -796,6 +796,24 @@ __device__ Xfe block_sum_xfe(Xfe v, Xfe* sh) {
     return r;
 }
 
+__device__ __forceinline__ Xfe shfl_xor_xfe_fwd(Xfe v, int m) {
+    return {(uint64_t)__shfl_xor((long long)v.c0, m), (uint64_t)__shfl_xor((long long)v.c1, m),
+            (uint64_t)__shfl_xor((long long)v.c2, m)};
+}
+
+// Workgroup sum with one LDS entry per wave (sh[blockDim / 64]); every thread gets the sum.
+__device__ Xfe block_sum_xfe_waves(Xfe v, Xfe* sh) {
+    const uint32_t tid = threadIdx.x, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) v = x_add(v, shfl_xor_xfe_fwd(v, m));
+    if ((tid & 63u) == 0) sh[tid >> 6] = v;
+    __syncthreads();
+    Xfe r = sh[0];
+    for (uint32_t w = 1; w < nw; ++w) r = x_add(r, sh[w]);
+    __syncthreads();
+    return r;
+}
+
 // ------------------------------------------------------------------ Challenges::new
 // triton-air 1.0 ChallengeId indices of the sampled indeterminates the derived challenges use
 // (public design, unpinned; oracle/stark_ref.py derive_challenges)
@@ -840,8 +858,8 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
     latency_priority();
     // all LDS in the dynamic region (16-B aligned carve, no static __shared__ in front of it)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    Xfe* red = reinterpret_cast<Xfe*>(smem);              // 256
-    Xfe* zinv = red + 256;                                 // 4
+    Xfe* red = reinterpret_cast<Xfe*>(smem);              // 16 (one per wave)
+    Xfe* zinv = red + 16;                                  // 4
     Xfe* chal_derived = zinv + 4;                          // 4 (Challenges::new)
     Xfe* misc = chal_derived + 4;                          // 4 (1 used: z - w^-1)
     uint32_t& zero_flag = *reinterpret_cast<uint32_t*>(misc + 4);
@@ -877,7 +895,7 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
         const Xfe cons = x_sub(zph, x_one());
         if (x_is_zero(cons)) atomicOr(&zero_flag, 1u);
         zinv[1] = x_inv(cons);
-    } else if (tid >= 192) {
+    } else if (tid >= 192 && tid < 256) {
         // Challenges::new: the 4 derived challenges in ChallengeId order, each an EvalArg terminal
         // folded from 1 with its named sampled indeterminate (wave 3, lane-parallel)
         auto chal = [&](uint32_t i) { return ld_xfe_raw(xs, xb + 3ull * (sl.chal + i)); };
@@ -935,7 +953,7 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
         }
         __syncthreads();
     }
-    const Xfe ood_q = block_sum_xfe(acc, red);
+    const Xfe ood_q = block_sum_xfe_waves(acc, red);
     // OOD linear combinations (DEEP needs them): lin weights = [main | aux | quot segs | deep]
     const uint32_t M = dims.num_main, A = dims.num_aux, Q = dims.num_quot_seg;
     Xfe lc = x_zero(), ln = x_zero();
@@ -946,8 +964,8 @@ __global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ wo
         lc = x_add(lc, x_mul(w, vc));
         ln = x_add(ln, x_mul(w, vn));
     }
-    const Xfe sum_c = block_sum_xfe(lc, red);
-    const Xfe sum_n = block_sum_xfe(ln, red);
+    const Xfe sum_c = block_sum_xfe_waves(lc, red);
+    const Xfe sum_n = block_sum_xfe_waves(ln, red);
     if (tid == 0) {
         Xfe seg = x_zero(), zk = x_one(), qlin = x_zero();
         for (uint32_t q = 0; q < Q; ++q) {
@@ -1314,7 +1332,7 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         mark(10, st);
         (void)hipStreamWaitEvent(sa, tm->ev[10], 0);
         mark(11, sa);
-        hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(256), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims, b.air_prog,
+        hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(b.air_block), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims, b.air_prog,
                            b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs, b.ood, b.fail,
                            b.air_lds_slots, b.air_gslots, b.air_gslot_n);
         mark(6, sa);
