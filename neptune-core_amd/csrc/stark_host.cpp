@@ -480,320 +480,331 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         }
         return rc;
     };
-    b->air = air;
-    b->device = nhip_internal_device(ctx);
-    b->scratch = scr;
-    b->H = HostBatch{};
-    HostBatch& H = b->H;
-    H.D = D;
-    H.n = (uint32_t)n;
-    const auto t0 = std::chrono::steady_clock::now();
-    // ---- layout and scratch sizes: proof words back to back, then the claim encodings; the
-    // padded height each proof declares (its first item, 5 header words) sizes the multiproof plan,
-    // the sample areas and the Fiat-Shamir program slots.  k_decode re-reads it and rejects a proof
-    // whose walk disagrees (never happens for one buffer; guards the scratch bounds).
-    std::vector<ProofIn> pin(n);
-    std::vector<ProofShape> shp(n);
-    uint64_t cur = 0;
-    for (size_t i = 0; i < n; ++i) {
-        pin[i].off = cur;
-        pin[i].len = proofs[i].len;
-        cur += proofs[i].len;
-    }
-    H.proof_words = cur;
-    for (size_t i = 0; i < n; ++i) {
-        pin[i].claim_off = cur;
-        pin[i].claim_in_n = (uint32_t)claims[i].input_len;
-        pin[i].claim_out_n = (uint32_t)claims[i].output_len;
-        cur += claim_words(claims[i]);
-    }
-    H.words_total = cur;
-    for (size_t i = 0; i < n; ++i) {
-        uint64_t lph = 0;
-        ProofShape s{};
-        if (header_log2_ph(proofs[i].words, proofs[i].len, lph) && shape_of(D, lph, s)) {
-            pin[i].sized_log2_ph = s.log2_ph;
-            shp[i] = s;
-            H.max_R = std::max(H.max_R, s.R);
-            H.levels = std::max(H.levels, s.log2_N);
-            H.max_last_cw = std::max(H.max_last_cw, 1u << (s.log2_N - s.R));
-        } else {
-            pin[i].sized_log2_ph = SHAPE_NONE;
+    // a host allocation failing below leaves no half-built batch behind (the upload threads are
+    // joined before anything after their start can throw)
+    try {
+        b->air = air;
+        b->device = nhip_internal_device(ctx);
+        b->scratch = scr;
+        b->H = HostBatch{};
+        HostBatch& H = b->H;
+        H.D = D;
+        H.n = (uint32_t)n;
+        const auto t0 = std::chrono::steady_clock::now();
+        // ---- layout and scratch sizes: proof words back to back, then the claim encodings; the
+        // padded height each proof declares (its first item, 5 header words) sizes the multiproof plan,
+        // the sample areas and the Fiat-Shamir program slots.  k_decode re-reads it and rejects a proof
+        // whose walk disagrees (never happens for one buffer; guards the scratch bounds).
+        std::vector<ProofIn> pin(n);
+        std::vector<ProofShape> shp(n);
+        uint64_t cur = 0;
+        for (size_t i = 0; i < n; ++i) {
+            pin[i].off = cur;
+            pin[i].len = proofs[i].len;
+            cur += proofs[i].len;
         }
-    }
-    H.fs_stride = fs_ops_for(H.max_R);
-    H.xs_stride = SampleLayout::of(D.d, H.max_R).total;
-    // ---- device word buffer (grow-only; its own allocation)
-    const size_t wbytes = H.words_total * 8 + 8;
-    {
-        void** dw = scr ? &scr->dwords : &b->dwords;
-        size_t* dwb = scr ? &scr->dwords_bytes : &b->dwords_bytes;
-        if (*dwb < wbytes) {
-            if (*dw) (void)hipFree(*dw);
-            *dw = nullptr;
-            *dwb = 0;
-            const size_t want = (reuse || scr) ? wbytes + wbytes / 4 : wbytes;
-            const hipError_t ea = hipMalloc(dw, want);
-            if (ea != hipSuccess) {
-                if (scr) b->dwords = nullptr;
-                return fail_out(hipfail(ea));
+        H.proof_words = cur;
+        for (size_t i = 0; i < n; ++i) {
+            pin[i].claim_off = cur;
+            pin[i].claim_in_n = (uint32_t)claims[i].input_len;
+            pin[i].claim_out_n = (uint32_t)claims[i].output_len;
+            cur += claim_words(claims[i]);
+        }
+        H.words_total = cur;
+        for (size_t i = 0; i < n; ++i) {
+            uint64_t lph = 0;
+            ProofShape s{};
+            if (header_log2_ph(proofs[i].words, proofs[i].len, lph) && shape_of(D, lph, s)) {
+                pin[i].sized_log2_ph = s.log2_ph;
+                shp[i] = s;
+                H.max_R = std::max(H.max_R, s.R);
+                H.levels = std::max(H.levels, s.log2_N);
+                H.max_last_cw = std::max(H.max_last_cw, 1u << (s.log2_N - s.R));
+            } else {
+                pin[i].sized_log2_ph = SHAPE_NONE;
             }
-            *dwb = want;
         }
-        b->dwords = *dw;
-    }
-    hipStream_t st = nhip_internal_stream(ctx);
-    uint64_t* d_words = (uint64_t*)b->dwords;
-    hipError_t e = hipSuccess;
-    auto dma = [&](uint64_t dst_word, const uint64_t* src, uint64_t nw) {
-        if (e == hipSuccess && nw) e = hipMemcpyAsync(d_words + dst_word, src, nw * 8, hipMemcpyHostToDevice, st);
-    };
-    // ---- upload.  Proofs in pinned caller memory (nhip_host_alloc / nhip_host_register) are
-    // DMA'd as they lie, adjacent ones as one copy; the others are copied into the context's
-    // pinned staging (same layout as the device buffer) by host threads, ~64 MB chunks in proof
-    // order, each chunk's DMA issued as soon as its copies are done.  The claim encodings go
-    // through the staging too.
-    {
-        std::vector<uint8_t> direct(n, 0);
-        for (size_t i = 0; i < n; ++i)
-            direct[i] = proofs[i].len && pinned().contains(proofs[i].words, proofs[i].len * 8) ? 1 : 0;
-        for (size_t i = 0; i < n;) {  // direct segments first: the DMA engine starts right away
-            if (!direct[i]) {
-                ++i;
-                continue;
+        H.fs_stride = fs_ops_for(H.max_R);
+        H.xs_stride = SampleLayout::of(D.d, H.max_R).total;
+        // ---- device word buffer (grow-only; its own allocation)
+        const size_t wbytes = H.words_total * 8 + 8;
+        {
+            void** dw = scr ? &scr->dwords : &b->dwords;
+            size_t* dwb = scr ? &scr->dwords_bytes : &b->dwords_bytes;
+            if (*dwb < wbytes) {
+                if (*dw) (void)hipFree(*dw);
+                *dw = nullptr;
+                *dwb = 0;
+                const size_t want = (reuse || scr) ? wbytes + wbytes / 4 : wbytes;
+                const hipError_t ea = hipMalloc(dw, want);
+                if (ea != hipSuccess) {
+                    if (scr) b->dwords = nullptr;
+                    return fail_out(hipfail(ea));
+                }
+                *dwb = want;
             }
-            size_t j = i + 1;
-            while (j < n && direct[j] && proofs[j].words == proofs[j - 1].words + proofs[j - 1].len) ++j;
-            dma(pin[i].off, proofs[i].words, pin[j - 1].off + pin[j - 1].len - pin[i].off);
-            i = j;
+            b->dwords = *dw;
         }
-        std::vector<uint64_t> pageable;
-        uint64_t* stage = (uint64_t*)nhip_internal_staging(ctx, wbytes);
-        if (!stage) {
-            pageable.resize(H.words_total + 1);
-            stage = pageable.data();
-        }
-        for (size_t i = 0; i < n; ++i) encode_claim(claims[i], stage + pin[i].claim_off);
-        std::vector<size_t> todo;  // staged proofs, in order
-        uint64_t staged_bytes = 0;
-        for (size_t i = 0; i < n; ++i)
-            if (!direct[i] && proofs[i].len) todo.push_back(i), staged_bytes += proofs[i].len * 8;
-        constexpr uint64_t CHUNK_WORDS = 8ull << 20;  // 64 MB
-        std::vector<size_t> cut{0};                   // chunk c = todo[cut[c] .. cut[c + 1])
-        for (size_t q = 1; q < todo.size(); ++q)
-            if (pin[todo[q]].off - pin[todo[cut.back()]].off >= CHUNK_WORDS) cut.push_back(q);
-        cut.push_back(todo.size());
-        const size_t nc = todo.empty() ? 0 : cut.size() - 1;
-        std::unique_ptr<std::atomic<size_t>[]> left(new std::atomic<size_t>[nc + 1]);
-        std::vector<size_t> chunk_of(todo.size());
-        for (size_t c = 0; c < nc; ++c) {
-            left[c].store(cut[c + 1] - cut[c]);
-            for (size_t q = cut[c]; q < cut[c + 1]; ++q) chunk_of[q] = c;
-        }
-        std::atomic<size_t> next{0};
-        auto work = [&]() {
-            for (size_t q; (q = next.fetch_add(1)) < todo.size();) {
-                const size_t i = todo[q];
-                std::memcpy(stage + pin[i].off, proofs[i].words, proofs[i].len * 8);
-                left[chunk_of[q]].fetch_sub(1, std::memory_order_release);
-            }
+        hipStream_t st = nhip_internal_stream(ctx);
+        uint64_t* d_words = (uint64_t*)b->dwords;
+        hipError_t e = hipSuccess;
+        auto dma = [&](uint64_t dst_word, const uint64_t* src, uint64_t nw) {
+            if (e == hipSuccess && nw) e = hipMemcpyAsync(d_words + dst_word, src, nw * 8, hipMemcpyHostToDevice, st);
         };
-        std::vector<std::thread> pool;
-        const unsigned threads = host_threads(staged_bytes);
-        if (threads > 1 && stage != pageable.data()) {
-            pool.reserve(threads);
-            for (unsigned t = 0; t < threads; ++t) {
-                try {
-                    pool.emplace_back(work);
-                } catch (const std::system_error&) {
-                    break;  // fewer threads: the running ones (and this one, below) take the rest
+        // ---- upload.  Proofs in pinned caller memory (nhip_host_alloc / nhip_host_register) are
+        // DMA'd as they lie, adjacent ones as one copy; the others are copied into the context's
+        // pinned staging (same layout as the device buffer) by host threads, ~64 MB chunks in proof
+        // order, each chunk's DMA issued as soon as its copies are done.  The claim encodings go
+        // through the staging too.
+        {
+            std::vector<uint8_t> direct(n, 0);
+            for (size_t i = 0; i < n; ++i)
+                direct[i] = proofs[i].len && pinned().contains(proofs[i].words, proofs[i].len * 8) ? 1 : 0;
+            for (size_t i = 0; i < n;) {  // direct segments first: the DMA engine starts right away
+                if (!direct[i]) {
+                    ++i;
+                    continue;
+                }
+                size_t j = i + 1;
+                while (j < n && direct[j] && proofs[j].words == proofs[j - 1].words + proofs[j - 1].len) ++j;
+                dma(pin[i].off, proofs[i].words, pin[j - 1].off + pin[j - 1].len - pin[i].off);
+                i = j;
+            }
+            std::vector<uint64_t> pageable;
+            uint64_t* stage = (uint64_t*)nhip_internal_staging(ctx, wbytes);
+            if (!stage) {
+                pageable.resize(H.words_total + 1);
+                stage = pageable.data();
+            }
+            for (size_t i = 0; i < n; ++i) encode_claim(claims[i], stage + pin[i].claim_off);
+            std::vector<size_t> todo;  // staged proofs, in order
+            uint64_t staged_bytes = 0;
+            for (size_t i = 0; i < n; ++i)
+                if (!direct[i] && proofs[i].len) todo.push_back(i), staged_bytes += proofs[i].len * 8;
+            constexpr uint64_t CHUNK_WORDS = 8ull << 20;  // 64 MB
+            std::vector<size_t> cut{0};                   // chunk c = todo[cut[c] .. cut[c + 1])
+            for (size_t q = 1; q < todo.size(); ++q)
+                if (pin[todo[q]].off - pin[todo[cut.back()]].off >= CHUNK_WORDS) cut.push_back(q);
+            cut.push_back(todo.size());
+            const size_t nc = todo.empty() ? 0 : cut.size() - 1;
+            std::unique_ptr<std::atomic<size_t>[]> left(new std::atomic<size_t>[nc + 1]);
+            std::vector<size_t> chunk_of(todo.size());
+            for (size_t c = 0; c < nc; ++c) {
+                left[c].store(cut[c + 1] - cut[c]);
+                for (size_t q = cut[c]; q < cut[c + 1]; ++q) chunk_of[q] = c;
+            }
+            std::atomic<size_t> next{0};
+            auto work = [&]() {
+                for (size_t q; (q = next.fetch_add(1)) < todo.size();) {
+                    const size_t i = todo[q];
+                    std::memcpy(stage + pin[i].off, proofs[i].words, proofs[i].len * 8);
+                    left[chunk_of[q]].fetch_sub(1, std::memory_order_release);
+                }
+            };
+            std::vector<std::thread> pool;
+            const unsigned threads = host_threads(staged_bytes);
+            if (threads > 1 && stage != pageable.data()) {
+                pool.reserve(threads);
+                for (unsigned t = 0; t < threads; ++t) {
+                    try {
+                        pool.emplace_back(work);
+                    } catch (const std::system_error&) {
+                        break;  // fewer threads: the running ones (and this one, below) take the rest
+                    }
                 }
             }
-        }
-        if (pool.empty()) work();
-        // DMA each chunk once copied: its staged proofs, adjacent ones as one copy
-        for (size_t c = 0; c < nc; ++c) {
-            while (left[c].load(std::memory_order_acquire) != 0) {
-                if (pool.empty()) break;
-                std::this_thread::sleep_for(std::chrono::microseconds(20));
+            if (pool.empty()) work();
+            // DMA each chunk once copied: its staged proofs, adjacent ones as one copy
+            for (size_t c = 0; c < nc; ++c) {
+                while (left[c].load(std::memory_order_acquire) != 0) {
+                    if (pool.empty()) break;
+                    std::this_thread::sleep_for(std::chrono::microseconds(20));
+                }
+                for (size_t q = cut[c]; q < cut[c + 1];) {
+                    size_t r = q + 1;
+                    while (r < cut[c + 1] && todo[r] == todo[r - 1] + 1) ++r;
+                    const size_t i0 = todo[q], i1 = todo[r - 1];
+                    dma(pin[i0].off, stage + pin[i0].off, pin[i1].off + pin[i1].len - pin[i0].off);
+                    q = r;
+                }
             }
-            for (size_t q = cut[c]; q < cut[c + 1];) {
-                size_t r = q + 1;
-                while (r < cut[c + 1] && todo[r] == todo[r - 1] + 1) ++r;
-                const size_t i0 = todo[q], i1 = todo[r - 1];
-                dma(pin[i0].off, stage + pin[i0].off, pin[i1].off + pin[i1].len - pin[i0].off);
-                q = r;
-            }
+            for (auto& th : pool) th.join();
+            dma(H.proof_words, stage + H.proof_words, H.words_total - H.proof_words);
+            if (stage == pageable.data() && e == hipSuccess) e = hipStreamSynchronize(st);  // pageable source
         }
-        for (auto& th : pool) th.join();
-        dma(H.proof_words, stage + H.proof_words, H.words_total - H.proof_words);
-        if (stage == pageable.data() && e == hipSuccess) e = hipStreamSynchronize(st);  // pageable source
-    }
-    const auto t1 = std::chrono::steady_clock::now();
-    b->stage_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-    if (e != hipSuccess) {
-        (void)hipStreamSynchronize(st);
-        if (scr) b->dwords = nullptr;
-        return fail_out(hipfail(e));
-    }
-    nhip_air::Dev adev{};
-    int rc = air_upload(ctx, air, &adev);
-    if (rc) {
-        (void)hipStreamSynchronize(st);
-        return fail_out(rc);
-    }
-    {
-        static std::mutex attrs_mu;
-        static uint64_t attrs_set = 0;  // devices whose kernel attributes are set
-        std::lock_guard<std::mutex> attrs_lock(attrs_mu);
-        const int adevice = nhip_internal_device(ctx);
-        if (adevice >= 64 || !((attrs_set >> adevice) & 1u)) {
-            if (stark_set_kernel_attributes() != hipSuccess) {
-                (void)hipStreamSynchronize(st);
-                return fail_out(NHIP_ERR_HIP);
-            }
-            if (adevice < 64) attrs_set |= 1ull << adevice;
-        }
-    }
-    const uint32_t k = D.d.num_checks;
-    // multiproof op capacity per (level, shard): a tree of height h has at most min(k, 2^(h-1-l))
-    // parents at level l; shard = proof index % MP_SHARDS
-    const uint32_t tpp = 4 + H.max_R;
-    const uint32_t levels = H.levels;
-    std::vector<uint64_t> mp_scap((size_t)levels * MP_SHARDS, 0), mp_sbase((size_t)levels * MP_SHARDS, 0);
-    b->mp_cap.assign(levels, 0);
-    for (size_t i = 0; i < n; ++i) {
-        if (pin[i].sized_log2_ph == SHAPE_NONE) continue;
-        const ProofShape& s = shp[i];
-        const uint32_t sh = (uint32_t)(i % MP_SHARDS);
-        for (uint32_t t = 0; t < 4 + s.R; ++t) {
-            const uint32_t h = t < 4 ? s.log2_N : s.log2_N - (t - 4);
-            for (uint32_t l = 0; l < h; ++l)
-                mp_scap[(size_t)l * MP_SHARDS + sh] += std::min<uint64_t>(k, 1ull << std::min(h - 1 - l, 40u));
-        }
-    }
-    uint64_t mp_total = 0;
-    for (uint32_t l = 0; l < levels; ++l)
-        for (uint32_t q = 0; q < MP_SHARDS; ++q) {
-            mp_sbase[(size_t)l * MP_SHARDS + q] = mp_total;
-            mp_total += mp_scap[(size_t)l * MP_SHARDS + q];
-            b->mp_cap[l] += mp_scap[(size_t)l * MP_SHARDS + q];
-        }
-    const size_t N1 = std::max<size_t>(1, n);
-    const size_t sz[] = {8,  // (slot 0 unused: the words have their own allocation)
-                         N1 * sizeof(ProofDesc),
-                         N1 * H.fs_stride * sizeof(FsOp),
-                         N1 * H.xs_stride * 24,
-                         N1 * k * 4,
-                         N1 * 3 * k * 40,
-                         N1 * 9 * 8,
-                         N1 * 4,
-                         N1 * sizeof(ProofIn),
-                         N1,
-                         CNT_N * 8,
-                         mp_total * 16 + 16,
-                         mp_total * 40 + 40,
-                         (size_t)levels * MP_SHARDS * 8 + 8,
-                         (size_t)levels * MP_SHARDS * 8 + 8,
-                         (size_t)levels * MP_SHARDS * 4 + 4,
-                         N1 * tpp * sizeof(MpRoot),
-                         N1 * (1 + H.max_R) * k * 8,
-                         N1 * (1 + H.max_R) * 4,
-                         N1 * k * 8,
-                         N1 * H.max_last_cw * 40,
-                         // OOD slots past the LDS budget (an AIR larger than ~6K live XFEs)
-                         N1 * (size_t)(air->slots - std::min<uint32_t>(air->slots, AIR_LDS_SLOTS_MAX)) * 24 + 24};
-    constexpr int NBUF = sizeof(sz) / sizeof(sz[0]);
-    size_t total = 0;
-    for (size_t x : sz) total += al(x);
-    if (scr) {  // grow-only device scratch of the context
-        if (scr->dmem_bytes < total) {
+        const auto t1 = std::chrono::steady_clock::now();
+        b->stage_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        if (e != hipSuccess) {
             (void)hipStreamSynchronize(st);
-            if (scr->dmem) (void)hipFree(scr->dmem);
-            scr->dmem = nullptr;
-            scr->dmem_bytes = 0;
-            e = hipMalloc(&scr->dmem, total + total / 4);
-            if (e == hipSuccess) scr->dmem_bytes = total + total / 4;
+            if (scr) b->dwords = nullptr;
+            return fail_out(hipfail(e));
         }
-        b->dmem = scr->dmem;
-    } else if (b->dmem_bytes < total) {  // new batch, or a refill that no longer fits
-        (void)hipStreamSynchronize(st);
-        if (b->dmem) (void)hipFree(b->dmem);
-        b->dmem = nullptr;
-        b->dmem_bytes = 0;
-        const size_t want = reuse ? total + total / 4 : total;
-        e = hipMalloc(&b->dmem, want);
-        if (e == hipSuccess) b->dmem_bytes = want;
+        nhip_air::Dev adev{};
+        int rc = air_upload(ctx, air, &adev);
+        if (rc) {
+            (void)hipStreamSynchronize(st);
+            return fail_out(rc);
+        }
+        {
+            static std::mutex attrs_mu;
+            static uint64_t attrs_set = 0;  // devices whose kernel attributes are set
+            std::lock_guard<std::mutex> attrs_lock(attrs_mu);
+            const int adevice = nhip_internal_device(ctx);
+            if (adevice >= 64 || !((attrs_set >> adevice) & 1u)) {
+                if (stark_set_kernel_attributes() != hipSuccess) {
+                    (void)hipStreamSynchronize(st);
+                    return fail_out(NHIP_ERR_HIP);
+                }
+                if (adevice < 64) attrs_set |= 1ull << adevice;
+            }
+        }
+        const uint32_t k = D.d.num_checks;
+        // multiproof op capacity per (level, shard): a tree of height h has at most min(k, 2^(h-1-l))
+        // parents at level l; shard = proof index % MP_SHARDS
+        const uint32_t tpp = 4 + H.max_R;
+        const uint32_t levels = H.levels;
+        std::vector<uint64_t> mp_scap((size_t)levels * MP_SHARDS, 0), mp_sbase((size_t)levels * MP_SHARDS, 0);
+        b->mp_cap.assign(levels, 0);
+        for (size_t i = 0; i < n; ++i) {
+            if (pin[i].sized_log2_ph == SHAPE_NONE) continue;
+            const ProofShape& s = shp[i];
+            const uint32_t sh = (uint32_t)(i % MP_SHARDS);
+            for (uint32_t t = 0; t < 4 + s.R; ++t) {
+                const uint32_t h = t < 4 ? s.log2_N : s.log2_N - (t - 4);
+                for (uint32_t l = 0; l < h; ++l)
+                    mp_scap[(size_t)l * MP_SHARDS + sh] += std::min<uint64_t>(k, 1ull << std::min(h - 1 - l, 40u));
+            }
+        }
+        uint64_t mp_total = 0;
+        for (uint32_t l = 0; l < levels; ++l)
+            for (uint32_t q = 0; q < MP_SHARDS; ++q) {
+                mp_sbase[(size_t)l * MP_SHARDS + q] = mp_total;
+                mp_total += mp_scap[(size_t)l * MP_SHARDS + q];
+                b->mp_cap[l] += mp_scap[(size_t)l * MP_SHARDS + q];
+            }
+        const size_t N1 = std::max<size_t>(1, n);
+        const size_t sz[] = {8,  // (slot 0 unused: the words have their own allocation)
+                             N1 * sizeof(ProofDesc),
+                             N1 * H.fs_stride * sizeof(FsOp),
+                             N1 * H.xs_stride * 24,
+                             N1 * k * 4,
+                             N1 * 3 * k * 40,
+                             N1 * 9 * 8,
+                             N1 * 4,
+                             N1 * sizeof(ProofIn),
+                             N1,
+                             CNT_N * 8,
+                             mp_total * 16 + 16,
+                             mp_total * 40 + 40,
+                             (size_t)levels * MP_SHARDS * 8 + 8,
+                             (size_t)levels * MP_SHARDS * 8 + 8,
+                             (size_t)levels * MP_SHARDS * 4 + 4,
+                             N1 * tpp * sizeof(MpRoot),
+                             N1 * (1 + H.max_R) * k * 8,
+                             N1 * (1 + H.max_R) * 4,
+                             N1 * k * 8,
+                             N1 * H.max_last_cw * 40,
+                             // OOD slots past the LDS budget (an AIR larger than ~6K live XFEs)
+                             N1 * (size_t)(air->slots - std::min<uint32_t>(air->slots, AIR_LDS_SLOTS_MAX)) * 24 + 24};
+        constexpr int NBUF = sizeof(sz) / sizeof(sz[0]);
+        size_t total = 0;
+        for (size_t x : sz) total += al(x);
+        if (scr) {  // grow-only device scratch of the context
+            if (scr->dmem_bytes < total) {
+                (void)hipStreamSynchronize(st);
+                if (scr->dmem) (void)hipFree(scr->dmem);
+                scr->dmem = nullptr;
+                scr->dmem_bytes = 0;
+                e = hipMalloc(&scr->dmem, total + total / 4);
+                if (e == hipSuccess) scr->dmem_bytes = total + total / 4;
+            }
+            b->dmem = scr->dmem;
+        } else if (b->dmem_bytes < total) {  // new batch, or a refill that no longer fits
+            (void)hipStreamSynchronize(st);
+            if (b->dmem) (void)hipFree(b->dmem);
+            b->dmem = nullptr;
+            b->dmem_bytes = 0;
+            const size_t want = reuse ? total + total / 4 : total;
+            e = hipMalloc(&b->dmem, want);
+            if (e == hipSuccess) b->dmem_bytes = want;
+        }
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(st);
+            if (scr) b->dmem = nullptr;
+            return fail_out(hipfail(e));
+        }
+        char* p = (char*)b->dmem;
+        void* ptr[NBUF];
+        for (int i = 0; i < NBUF; ++i) {
+            ptr[i] = p;
+            p += al(sz[i]);
+        }
+        if (n) e = hipMemcpyAsync(ptr[8], pin.data(), n * sizeof(ProofIn), hipMemcpyHostToDevice, st);
+        if (e == hipSuccess && levels)
+            e = hipMemcpyAsync(ptr[13], mp_sbase.data(), mp_sbase.size() * 8, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess && levels)
+            e = hipMemcpyAsync(ptr[14], mp_scap.data(), mp_scap.size() * 8, hipMemcpyHostToDevice, st);
+        {
+            const hipError_t es = hipStreamSynchronize(st);  // the sources are host vectors / the staging
+            if (e == hipSuccess) e = es;
+        }
+        const auto t2 = std::chrono::steady_clock::now();
+        b->upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+        if (e != hipSuccess) return fail_out(hipfail(e));
+        StarkBatchDev& dv = b->dev;
+        dv.n_proofs = (uint32_t)n;
+        dv.max_R = H.max_R;
+        dv.dims = D.d;
+        dv.D = D;
+        dv.fs_stride = H.fs_stride;
+        dv.xs_stride = H.xs_stride;
+        dv.words = d_words;
+        dv.desc = (ProofDesc*)ptr[1];
+        dv.ops = (FsOp*)ptr[2];
+        dv.xs = (uint64_t*)ptr[3];
+        dv.idx = (uint32_t*)ptr[4];
+        dv.dig = (uint64_t*)ptr[5];
+        dv.ood = (uint64_t*)ptr[6];
+        dv.fail = (uint32_t*)ptr[7];
+        dv.in = (const ProofIn*)ptr[8];
+        dv.verdicts = (uint8_t*)ptr[9];
+        dv.counters = (unsigned long long*)ptr[10];
+        dv.mp.ops = (uint64_t*)ptr[11];
+        dv.mp.arena = (uint64_t*)ptr[12];
+        dv.mp.shard_base = (const uint64_t*)ptr[13];
+        dv.mp.shard_cap = (const uint64_t*)ptr[14];
+        dv.mp.counter = (uint32_t*)ptr[15];
+        dv.mp.roots = (MpRoot*)ptr[16];
+        dv.mp.dups = (uint32_t*)ptr[17];
+        dv.mp.ndup = (uint32_t*)ptr[18];
+        dv.mp.levels = levels;
+        dv.xdom = (uint64_t*)ptr[19];
+        dv.lcw = (uint64_t*)ptr[20];
+        dv.max_lcw = H.max_last_cw;
+        dv.mp_cap_host = b->mp_cap.data();
+        dv.air_prog = adev.d_prog;
+        dv.air_prog_off = adev.d_prog_off;
+        dv.air_n_levels = (uint32_t)air->prog_off.size() - 1;
+        dv.air_consts = adev.d_consts;
+        dv.air_cons_off = air->cons_off;
+        dv.air_lds_slots = std::min<uint32_t>(air->slots, AIR_LDS_SLOTS_MAX);
+        dv.air_gslot_n = air->slots - dv.air_lds_slots;
+        dv.air_gslots = (Xfe*)ptr[21];
+        dv.air_lds_bytes = AIR_LDS_HEADER + (size_t)dv.air_lds_slots * 24;
+        // 256 threads per proof: 1,024-thread workgroups for a triton-air-sized circuit (one workgroup
+        // per CU either way, the slot area fills its LDS) ran the 256-proof evaluation 0.248 -> 0.213 ms
+        // alone but took the wave slots the concurrent hashing needs (config 4: 354k -> 305k proofs/s)
+        dv.air_block = 256u;
+        *out = b;
+        return NHIP_OK;
+    } catch (const std::bad_alloc&) {
+        (void)hipStreamSynchronize(nhip_internal_stream(ctx));
+        if (scr) {
+            b->dwords = nullptr;
+            b->dmem = nullptr;
+        }
+        return fail_out(NHIP_ERR_OOM);
     }
-    if (e != hipSuccess) {
-        (void)hipStreamSynchronize(st);
-        if (scr) b->dmem = nullptr;
-        return fail_out(hipfail(e));
-    }
-    char* p = (char*)b->dmem;
-    void* ptr[NBUF];
-    for (int i = 0; i < NBUF; ++i) {
-        ptr[i] = p;
-        p += al(sz[i]);
-    }
-    if (n) e = hipMemcpyAsync(ptr[8], pin.data(), n * sizeof(ProofIn), hipMemcpyHostToDevice, st);
-    if (e == hipSuccess && levels)
-        e = hipMemcpyAsync(ptr[13], mp_sbase.data(), mp_sbase.size() * 8, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess && levels)
-        e = hipMemcpyAsync(ptr[14], mp_scap.data(), mp_scap.size() * 8, hipMemcpyHostToDevice, st);
-    {
-        const hipError_t es = hipStreamSynchronize(st);  // the sources are host vectors / the staging
-        if (e == hipSuccess) e = es;
-    }
-    const auto t2 = std::chrono::steady_clock::now();
-    b->upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
-    if (e != hipSuccess) return fail_out(hipfail(e));
-    StarkBatchDev& dv = b->dev;
-    dv.n_proofs = (uint32_t)n;
-    dv.max_R = H.max_R;
-    dv.dims = D.d;
-    dv.D = D;
-    dv.fs_stride = H.fs_stride;
-    dv.xs_stride = H.xs_stride;
-    dv.words = d_words;
-    dv.desc = (ProofDesc*)ptr[1];
-    dv.ops = (FsOp*)ptr[2];
-    dv.xs = (uint64_t*)ptr[3];
-    dv.idx = (uint32_t*)ptr[4];
-    dv.dig = (uint64_t*)ptr[5];
-    dv.ood = (uint64_t*)ptr[6];
-    dv.fail = (uint32_t*)ptr[7];
-    dv.in = (const ProofIn*)ptr[8];
-    dv.verdicts = (uint8_t*)ptr[9];
-    dv.counters = (unsigned long long*)ptr[10];
-    dv.mp.ops = (uint64_t*)ptr[11];
-    dv.mp.arena = (uint64_t*)ptr[12];
-    dv.mp.shard_base = (const uint64_t*)ptr[13];
-    dv.mp.shard_cap = (const uint64_t*)ptr[14];
-    dv.mp.counter = (uint32_t*)ptr[15];
-    dv.mp.roots = (MpRoot*)ptr[16];
-    dv.mp.dups = (uint32_t*)ptr[17];
-    dv.mp.ndup = (uint32_t*)ptr[18];
-    dv.mp.levels = levels;
-    dv.xdom = (uint64_t*)ptr[19];
-    dv.lcw = (uint64_t*)ptr[20];
-    dv.max_lcw = H.max_last_cw;
-    dv.mp_cap_host = b->mp_cap.data();
-    dv.air_prog = adev.d_prog;
-    dv.air_prog_off = adev.d_prog_off;
-    dv.air_n_levels = (uint32_t)air->prog_off.size() - 1;
-    dv.air_consts = adev.d_consts;
-    dv.air_cons_off = air->cons_off;
-    dv.air_lds_slots = std::min<uint32_t>(air->slots, AIR_LDS_SLOTS_MAX);
-    dv.air_gslot_n = air->slots - dv.air_lds_slots;
-    dv.air_gslots = (Xfe*)ptr[21];
-    dv.air_lds_bytes = AIR_LDS_HEADER + (size_t)dv.air_lds_slots * 24;
-    // 256 threads per proof: 1,024-thread workgroups for a triton-air-sized circuit (one workgroup
-    // per CU either way, the slot area fills its LDS) ran the 256-proof evaluation 0.248 -> 0.213 ms
-    // alone but took the wave slots the concurrent hashing needs (config 4: 354k -> 305k proofs/s)
-    dv.air_block = 256u;
-    *out = b;
-    return NHIP_OK;
 }
 }  // namespace
 
