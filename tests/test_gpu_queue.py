@@ -98,3 +98,40 @@ def test_queue_bad_arguments_stay_with_the_caller(ctx, pool_batch):
         assert rc == _lib.NHIP_ERR_ARG
         assert q.verify_many([(claims[0], [1, 2, 3]), (claims[1], proofs[1])]) == [False, bool(expect[1])]
         assert ctypes.sizeof(_lib.Proof) == 16
+
+
+def test_queue_mixed_request_sizes_small_max_batch(ctx, pool_batch):
+    """Requests of 1-20 proofs from 16 threads through a queue capped at 8 proofs per batch: a
+    request larger than the cap runs as a batch of its own, smaller ones are coalesced up to the cap,
+    every caller gets exactly its own verdicts (corrupted proofs of one caller do not touch another
+    caller's), and the slots are refilled with batches of varying size throughout."""
+    NS = _ns()
+    gair, claims, proofs, expect = pool_batch
+    n = len(proofs)
+    rng = np.random.default_rng(0x9E)
+    reqs = []
+    for _ in range(48):
+        k = int(rng.integers(1, 21))
+        idx = [int(x) for x in rng.integers(0, n, size=k)]
+        reqs.append(idx)
+    out = [None] * len(reqs)
+    errors = []
+    with NS.Queue(ctx, gair, NS.Stark.default(), max_batch=8, max_wait_us=300) as q:
+        def worker(w):
+            try:
+                for r in range(w, len(reqs), 16):
+                    out[r] = q.verify_many([(claims[i], proofs[i]) for i in reqs[r]])
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+
+        ths = [threading.Thread(target=worker, args=(w,)) for w in range(16)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        st = q.stats()
+    assert not errors
+    for r, idx in enumerate(reqs):
+        assert out[r] == [bool(expect[i]) for i in idx], r
+    total = sum(len(x) for x in reqs)
+    assert st["proofs"] == total and st["batches"] >= total // 20, st
