@@ -1,5 +1,6 @@
 // Internal launch wrappers (C++ linkage) shared between kernel TUs and the C-ABI layer.
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -40,6 +41,16 @@ static constexpr uint64_t MP_WIDE_MAX_OPS = 48 * 1024;
 // by one workgroup in one launch (k_mp_hash_tail), up to MP_TAIL_LEVELS_MAX levels
 static constexpr uint64_t MP_TAIL_MAX_OPS = 256;
 static constexpr uint32_t MP_TAIL_LEVELS_MAX = 32;
+// batches of at most this many proofs climb every tree in its own workgroup (k_mp_climb), one
+// launch for all levels, instead of one launch per level
+static constexpr uint32_t MP_CLIMB_MAX_PROOFS = 32;
+inline uint32_t climb_max_proofs() {  // NHIP_CLIMB_MAX overrides (A/B runs)
+    static const uint32_t v = [] {
+        const char* e = std::getenv("NHIP_CLIMB_MAX");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : MP_CLIMB_MAX_PROOFS;
+    }();
+    return v;
+}
 // batches below this many proofs replay Fiat-Shamir on the two-row pair Tip5 (k_fs_replay_wide):
 // one-collection latency 1.89 -> 1.65 ms, while from 512 proofs on (several steps in flight) the
 // one-row form is 2-3% faster (profiles/r01i/ab_pair.log)
@@ -59,6 +70,11 @@ struct MpPlan {
     uint32_t* dups;               // [n_proofs][1 + max_R][k] (slot, earlier slot) pairs of equal leaf indices
     uint32_t* ndup;               // [n_proofs][1 + max_R]
     uint32_t levels;
+    // per (proof, tree group) and level: the group's first op and its ops per tree (written by the
+    // plan; k_mp_climb walks them), and the number of levels recorded
+    uint64_t* lvl_g0;   // [n_proofs][1 + max_R][levels]
+    uint32_t* lvl_cnt;  // [n_proofs][1 + max_R][levels]
+    uint32_t* lvl_n;    // [n_proofs][1 + max_R]
 };
 
 // One proof of a batch as staged for k_decode: its raw words and its staged claim encoding in the
@@ -112,8 +128,9 @@ struct StarkBatchDev {
 };
 
 // events: 0 start (after k_decode, aux stream) | fs | rows | mp plan | mp hash levels | mp roots | ood | fri | deep | 9 verdicts
-// 10: main stream at the aux-chain release point, 11: aux stream after that wait, 12: before k_decode
-static constexpr int STARK_EVENTS = 13;
+// 10: main stream at the aux-chain release point, 11: aux stream after that wait, 12: before k_decode,
+// 13: before FRI on the main stream (small batches)
+static constexpr int STARK_EVENTS = 14;
 struct StarkPhaseTimer {
     hipEvent_t ev[STARK_EVENTS];
     hipEvent_t lev[2 * MAX_HASH_LAUNCHES];  // per hash launch: dispatch begin / end (nullptr = untimed)

@@ -705,7 +705,11 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
                              N1 * k * 8,
                              N1 * H.max_last_cw * 40,
                              // OOD slots past the LDS budget (an AIR larger than ~6K live XFEs)
-                             N1 * (size_t)(air->slots - std::min<uint32_t>(air->slots, AIR_LDS_SLOTS_MAX)) * 24 + 24};
+                             N1 * (size_t)(air->slots - std::min<uint32_t>(air->slots, AIR_LDS_SLOTS_MAX)) * 24 + 24,
+                             // per (proof, tree group, level) op ranges of the plan (k_mp_climb)
+                             N1 * (1 + H.max_R) * (size_t)(levels + 1) * 8,
+                             N1 * (1 + H.max_R) * (size_t)(levels + 1) * 4,
+                             N1 * (1 + H.max_R) * 4};
         constexpr int NBUF = sizeof(sz) / sizeof(sz[0]);
         size_t total = 0;
         for (size_t x : sz) total += al(x);
@@ -790,6 +794,9 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         dv.air_lds_slots = std::min<uint32_t>(air->slots, AIR_LDS_SLOTS_MAX);
         dv.air_gslot_n = air->slots - dv.air_lds_slots;
         dv.air_gslots = (Xfe*)ptr[21];
+        dv.mp.lvl_g0 = (uint64_t*)ptr[22];
+        dv.mp.lvl_cnt = (uint32_t*)ptr[23];
+        dv.mp.lvl_n = (uint32_t*)ptr[24];
         dv.air_lds_bytes = AIR_LDS_HEADER + (size_t)dv.air_lds_slots * 24;
         // 256 threads per proof: 1,024-thread workgroups for a triton-air-sized circuit (one workgroup
         // per CU either way, the slot area fills its LDS) ran the 256-proof evaluation 0.248 -> 0.213 ms
@@ -949,8 +956,9 @@ int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* al
         b->ph.hash = std::min(el(2, 4), el(3, 4));
         b->ph.roots = el(4, 5);
         b->ph.ood = el(11, 6);
-        b->ph.fri = el(6, 7);
-        b->ph.deep = el(7, 8);
+        const bool small = n <= climb_max_proofs();  // FRI on the main stream (launch_stark_phases)
+        b->ph.fri = small ? el(13, 7) : el(6, 7);
+        b->ph.deep = small ? el(6, 8) : el(7, 8);
         b->ph.total = el(12, 9);
     }
     const uint8_t* v = b->h_out + OUT_HDR + cnt_n * 4;

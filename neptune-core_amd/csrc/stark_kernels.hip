@@ -348,7 +348,10 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
     const uint32_t NT = grp == 0 ? 4u : 1u;
     const uint32_t tree0 = grp == 0 ? 0u : 3u + grp;  // tree id of this group's first tree
     if (tid < NT) plan.roots[(uint64_t)p * trees_per_proof + tree0 + tid].code = MPS_NONE;
-    if (tid == 0) plan.ndup[(uint64_t)p * (trees_per_proof - 3) + grp] = 0;
+    if (tid == 0) {
+        plan.ndup[(uint64_t)p * (trees_per_proof - 3) + grp] = 0;
+        plan.lvl_n[(uint64_t)p * (trees_per_proof - 3) + grp] = 0;
+    }
     if (fail[p] & FAIL_DECODE) return;
     if (grp > d.R) return;
     uint32_t h, auth_n[4], fail_bit[4];
@@ -430,7 +433,7 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
     if (tid == 0) plan.ndup[grp_id] = L.ndup;
     __syncthreads();
     // ---- climb on indices; emit one op per parent node and tree
-    uint32_t ap = 0;
+    uint32_t ap = 0, done = 0;
     int cur = 0;
     for (uint32_t lvl = 0; lvl < h; ++lvl) {
         const uint32_t i = tid;
@@ -457,6 +460,11 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
             if (tid == 0) L.bad = bad;
             break;  // uniform
         }
+        if (tid == 0) {
+            plan.lvl_g0[grp_id * plan.levels + lvl] = plan.shard_base[sidx] + base;
+            plan.lvl_cnt[grp_id * plan.levels + lvl] = n_own;
+        }
+        done = lvl + 1;
         if (owner) {
             const uint64_t g0 = plan.shard_base[sidx] + base + opos;
             for (uint32_t t = 0; t < NT; ++t) {
@@ -492,6 +500,7 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
         __syncthreads();
     }
     __syncthreads();
+    if (tid == 0) plan.lvl_n[grp_id] = done;
     if (tid < NT) {
         const uint32_t t = tid;
         const bool ok = !((L.bad >> t) & 1u) && m == 1 && L.key[cur][0] == 1u && ap == auth_n[t];
@@ -740,6 +749,66 @@ __global__ void __launch_bounds__(MP_TAIL_THREADS) k_mp_hash_tail(const uint64_t
             if (e < 5) o[e] = st;
         }
         __syncthreads();  // every parent of this level written before the next level reads it
+    }
+}
+
+// Small batches: one 1,024-thread workgroup per (proof, tree) climbs that tree's every level
+// itself (the plan's per-level op ranges of its group, this tree's share), 64 ops in flight on
+// 16-lane rows, a barrier between levels; grid.y = trees_per_proof is each proof's last-codeword
+// tree.  One launch replaces the per-level chain, whose ~14 us per level (9 of it dispatch latency)
+// is most of a small batch's Merkle phase.  A tree's parents depend only on its own earlier
+// levels, its leaves (row digests, done before this launch) and proof words.
+static constexpr uint32_t MP_CLIMB_THREADS = 1024;
+__global__ void __launch_bounds__(MP_CLIMB_THREADS) k_mp_climb(const uint64_t* __restrict__ words,
+                                                               const uint64_t* __restrict__ dig, MpPlan plan,
+                                                               uint32_t trees_per_proof,
+                                                               const ProofDesc* __restrict__ desc, uint32_t n_proofs,
+                                                               const uint32_t* __restrict__ fail, LcwTree lcw) {
+    latency_priority();
+    __shared__ Tip5Lds t5;
+    tip5_lds_init(t5);
+    const uint32_t p = blockIdx.x, y = blockIdx.y;
+    if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;  // uniform per workgroup
+    const uint32_t e = threadIdx.x & 15u, row0 = threadIdx.x >> 4;
+    constexpr uint32_t ROWS = MP_CLIMB_THREADS / 16;
+    uint64_t rcs[TIP5_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < TIP5_ROUNDS; ++r) rcs[r] = c_tip5_rc_raw[r * 16 + e];
+    if (y == trees_per_proof) {  // the last codeword's tree: every node
+        const ProofDesc& d = desc[p];
+        const uint32_t L = d.last_cw_n;
+        uint64_t* mine = lcw.nodes + (uint64_t)p * lcw.max_len * 5;
+        for (uint32_t lvl = 0; (L >> (lvl + 1)) > 0; ++lvl) {
+            const uint32_t cnt = L >> (lvl + 1);
+            for (uint32_t row = row0; row < cnt; row += ROWS) {  // uniform within the 16-lane row
+                const uint32_t v = cnt + row;
+                uint64_t st = MONT_ONE;
+                if (e < 5) st = lcw_node_word(words, d, mine, 2 * v, L, e);
+                else if (e < 10) st = lcw_node_word(words, d, mine, 2 * v + 1, L, e - 5);
+                st = tip5_permute_wide(st, e, rcs, t5.lut);
+                if (e < 5) mine[5ull * v + e] = st;
+            }
+            __syncthreads();
+        }
+        return;
+    }
+    const uint32_t grp = y < 4 ? 0u : y - 3u, sub = y < 4 ? y : 0u;
+    const uint64_t grp_id = (uint64_t)p * (trees_per_proof - 3) + grp;
+    const uint32_t nl = plan.lvl_n[grp_id];
+    for (uint32_t lvl = 0; lvl < nl; ++lvl) {
+        const uint64_t g0 = plan.lvl_g0[grp_id * plan.levels + lvl];
+        const uint32_t cnt = plan.lvl_cnt[grp_id * plan.levels + lvl];
+        for (uint32_t row = row0; row < cnt; row += ROWS) {  // uniform within the 16-lane row
+            const uint64_t g = g0 + (uint64_t)sub * cnt + row;
+            const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
+            if (lc == MPS_NONE) continue;  // a tree that already failed
+            uint64_t st = MONT_ONE;
+            if (e < 5) st = mp_load_word(lc, e, words, dig, plan.arena);
+            else if (e < 10) st = mp_load_word(rc, e - 5, words, dig, plan.arena);
+            st = tip5_permute_wide(st, e, rcs, t5.lut);
+            if (e < 5) plan.arena[5 * g + e] = st;
+        }
+        __syncthreads();
     }
 }
 
@@ -1286,6 +1355,11 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     const uint32_t k = b.dims.num_checks;
     const uint32_t tpp = 4 + b.max_R;
     auto mark = [&](int i, hipStream_t s) { (void)hipEventRecord(tm->ev[i], s); };
+    // small batches: every Merkle tree climbed in one launch (k_mp_climb), and FRI on the main
+    // stream (it needs only the sponge samples) concurrent with the plan and OOD on the aux stream;
+    // DEEP (which needs both) waits for it.  With the climb that short, OOD -> FRI -> DEEP in a row
+    // would be the critical path.
+    const bool small = n <= climb_max_proofs();
     // fork: the aux stream starts after everything already queued on st (counter resets)
     mark(12, st);
     (void)hipStreamWaitEvent(sa, tm->ev[12], 0);
@@ -1324,20 +1398,30 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         hipLaunchKernelGGL(k_hash_rows, dim3(gx, 3), dim3(256), 0, st, b.words, b.desc, n, k, b.dims, b.dig, b.fail);
     }
     mark(2, st);
+    if (small) {
+        (void)hipStreamWaitEvent(st, tm->ev[1], 0);  // sponge replay done
+        mark(13, st);
+        hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), 0, st, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
+        mark(7, st);
+    }
     (void)hipStreamWaitEvent(st, tm->ev[3], 0);  // plan done
     // The OOD / FRI / DEEP chain only needs the Fiat-Shamir samples, but its kernels are latency-bound
     // and hold CU resources for long; started after the first `aux_after_level` (wide, VALU-bound)
     // hash levels it overlaps the narrow, latency-bound top levels instead.
     auto launch_aux_chain = [&]() {
         mark(10, st);
-        (void)hipStreamWaitEvent(sa, tm->ev[10], 0);
+        if (!small) (void)hipStreamWaitEvent(sa, tm->ev[10], 0);  // small: OOD right after the plan
         mark(11, sa);
         hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(b.air_block), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims, b.air_prog,
                            b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs, b.ood, b.fail,
                            b.air_lds_slots, b.air_gslots, b.air_gslot_n);
         mark(6, sa);
-        hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
-        mark(7, sa);
+        if (small) {
+            (void)hipStreamWaitEvent(sa, tm->ev[7], 0);  // FRI done (main stream)
+        } else {
+            hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
+            mark(7, sa);
+        }
         const uint32_t S = deep_chunks(b.dims);
         hipLaunchKernelGGL(k_deep, dim3(n), dim3(S * k), deep_lds_bytes(b.dims), sa, b.words, b.desc, n, b.dims, S,
                            b.xs, b.xdom, b.ood, b.fail);
@@ -1345,6 +1429,15 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     };
     uint32_t launches = 0;
     bool aux_started = false;
+    if (small) {  // every tree climbed by its own workgroup, one launch
+        launch_aux_chain();
+        aux_started = true;
+        const bool timed = tm->lev[0] != nullptr;
+        hipExtLaunchKernelGGL(k_mp_climb, dim3(n, tpp + 1), dim3(MP_CLIMB_THREADS), 0, st,
+                              timed ? tm->lev[0] : nullptr, timed ? tm->lev[1] : nullptr, 0, b.words, b.dig, b.mp,
+                              tpp, b.desc, n, (const uint32_t*)b.fail, LcwTree{b.lcw, b.max_lcw});
+        launches = 1;
+    }
     const LcwTree lcw{b.lcw, b.max_lcw};
     const uint32_t log2_lcw = 31 - __builtin_clz(b.max_lcw);
     const uint32_t hash_levels = b.mp.levels > log2_lcw ? b.mp.levels : log2_lcw;
@@ -1357,7 +1450,7 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         --tail0;
     }
     if (hash_levels - tail0 < 2) tail0 = hash_levels;  // a single small level: the per-level launch
-    for (uint32_t l = 0; l < hash_levels; ++l) {
+    for (uint32_t l = 0; l < hash_levels && !small; ++l) {
         if (!aux_started && (l >= tm->aux_after_level || l == tail0)) {  // the tail is one workgroup
             launch_aux_chain();
             aux_started = true;
