@@ -396,3 +396,37 @@ def test_fs_row_and_pair_forms_agree(ctx):
         assert tb == ts and tb[2] == 0
     big.close()
     small.close()
+
+
+def test_merkle_climb_and_level_paths_agree(ctx):
+    """Batches of <= 32 proofs hash their Merkle trees with one workgroup per tree (k_mp_climb, FRI
+    beside the plan), larger ones level by level over all trees: the same 32 proofs (pool proofs and
+    copies with one word changed in their authentication structures, revealed rows, FRI data or
+    last codeword) give the same verdicts and transcripts in a 32-proof batch and inside a 96-proof
+    batch."""
+    NS = _ns()
+    air_w, pool = _pool()
+    gair = NS.Air([int(w) for w in air_w])
+    stark = NS.Stark.default()
+    rng = np.random.default_rng(0xC11B)
+    claims, proofs = [], []
+    for claim, proof, _ in pool:
+        claims.append(NS.Claim(*claim))
+        proofs.append(proof)
+    while len(proofs) < 32:
+        j = int(rng.integers(0, len(pool)))
+        m = pool[j][1].copy()
+        pos = int(rng.integers(len(m) // 4, len(m)))  # past the roots and OOD rows
+        m[pos] = np.uint64((int(m[pos]) + 1) % S.P)
+        claims.append(NS.Claim(*pool[j][0]))
+        proofs.append(m)
+    small = NS.Batch(ctx, gair, stark, claims, proofs)
+    big = NS.Batch(ctx, gair, stark, claims * 3, proofs * 3)
+    vs, _ = small.run()
+    vb, _ = big.run()
+    assert list(vb[64:96]) == list(vs) and list(vb[:32]) == list(vs)
+    assert all(vs[:len(pool)]) and not all(vs)
+    for i in range(32):
+        assert small.transcript(i) == big.transcript(64 + i), i
+    small.close()
+    big.close()
