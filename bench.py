@@ -379,6 +379,9 @@ def main():
                     help="AIR circuit: the pool's synthetic AIR (505 constraints, 3,151 nodes) or the same "
                          "constraints bloated to triton-air's size class (~21.7k nodes, stark_ref.bloat_air; "
                          "identically-zero extra terms, so the same proofs verify)")
+    ap.add_argument("--iso-steps", type=int, default=ISO_STEPS,
+                    help="steps run one at a time after the timed region for roofline_isolated (0 = none: a "
+                         "profiled run's kernel statistics then hold only in-flight steps)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
     ap.add_argument("--stream-batches", type=int, default=6,
@@ -509,14 +512,15 @@ def main():
     elapsed = time.perf_counter() - t_start
     # the same steps one at a time (nothing else on the device): the kernel's own roofline
     acc_iso, iso_ms = {}, 0.0
-    if R > 1 and ISO_STEPS:
+    iso_steps = args.iso_steps
+    if R > 1 and iso_steps:
         t_iso = time.perf_counter()
-        for _ in range(ISO_STEPS):
+        for _ in range(iso_steps):
             ring[0].launch()
             ring[0].wait()
             for k, x in ring[0].stats().items():
                 acc_iso[k] = acc_iso.get(k, 0.0) + x
-        iso_ms = (time.perf_counter() - t_iso) / ISO_STEPS * 1e3
+        iso_ms = (time.perf_counter() - t_iso) / iso_steps * 1e3
 
     if dist is not None:
         import torch
@@ -618,12 +622,13 @@ def main():
                                                        "ms_deep", "ms_device_total")},
         "host_prepare_ms": {"stage": st0["ms_decode"], "upload_wait": st0["ms_upload"], "total": prep_s * 1e3},
         "inflight": R,
+        "iso_steps": iso_steps if acc_iso else 0,
         "roofline": roofline(acc, K, step_ms, R, f"timed region, {R} step(s) in flight; per-launch HIP events "
                                                  f"(hipExtLaunchKernel start/stop)"),
     }
     if acc_iso:
-        res["roofline_isolated"] = roofline(acc_iso, ISO_STEPS, iso_ms, 1,
-                                            f"{ISO_STEPS} steps one at a time after the timed region; per-launch HIP "
+        res["roofline_isolated"] = roofline(acc_iso, iso_steps, iso_ms, 1,
+                                            f"{iso_steps} steps one at a time after the timed region; per-launch HIP "
                                             f"events (hipExtLaunchKernel start/stop)")
     valu_step, valu_tag = pmc_valu_per_step(args.config, len(proofs)) if args.air == "synthetic" else (None, None)
     if valu_step:

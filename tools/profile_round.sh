@@ -10,10 +10,13 @@ ARGS=${*:-"--steps 20 --warmup 5 --no-cpu --paths-log2 0 --stream-batches 0"}
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- python3 bench.py $ARGS > $OUT/bench_trace.json 2> $OUT/trace.err || exit 1
+# the kernel trace of in-flight steps only (--iso-steps 0): trace_kernel_stats.csv's Merkle-hash average
+# is then the bench roofline's own kernel_avg_ms; a second trace adds the one-at-a-time steps
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- python3 bench.py $ARGS --iso-steps 0 > $OUT/bench_trace.json 2> $OUT/trace.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_iso -o trace --output-format csv -- python3 bench.py $ARGS > $OUT/bench_trace_iso.json 2> $OUT/trace_iso.err || exit 1
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_LDS SQ_INSTS_SALU -d $OUT/pmc_valu -o pmc_valu --output-format csv -- python3 bench.py $ARGS > /dev/null 2> $OUT/pmc_valu.err || exit 1
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -d $OUT/pmc_cycles -o pmc_cycles --output-format csv -- python3 bench.py $ARGS > /dev/null 2> $OUT/pmc_cycles.err || exit 1
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o pmc_fetch --output-format csv -- python3 bench.py $ARGS > /dev/null 2> $OUT/pmc_fetch.err || exit 1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o pmc_write --output-format csv -- python3 bench.py $ARGS > /dev/null 2> $OUT/pmc_write.err || exit 1
-python3 tools/summarize_profile.py $OUT > $OUT/SUMMARY.md
+python3 tools/summarize_profile.py $OUT > $OUT/SUMMARY.md && python3 tools/summarize_profile.py $OUT iso >> $OUT/SUMMARY.md
 echo done
