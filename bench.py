@@ -397,7 +397,9 @@ def main():
     # their own hardware queues (streams sharing a queue serialize); the GPU boxes export HIP's
     # default of 4
     want_q = max(8, 2 * (args.inflight or 4) + 2)
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < want_q:
+    if os.environ.get("NHIP_BENCH_HWQ"):  # A/B runs: exactly this many
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ["NHIP_BENCH_HWQ"]
+    elif int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < want_q:
         os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
