@@ -395,8 +395,10 @@ def main():
     args = ap.parse_args()
     # before anything initialises HIP: R resident batches x 2 streams + the context stream need
     # their own hardware queues (streams sharing a queue serialize); the GPU boxes export HIP's
-    # default of 4
-    want_q = max(8, 2 * (args.inflight or 4) + 2)
+    # default of 4.  With several ranks, two more for torch's stream and RCCL's, so that no batch
+    # stream queues behind a collective waiting for the other ranks.
+    multi_rank = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    want_q = max(8, 2 * (args.inflight or 4) + 2 + (2 if multi_rank else 0))
     if os.environ.get("NHIP_BENCH_HWQ"):  # A/B runs: exactly this many
         os.environ["GPU_MAX_HW_QUEUES"] = os.environ["NHIP_BENCH_HWQ"]
     elif int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < want_q:
