@@ -402,7 +402,8 @@ def test_merkle_climb_and_level_paths_agree(ctx):
     """Batches of <= 32 proofs hash their Merkle trees with one workgroup per tree (k_mp_climb, FRI
     beside the plan), larger ones level by level over all trees: the same 32 proofs (pool proofs and
     copies with one word changed in their authentication structures, revealed rows, FRI data or
-    last codeword) give the same verdicts and transcripts in a 32-proof batch and inside a 96-proof
+    last codeword) give the same verdicts and transcripts in a 32-proof batch, inside a 48-proof batch
+    (per-level launches, the last small levels in one k_mp_hash_tail launch) and inside a 96-proof
     batch."""
     NS = _ns()
     air_w, pool = _pool()
@@ -421,12 +422,15 @@ def test_merkle_climb_and_level_paths_agree(ctx):
         claims.append(NS.Claim(*pool[j][0]))
         proofs.append(m)
     small = NS.Batch(ctx, gair, stark, claims, proofs)
+    mid = NS.Batch(ctx, gair, stark, claims + claims[:16], proofs + proofs[:16])  # levels + one-launch tail
     big = NS.Batch(ctx, gair, stark, claims * 3, proofs * 3)
     vs, _ = small.run()
+    vm, _ = mid.run()
     vb, _ = big.run()
-    assert list(vb[64:96]) == list(vs) and list(vb[:32]) == list(vs)
+    assert list(vb[64:96]) == list(vs) and list(vb[:32]) == list(vs) and list(vm[:32]) == list(vs)
     assert all(vs[:len(pool)]) and not all(vs)
     for i in range(32):
-        assert small.transcript(i) == big.transcript(64 + i), i
+        assert small.transcript(i) == big.transcript(64 + i) == mid.transcript(i), i
     small.close()
+    mid.close()
     big.close()
