@@ -1,0 +1,53 @@
+"""bench.py's use of the committed rocprofv3 profiles (profiles/LATEST): the PMC figures it attaches
+to the roofline and HBM fields come from the profile of the same workload (config and per-GPU proof
+count) or are left out, and the committed profile holds what DESIGN.md cites (trace, PMC passes,
+the default bench line with its roofline and cpu_baseline objects)."""
+import json
+import os
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _latest():
+    parts = open(os.path.join(ROOT, "profiles", "LATEST")).read().split()
+    return parts[0], int(parts[1]), int(parts[2])
+
+
+def test_latest_profile_is_keyed_by_workload():
+    tag, cfg, n = _latest()
+    assert bench.latest_profile(cfg, n) == tag
+    assert bench.latest_profile(cfg, n // 8) is None  # another per-GPU batch size
+    assert bench.latest_profile(3 if cfg != 3 else 4, n) is None
+
+
+def test_latest_profile_files_and_pmc_figures():
+    tag, cfg, n = _latest()
+    d = os.path.join(ROOT, "profiles", tag)
+    for f in ("SUMMARY.md", "bench_default.json", "bench_trace.json", "trace_kernel_stats.csv",
+              "pmc_valu_counter_collection.csv", "pmc_fetch_counter_collection.csv",
+              "pmc_write_counter_collection.csv"):
+        assert os.path.exists(os.path.join(d, f)), f
+    traffic, t_tag = bench.pmc_traffic("k_mp_hash", cfg, n)
+    valu, v_tag = bench.pmc_valu_per_step(cfg, n)
+    nbytes, b_tag = bench.pmc_bytes_per_step(cfg, n)
+    assert t_tag == v_tag == b_tag == tag
+    b = json.load(open(os.path.join(d, "bench_default.json")))
+    rf = b["roofline"]
+    # the level kernel moves about its algorithmic 80 B in + 40 B out per permutation
+    assert 0.8 < traffic / (rf["perms_per_launch"] * 120) < 1.5
+    assert valu > 1e9 and nbytes > 1e9
+    assert b["config"]["workload"].startswith("BASELINE config 4") and b["n_gpus"] == 1
+    assert rf["bound"] == "valu" and 0 < rf["frac"] < 1 and b["cpu_baseline"]["cores"] >= 1
+    assert b["verdicts_correct"] is True
+
+
+def test_summary_reproduces_the_bench_roofline():
+    """SUMMARY.md's figure from trace_kernel_stats.csv alone agrees with the bench's frac within 5%."""
+    tag, _, _ = _latest()
+    text = open(os.path.join(ROOT, "profiles", tag, "SUMMARY.md")).read()
+    line = next(x for x in text.splitlines() if x.startswith("Merkle hash launches in trace_kernel_stats.csv"))
+    frac_trace = float(line.split("T = ")[1].split(";")[0])
+    frac_bench = float(line.rsplit("frac ", 1)[1])
+    assert abs(frac_trace / frac_bench - 1) < 0.05, (frac_trace, frac_bench)
