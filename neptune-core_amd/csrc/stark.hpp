@@ -5,12 +5,14 @@
 // 1.0.0, Cargo.lock:4260; single call site neptune-core/src/protocol/proof_abstractions/
 // verifier.rs:60-63).  The verification of one proof is split into phases that run batched over
 // all proofs of a call (phase-synchronous design, SURVEY.md §7 "hard parts" 4):
-//   host   decode   : BFieldCodec proof stream -> ProofDesc (offsets into the batch word buffer)
-//   k_fs_replay     : Fiat-Shamir sponge replay, one lane per proof (challenges, weights, z, FRI
-//                     folding challenges, indices, last-round indeterminate)
+//   k_decode        : BFieldCodec proof stream -> ProofDesc (offsets into the batch word buffer)
+//                     and the proof's Fiat-Shamir program, one wave per proof (proof_codec.hpp)
+//   k_fs_replay_wide: Fiat-Shamir sponge replay, one 16-lane DPP row (two below 512 proofs) per
+//                     proof (challenges, weights, z, FRI folding challenges, indices)
 //   k_hash_rows     : Tip5::hash_varlen of every revealed main / aux / quotient row
-//   k_multiproof    : Merkle authentication structures (main, aux, quotient, FRI rounds), one
-//                     workgroup per (proof, tree)
+//   k_mp_plan, k_mp_hash*, k_mp_roots : Merkle authentication structures (main, aux, quotient,
+//                     FRI rounds): index-only plan per (proof, tree group), then one launch per
+//                     tree level over all trees of all proofs, then the root compares
 //   k_ood_air       : AIR circuit at the out-of-domain point, zerofiers, quotient identity; one
 //                     workgroup per proof, circuit levels evaluated in LDS
 //   k_fri           : collinearity folds, last codeword root / agreement / low degree
