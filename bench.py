@@ -12,9 +12,11 @@ tests/golden/c3_pool.npz (made by tests/golden/make_bench_pool.py), each stored 
 One step = whole verification of the rank's batch from its raw proof words in HBM: the proof-stream
 decode on the device (k_decode: ProofStream::try_from + the dequeue order of Stark::verify, every
 step again), Fiat-Shamir replay, row hashing, Merkle multiproofs, OOD AIR evaluation, FRI, DEEP, the
-verdict copy back (nhip_batch_launch / nhip_batch_wait) and, for N > 1, the batch verdict AND over
-ranks with one RCCL all-reduce(MIN) plus the all-gather of the per-proof verdicts (block validation
-needs every transaction's verdict: SURVEY.md §8e).  Steps are pipelined as a node verifying a stream
+verdict copy back (nhip_batch_launch / nhip_batch_wait) and, for N > 1, the verdict exchange: configs
+4 / 5 one RCCL all-gather per step of [batch verdict byte, per-proof verdict bytes] (the batch
+verdict is the MIN of the leading bytes; block validation needs every transaction's verdict:
+SURVEY.md §8e), posted without waiting and completed one step later, the last one inside the timed
+region (shard.VerdictExchange); config 3 one all-reduce(MIN) of the batch verdict.  Steps are pipelined as a node verifying a stream
 of batches runs them (--inflight 2): resident copies alternate, step k+1 is launched before step k
 is waited on, so one step's latency-bound phases overlap the other's VALU-bound hashing; every timed
 step is launched and waited inside the timed region.  Two copies x 2 streams need more than HIP's
@@ -464,7 +466,11 @@ def main():
     launched = []   # ring slots in flight, oldest first
     next_slot = [0]
     to_launch = [0]  # launches left in the current region: each region starts and ends with nothing in flight
-    gathered = [None]
+    # configs 4 / 5 with several ranks: one all-gather per step carries every rank's batch verdict
+    # and per-proof verdicts (shard.VerdictExchange), posted without waiting and completed one step
+    # later; config 3 (no per-proof exchange): the all-reduce(MIN) of the batch verdict
+    exch = shard.VerdictExchange(shards, total, dist) if (dist is not None and shards is not None) else None
+    exchanged = []  # (batch verdict, job verdict vector) of every completed exchange
 
     def launch_one():
         ring[next_slot[0]].launch()
@@ -483,11 +489,17 @@ def main():
         st = b.stats()
         if to_launch[0]:
             launch_one()
-        if dist is not None:
+        if exch is not None:  # block validation: every rank gets every proof's verdict
+            exch.post(ok, v)
+            if len(exch.pending) > 1:
+                exchanged.append(exch.complete())
+        elif dist is not None:
             ok = shard.all_ok(ok, dist)  # RCCL all-reduce(MIN) of the batch verdict
-            if shards is not None:  # block validation: every rank gets every proof's verdict
-                gathered[0] = shard.gather_verdicts(v, shards, total, dist)
         return st, v, ok
+
+    def drain_exchange():
+        while exch is not None and exch.pending:
+            exchanged.append(exch.complete())
 
     def barrier_sync():
         ctx.synchronize()
@@ -499,6 +511,8 @@ def main():
     to_launch[0] = args.warmup
     for _ in range(args.warmup):
         step()
+    drain_exchange()
+    exchanged.clear()
     barrier_sync()
     acc = {}
     batch_ok = None
@@ -508,12 +522,16 @@ def main():
     for _ in range(args.steps):
         st, v, batch_ok = step()
         correct = correct and bool((np.asarray(v, dtype=bool) == expect).all())
-        if gathered[0] is not None:
-            correct = correct and bool((gathered[0].astype(bool) == expect_all).all())
         for k, x in st.items():
             acc[k] = acc.get(k, 0.0) + x
+    drain_exchange()  # the last step's exchange completes inside the timed region
     barrier_sync()
     elapsed = time.perf_counter() - t_start
+    if exch is not None:
+        correct = correct and len(exchanged) == args.steps
+        for ok_all, full in exchanged:
+            correct = correct and bool((full.astype(bool) == expect_all).all())
+            batch_ok = ok_all
     # the same steps one at a time (nothing else on the device): the kernel's own roofline
     acc_iso, iso_ms = {}, 0.0
     iso_steps = args.iso_steps

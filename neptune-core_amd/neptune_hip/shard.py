@@ -54,6 +54,60 @@ def all_ok(local_ok: bool, dist) -> bool:
     return bool(t.item())
 
 
+class VerdictExchange:
+    """The per-step verdict exchange of a sharded batch as ONE collective, posted without waiting.
+
+    Every rank all-gathers ``[local_ok, verdict bytes of its shard (padded to the widest shard)]``;
+    the batch verdict is the MIN of the leading bytes (what ``all_ok``'s all-reduce(MIN) gives) and
+    the job's verdict vector is scattered from the rest (what ``gather_verdicts`` gives), so one
+    collective replaces the pair.  ``post`` enqueues the all-gather (``async_op``) on preallocated
+    double buffers and returns at once; ``complete`` waits for the oldest posted exchange and
+    returns ``(batch_ok, verdicts)``.  A caller keeps at most two exchanges posted (post step k,
+    complete step k - 1), so a slow collective never stalls the launch of the next GPU step.
+    """
+
+    def __init__(self, shards: List[List[int]], n: int, dist):
+        import torch
+        self.dist = dist
+        self.n = n
+        self.dev = _device_for(dist)
+        self.world = dist.get_world_size()
+        self.width = 1 + (max(len(s) for s in shards) if shards else 0)
+        self.index = [np.asarray(s, dtype=np.int64) for s in shards]
+        # gloo has no all_gather_into_tensor: per-rank views of the flat receive buffer instead
+        self.flat = self.dev.type == "cuda"
+        self.send = [torch.zeros(self.width, dtype=torch.uint8, device=self.dev) for _ in range(2)]
+        self.recv = [torch.zeros(self.world * self.width, dtype=torch.uint8, device=self.dev) for _ in range(2)]
+        self.pending: List[tuple] = []
+        self.slot = 0
+
+    def post(self, local_ok: bool, local: np.ndarray) -> None:
+        import torch
+        if len(self.pending) >= 2:
+            raise RuntimeError("VerdictExchange: complete() the oldest exchange before posting a third")
+        s = self.slot
+        self.slot ^= 1
+        host = np.zeros(self.width, dtype=np.uint8)
+        host[0] = 1 if local_ok else 0
+        host[1:1 + len(local)] = np.asarray(local, dtype=np.uint8)
+        self.send[s].copy_(torch.from_numpy(host))
+        if self.flat:
+            work = self.dist.all_gather_into_tensor(self.recv[s], self.send[s], async_op=True)
+        else:
+            work = self.dist.all_gather(list(self.recv[s].view(self.world, self.width)), self.send[s], async_op=True)
+        self.pending.append((s, work))
+
+    def complete(self):
+        s, work = self.pending.pop(0)
+        work.wait()
+        got = self.recv[s].view(self.world, self.width).cpu().numpy()
+        full = np.zeros(self.n, dtype=np.uint8)
+        for r, idx in enumerate(self.index):
+            if len(idx):
+                full[idx] = got[r, 1:1 + len(idx)]
+        return bool(got[:, 0].min()), full
+
+
 def gather_verdicts(local: np.ndarray, shards: List[List[int]], n: int, dist) -> np.ndarray:
     """All-gather per-unit verdict bytes; ``shards`` is the assignment every rank agrees on."""
     import torch

@@ -122,3 +122,65 @@ def test_two_rank_config4_stark_sharding():
     assert fulls[0] == fulls[1] and sum(fulls[0]) == 48 - 5
     for rank, ok, full, matches, sizes, gathered_ok in res:
         assert ok is False and all(matches) and sum(sizes) == 48 and gathered_ok
+
+
+def _exchange_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from neptune_hip import shard
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 37
+    costs = [(7 * i) % 11 + 1 for i in range(n)]
+    shards = shard.lpt_shard(costs, world)
+    mine = np.asarray(shards[rank], dtype=np.int64)
+    steps = []
+    for k in range(4):  # a different verdict vector per step: exchanges must complete in order
+        full = np.ones(n, dtype=np.uint8)
+        full[[k, (5 * k + 3) % n]] = 0
+        if k == 3:
+            full[:] = 1
+        steps.append(full)
+    ex = shard.VerdictExchange(shards, n, dist)
+    got = []
+    for k, full in enumerate(steps):
+        v = full[mine]
+        ex.post(bool(v.all()), v)
+        if len(ex.pending) > 1:
+            got.append(ex.complete())
+    try:
+        ex.post(True, steps[0][mine])
+        ex.post(True, steps[0][mine])  # a third posted exchange is refused
+        third = False
+    except RuntimeError:
+        third = True
+    while ex.pending:
+        got.append(ex.complete())
+    # the two-collective form gives the same answers
+    v = steps[1][mine]
+    pair = (shard.all_ok(bool(v.all()), dist), shard.gather_verdicts(v, shards, n, dist).tolist())
+    q.put((rank, [(ok, full.tolist()) for ok, full in got], [s.tolist() for s in steps], pair, third))
+    dist.destroy_process_group()
+
+
+def test_two_rank_verdict_exchange_one_collective():
+    """shard.VerdictExchange at world size 2 (gloo): one all-gather per step carries the batch verdict
+    (the MIN of every rank's leading byte) and the per-proof verdicts, exchanges posted two at a
+    time complete in posting order, and the answers equal all_ok + gather_verdicts."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, got, steps, pair, third in res:
+        assert third
+        assert len(got) == 5
+        for k, full in enumerate(steps):
+            assert got[k] == (all(full), full)
+        assert got[4] == (True, steps[0])  # the extra post: local_ok as given, step 0's verdicts
+        assert pair == (all(steps[1]), steps[1])
