@@ -127,9 +127,9 @@ def permutation_raw_pair(states_raw: np.ndarray):
     return a, b
 
 
-def stark_verify_batch(air_words, params, claims, proofs, threads: int = 1) -> np.ndarray:
-    """C restatement of the verifier (oracle/stark_oracle.c) over (claim, proof) pairs.
-    params: oracle StarkParams; claims: (digest, version, input, output) tuples; proofs: word lists."""
+def stark_batch_args(air_words, params, claims, proofs):
+    """The flat arguments of oracle_stark_verify_batch for (claim, proof) pairs, built once (the CPU
+    baseline times only the C verifier over them, not this marshaling)."""
     L = lib()
     fn = L.oracle_stark_verify_batch
     fn.argtypes = [_u64p, ctypes.c_size_t, np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS"),
@@ -162,8 +162,20 @@ def stark_verify_batch(air_words, params, claims, proofs, threads: int = 1) -> n
     ind, ino = flat([list(map(int, c[2])) for c in claims])
     outd, outo = flat([list(map(int, c[3])) for c in claims])
     prd, pro = flat(proofs)
+    return (air, air.size, pw, dig, ver, ind, ino, outd, outo, prd, pro, n)
+
+
+def stark_verify_args(args, threads: int = 1) -> np.ndarray:
+    """oracle_stark_verify_batch over stark_batch_args' arrays on `threads` host threads."""
+    n = args[-1]
     v = np.zeros(max(n, 1), dtype=np.uint8)
-    rc = fn(air, air.size, pw, dig, ver, ind, ino, outd, outo, prd, pro, n, v, threads)
+    rc = lib().oracle_stark_verify_batch(*args, v, threads)
     if rc != 0:
         raise ValueError("oracle_stark_verify_batch: malformed AIR or parameters")
     return v[:n]
+
+
+def stark_verify_batch(air_words, params, claims, proofs, threads: int = 1) -> np.ndarray:
+    """C restatement of the verifier (oracle/stark_oracle.c) over (claim, proof) pairs.
+    params: oracle StarkParams; claims: (digest, version, input, output) tuples; proofs: word lists."""
+    return stark_verify_args(stark_batch_args(air_words, params, claims, proofs), threads)

@@ -25,6 +25,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 
 #define P 0xFFFFFFFF00000001ull
 typedef unsigned __int128 u128;
@@ -36,6 +39,9 @@ static uint8_t LUT_STORE[256];
 static const uint64_t MDS[16] = {61402, 1108, 28750, 33823, 7454, 43244, 53865, 12034,
                                  56951, 27521, 41351, 40901, 12021, 59689, 26798, 17845};
 static int initialised = 0;
+/* MDS_COL[j][i] = MDS[(i - j) & 15]: column j of the circulant (the AVX2 accumulation below) */
+static uint64_t MDS_COL[16][16];
+static int have_avx2 = 0;
 
 /* twenty-first montyred: x (< p * 2^64) -> x * 2^-64 mod p, result in [0, p) */
 static inline uint64_t montyred(u128 x) {
@@ -65,6 +71,12 @@ void oracle_init(const uint64_t rc_raw[80]) {
     }
     LUT = LUT_STORE;
     memcpy(RC_RAW, rc_raw, sizeof(RC_RAW));
+    for (int j = 0; j < 16; ++j)
+        for (int i = 0; i < 16; ++i) MDS_COL[j][i] = MDS[(i - j) & 15];
+#if defined(__x86_64__)
+    __builtin_cpu_init();
+    have_avx2 = __builtin_cpu_supports("avx2");
+#endif
     initialised = 1;
 }
 
@@ -90,45 +102,101 @@ static void perm_raw(uint64_t s[16]) {
     }
 }
 
+/* MDS accumulators of twenty-first's split form: al[i] = sum_j c[(i-j)&15] * lo32(s[j]),
+ * ah[i] = the same over hi32(s[j]); each < 2^53, so plain 64-bit sums are exact. */
+static inline void mds_acc_scalar(const uint64_t s[16], uint64_t al[16], uint64_t ah[16]) {
+    for (int i = 0; i < 16; ++i) {
+        uint64_t a = 0, h = 0;
+        for (int j = 0; j < 16; ++j) {
+            a += MDS[(i - j) & 15] * (s[j] & 0xFFFFFFFFull);
+            h += MDS[(i - j) & 15] * (s[j] >> 32);
+        }
+        al[i] = a;
+        ah[i] = h;
+    }
+}
+
+#if defined(__x86_64__)
+/* The same sums with AVX2: column j of the circulant times the broadcast 32-bit half of s[j]
+ * (vpmuludq: 32 x 32 -> 64 per lane), 16 outputs in four 4-lane accumulators per half.  Selected
+ * at run time (oracle_init) when the host has AVX2; tests/test_stark_oracle_c.py checks the fast
+ * permutation against perm_raw either way. */
+__attribute__((target("avx2"))) static inline void mds_acc_avx2(const uint64_t s[16], uint64_t al[16], uint64_t ah[16]) {
+    __m256i a0 = _mm256_setzero_si256(), a1 = a0, a2 = a0, a3 = a0, h0 = a0, h1 = a0, h2 = a0, h3 = a0;
+    for (int j = 0; j < 16; ++j) {
+        const __m256i lo = _mm256_set1_epi64x((long long)(s[j] & 0xFFFFFFFFull));
+        const __m256i hi = _mm256_set1_epi64x((long long)(s[j] >> 32));
+        const __m256i m0 = _mm256_loadu_si256((const __m256i *)&MDS_COL[j][0]);
+        const __m256i m1 = _mm256_loadu_si256((const __m256i *)&MDS_COL[j][4]);
+        const __m256i m2 = _mm256_loadu_si256((const __m256i *)&MDS_COL[j][8]);
+        const __m256i m3 = _mm256_loadu_si256((const __m256i *)&MDS_COL[j][12]);
+        a0 = _mm256_add_epi64(a0, _mm256_mul_epu32(m0, lo));
+        h0 = _mm256_add_epi64(h0, _mm256_mul_epu32(m0, hi));
+        a1 = _mm256_add_epi64(a1, _mm256_mul_epu32(m1, lo));
+        h1 = _mm256_add_epi64(h1, _mm256_mul_epu32(m1, hi));
+        a2 = _mm256_add_epi64(a2, _mm256_mul_epu32(m2, lo));
+        h2 = _mm256_add_epi64(h2, _mm256_mul_epu32(m2, hi));
+        a3 = _mm256_add_epi64(a3, _mm256_mul_epu32(m3, lo));
+        h3 = _mm256_add_epi64(h3, _mm256_mul_epu32(m3, hi));
+    }
+    _mm256_storeu_si256((__m256i *)&al[0], a0);
+    _mm256_storeu_si256((__m256i *)&al[4], a1);
+    _mm256_storeu_si256((__m256i *)&al[8], a2);
+    _mm256_storeu_si256((__m256i *)&al[12], a3);
+    _mm256_storeu_si256((__m256i *)&ah[0], h0);
+    _mm256_storeu_si256((__m256i *)&ah[4], h1);
+    _mm256_storeu_si256((__m256i *)&ah[8], h2);
+    _mm256_storeu_si256((__m256i *)&ah[12], h3);
+}
+#endif
+
 /* The same permutation with twenty-first's MDS arithmetic (split into 32-bit halves, 64-bit
  * accumulation, s = lo + hi * 2^32 reduced as s_lo + s_hi * (2^32 - 1) with the overflow fix, then
  * BFieldElement addition of the round constant), used by the STARK oracle (stark_oracle.c) where
- * speed matters; tests/test_stark_oracle_c.py checks it against perm_raw. */
-void oracle_tip5_permutation_raw_fast(uint64_t s[16]) {
-    for (int r = 0; r < 5; ++r) {
-        for (int i = 0; i < 4; ++i) {
-            uint64_t v = s[i], o = 0;
-            for (int k = 0; k < 8; ++k) o |= (uint64_t)LUT[(v >> (8 * k)) & 0xFF] << (8 * k);
-            s[i] = o;
-        }
-        for (int i = 4; i < 16; ++i) {
-            uint64_t x = s[i], x2 = mmul(x, x), x4 = mmul(x2, x2);
-            s[i] = mmul(mmul(x, x2), x4);
-        }
-        uint64_t lo[16], hi[16];
-        for (int j = 0; j < 16; ++j) {
-            lo[j] = s[j] & 0xFFFFFFFFull;
-            hi[j] = s[j] >> 32;
-        }
-        for (int i = 0; i < 16; ++i) {
-            uint64_t al = 0, ah = 0;
-            for (int j = 0; j < 16; ++j) {
-                al += MDS[(i - j) & 15] * lo[j];
-                ah += MDS[(i - j) & 15] * hi[j];
-            }
-            const u128 sum = (u128)al + ((u128)ah << 32);
-            const uint64_t s_lo = (uint64_t)sum, s_hi = (uint64_t)(sum >> 64);
-            uint64_t res = s_lo + s_hi * 0xFFFFFFFFull;
-            if (res < s_lo) res += 0xFFFFFFFFull;
-            s[i] = res;
-        }
-        for (int i = 0; i < 16; ++i) {
-            const uint64_t q = P - RC_RAW[r * 16 + i];
-            uint64_t x1 = s[i] - q;
-            if (s[i] < q) x1 -= 0xFFFFFFFFull;  /* BFieldElement add: borrow -> + p (mod 2^64) */
-            s[i] = x1;
-        }
+ * speed matters (the CPU baseline); tests/test_stark_oracle_c.py checks it against perm_raw.
+ * The 12 x^7 chains are written stage by stage so the independent products overlap.  One body,
+ * compiled twice (MDS sums scalar, or AVX2 for hosts that have it; chosen per call). */
+#define TIP5_FAST_BODY(MDS_ACC)                                                          \
+    for (int r = 0; r < 5; ++r) {                                                        \
+        for (int i = 0; i < 4; ++i) {                                                    \
+            uint64_t v = s[i], o = 0;                                                    \
+            for (int k = 0; k < 8; ++k) o |= (uint64_t)LUT[(v >> (8 * k)) & 0xFF] << (8 * k); \
+            s[i] = o;                                                                    \
+        }                                                                                \
+        uint64_t x2[12], x3[12], x4[12];                                                 \
+        for (int i = 0; i < 12; ++i) x2[i] = mmul(s[4 + i], s[4 + i]);                   \
+        for (int i = 0; i < 12; ++i) {                                                   \
+            x4[i] = mmul(x2[i], x2[i]);                                                  \
+            x3[i] = mmul(x2[i], s[4 + i]);                                               \
+        }                                                                                \
+        for (int i = 0; i < 12; ++i) s[4 + i] = mmul(x3[i], x4[i]);                      \
+        uint64_t al[16], ah[16];                                                         \
+        MDS_ACC(s, al, ah);                                                              \
+        for (int i = 0; i < 16; ++i) {                                                   \
+            const u128 sum = (u128)al[i] + ((u128)ah[i] << 32);                          \
+            const uint64_t s_lo = (uint64_t)sum, s_hi = (uint64_t)(sum >> 64);           \
+            uint64_t res = s_lo + s_hi * 0xFFFFFFFFull;                                  \
+            if (res < s_lo) res += 0xFFFFFFFFull;                                        \
+            const uint64_t q = P - RC_RAW[r * 16 + i];                                   \
+            uint64_t x1 = res - q;                                                       \
+            if (res < q) x1 -= 0xFFFFFFFFull; /* BFieldElement add: borrow -> + p */     \
+            s[i] = x1;                                                                   \
+        }                                                                                \
     }
+
+static void perm_fast_scalar(uint64_t s[16]) { TIP5_FAST_BODY(mds_acc_scalar) }
+#if defined(__x86_64__)
+__attribute__((target("avx2"))) static void perm_fast_avx2(uint64_t s[16]) { TIP5_FAST_BODY(mds_acc_avx2) }
+#endif
+
+void oracle_tip5_permutation_raw_fast(uint64_t s[16]) {
+#if defined(__x86_64__)
+    if (have_avx2) {
+        perm_fast_avx2(s);
+        return;
+    }
+#endif
+    perm_fast_scalar(s);
 }
 uint64_t oracle_to_mont(uint64_t x) { return to_mont(x % P); }
 uint64_t oracle_from_mont(uint64_t r) { return from_mont(r); }
