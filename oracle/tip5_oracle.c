@@ -198,7 +198,14 @@ void oracle_tip5_permutation_raw_fast(uint64_t s[16]) {
 #endif
     perm_fast_scalar(s);
 }
-uint64_t oracle_to_mont(uint64_t x) { return to_mont(x % P); }
+/* Any u64 (read mod p) -> raw Montgomery word x * 2^64 mod p without a division: with x = h*2^32 + l
+ * and 2^64 == 2^32 - 1, x * 2^64 == l*2^32 - h - l, an integer in (-2^33, p - 1], so one conditional
+ * + p makes it canonical (the same word as to_mont(x % P); tests/test_stark_oracle_c.py). */
+uint64_t oracle_to_mont(uint64_t x) {
+    const uint64_t l = x & 0xFFFFFFFFull, h = x >> 32;
+    const uint64_t sum = h + l, t = l << 32, v = t - sum;
+    return t < sum ? v + P : v;
+}
 uint64_t oracle_from_mont(uint64_t r) { return from_mont(r); }
 void oracle_tip5_permutation_raw(uint64_t s[16]) { perm_raw(s); }
 
