@@ -10,7 +10,8 @@
 // own streams (nhip_verify_batch per member, one host thread each) and writes the verdicts back
 // in the caller's order.  The only exchange is the verdict bytes, which every member already
 // copies to the host; the batch AND is taken there.  (The multi-process form - one rank per GPU,
-// one RCCL all-reduce(MIN) of the batch verdict - is neptune_hip.shard / bench.py.)
+// one RCCL all-gather of the batch and per-proof verdicts per step - is neptune_hip.shard /
+// bench.py.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

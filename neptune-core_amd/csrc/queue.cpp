@@ -15,6 +15,7 @@
 // fault, never "accept").
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -132,7 +133,8 @@ struct nhip_queue {
             const Clock::time_point deadline = pending.front()->arrived + max_wait;
             cv_in.wait_until(lk, deadline, [&] { return stop || pending_proofs >= max_batch; });
             size_t taken = 0;
-            while (!pending.empty() && (taken == 0 || taken + pending.front()->n <= max_batch)) {
+            while (!pending.empty() && (taken == 0 || taken + pending.front()->n <= max_batch) &&
+                   in_slot[s].size() < in_slot[s].capacity()) {
                 Req* r = pending.front();
                 pending.pop_front();
                 pending_proofs -= r->n;
@@ -169,10 +171,16 @@ int nhip_queue_create(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* par
     q->max_batch = max_batch ? max_batch : 4096;
     q->max_wait = std::chrono::microseconds(max_wait_us);
     try {
+        // a slot holds at most max_batch requests (each of >= 1 proof): the worker's push_back
+        // under its lock never allocates
+        for (auto& v : q->in_slot) v.reserve(std::min<size_t>(q->max_batch, 1u << 16) + 1);
         q->worker = std::thread([q] { q->run(); });
     } catch (const std::system_error&) {
         delete q;
         return NHIP_ERR_HIP;
+    } catch (const std::bad_alloc&) {
+        delete q;
+        return NHIP_ERR_OOM;
     }
     *out = q;
     return NHIP_OK;
