@@ -675,9 +675,11 @@ def main():
                            "pmc_frac": bytes_step / step_s / HBM_PEAK, "pmc_profile": bytes_tag})
     for b in ring:
         b.close()
-    if rank == 0 and args.stream_batches > 0:
+    # the PCIe-inclusive leg and the config-2 microbench belong to the one-GPU report (N = 1): with
+    # several ranks, rank 0 would run them alone while the others tear down
+    if world == 1 and args.stream_batches > 0:
         res["pcie_inclusive"] = pcie_stream(ctx, gair, stark, claims, proofs, expect, args.stream_batches)
-    if rank == 0 and args.paths_log2 > 0:
+    if world == 1 and args.paths_log2 > 0:
         res["tip5_paths"] = tip5_paths(ctx, args.paths_log2, 5)
     if cpu is not None:
         res["cpu_baseline"] = cpu
@@ -685,6 +687,7 @@ def main():
         print(json.dumps(res), flush=True)
     ctx.close()
     if dist is not None:
+        dist.barrier()  # every rank tears its communicator down together
         dist.destroy_process_group()
     return 0 if correct else 1
 

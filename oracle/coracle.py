@@ -111,6 +111,11 @@ def mtree_verify_batch(roots, indices, leaves, paths, depth: int, nthreads: int 
     return verdicts[:n]
 
 
+def set_mds_avx2(on: bool) -> bool:
+    """The fast permutation's MDS form: AVX2 (where the host has it) or scalar; returns AVX2 in use."""
+    return bool(lib().oracle_set_mds_avx2(1 if on else 0))
+
+
 def permutation_raw_pair(states_raw: np.ndarray):
     """(reference-form perm_raw, twenty-first-MDS perm_raw_fast) of raw Montgomery states, for the
     cross-check of the two C permutations."""

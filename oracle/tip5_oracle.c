@@ -189,6 +189,18 @@ static void perm_fast_scalar(uint64_t s[16]) { TIP5_FAST_BODY(mds_acc_scalar) }
 __attribute__((target("avx2"))) static void perm_fast_avx2(uint64_t s[16]) { TIP5_FAST_BODY(mds_acc_avx2) }
 #endif
 
+/* Select the MDS form of the fast permutation (tests: both forms against perm_raw); AVX2 only where
+ * the host has it.  Returns the form in use afterwards (1 = AVX2). */
+int oracle_set_mds_avx2(int on) {
+#if defined(__x86_64__)
+    __builtin_cpu_init();
+    have_avx2 = on && __builtin_cpu_supports("avx2");
+#else
+    (void)on;
+#endif
+    return have_avx2;
+}
+
 void oracle_tip5_permutation_raw_fast(uint64_t s[16]) {
 #if defined(__x86_64__)
     if (have_avx2) {

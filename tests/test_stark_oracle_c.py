@@ -20,8 +20,14 @@ def test_fast_permutation_matches_reference_form():
     st[:8] = np.uint64(T.P - 1)
     st[8:16] = 0
     raw = np.array([[T.to_mont(int(x)) for x in row] for row in st], dtype=np.uint64)
-    a, b = C.permutation_raw_pair(raw)
-    assert (a == b).all()
+    avx2 = C.set_mds_avx2(True)
+    try:
+        for form in ([True, False] if avx2 else [False]):  # the MDS sums in AVX2 and scalar
+            assert C.set_mds_avx2(form) == form
+            a, b = C.permutation_raw_pair(raw)
+            assert (a == b).all()
+    finally:
+        C.set_mds_avx2(avx2)
 
 
 def _tiny():
