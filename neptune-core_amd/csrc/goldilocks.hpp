@@ -62,6 +62,30 @@ __host__ __device__ __forceinline__ uint64_t mont_mul(uint64_t a, uint64_t b) {
 
 __host__ __device__ __forceinline__ uint64_t mont_sqr(uint64_t a) { return mont_mul(a, a); }
 
+// The same product for latency-bound code (one dependent chain per lane: the sponge replay's row
+// Tip5).  A carry passed from one VALU instruction to the next through an SGPR pair costs ~14 cycles
+// on gfx950 (two mandatory wait states; neptune-core_amd/tools/valu_latency.hip), and montyred above
+// has five such links.  Here the sums are 64-bit values (v_mad_u64_u32 / v_lshl_add_u64, no carry
+// flags) and only the final sign test goes through VCC.  Exactly montyred's result for any 64-bit
+// inputs: with s = l0 + l1 (33 bits, e = s >> 32) and M = s_lo * (2^32 - 1) + l0, twenty-first's
+// b = a - (a >> 32) - e equals M - e (>= 0), so r = xh - b = E - M with E = xh + e (no overflow:
+// xh <= 2^64 - 2), + p when E < M.  More instructions (22 vs 17), ~half the dependent latency.
+__host__ __device__ __forceinline__ uint64_t mont_mul_lat(uint64_t a, uint64_t b) {
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
+    const uint32_t b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const uint64_t p00 = (uint64_t)a0 * b0;
+    const uint64_t t = (uint64_t)a0 * b1 + (p00 >> 32);
+    const uint64_t u = (uint64_t)a1 * b0 + (uint32_t)t;
+    const uint64_t v = (uint64_t)a1 * b1 + (t >> 32);
+    const uint64_t xh = v + (u >> 32);
+    const uint64_t l0 = (uint32_t)p00, l1 = (uint32_t)u;
+    const uint64_t sum = l1 + l0;
+    const uint64_t M = (uint64_t)(uint32_t)sum * 0xFFFFFFFFull + l0;
+    const uint64_t E = (sum >> 32) + xh;
+    const bool neg = E < M;
+    return (E + ~M) + (neg ? GL_P + 1 : 1ull);
+}
+
 // N independent Montgomery products, written stage by stage so that the carry-chain
 // instructions of different elements interleave (fills the VALU->VCC->VALU wait states that a
 // single chain would pad with s_nop).

@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
     for (int j = 0; j < 8; ++j) cm[j] = h ? TIP5_MDS[j + 8] : TIP5_MDS[j];
     auto permute = [&](uint64_t st) {
         if constexpr (PAIR) return tip5_permute_pair(st, e, h, rc, cm, lds.lut);
-        else return tip5_permute_wide(st, e, rc, lds.lut);
+        else return tip5_permute_wide<false>(st, e, rc, lds.lut);
     };
     const bool writer = h == 0;
     const ProofDesc& d = desc[g];
@@ -671,7 +671,7 @@ __global__ void __launch_bounds__(256) k_mp_hash_wide(const uint64_t* __restrict
     uint64_t rcs[TIP5_ROUNDS];
 #pragma unroll
     for (int r = 0; r < TIP5_ROUNDS; ++r) rcs[r] = c_tip5_rc_raw[r * 16 + e];
-    s = tip5_permute_wide(s, e, rcs, t5.lut);
+    s = tip5_permute_wide<false>(s, e, rcs, t5.lut);
     if (e < 5) o[e] = s;
 }
 
@@ -745,7 +745,7 @@ __global__ void __launch_bounds__(MP_TAIL_THREADS) k_mp_hash_tail(const uint64_t
                 else if (e < 10) st = lcw_node_word(words, d, mine, 2 * v + 1, L, e - 5);
                 o = mine + 5ull * v;
             }
-            st = tip5_permute_wide(st, e, rcs, t5.lut);
+            st = tip5_permute_wide<true>(st, e, rcs, t5.lut);
             if (e < 5) o[e] = st;
         }
         __syncthreads();  // every parent of this level written before the next level reads it
@@ -785,7 +785,7 @@ __global__ void __launch_bounds__(MP_CLIMB_THREADS) k_mp_climb(const uint64_t* _
                 uint64_t st = MONT_ONE;
                 if (e < 5) st = lcw_node_word(words, d, mine, 2 * v, L, e);
                 else if (e < 10) st = lcw_node_word(words, d, mine, 2 * v + 1, L, e - 5);
-                st = tip5_permute_wide(st, e, rcs, t5.lut);
+                st = tip5_permute_wide<true>(st, e, rcs, t5.lut);
                 if (e < 5) mine[5ull * v + e] = st;
             }
             __syncthreads();
@@ -805,7 +805,7 @@ __global__ void __launch_bounds__(MP_CLIMB_THREADS) k_mp_climb(const uint64_t* _
             uint64_t st = MONT_ONE;
             if (e < 5) st = mp_load_word(lc, e, words, dig, plan.arena);
             else if (e < 10) st = mp_load_word(rc, e - 5, words, dig, plan.arena);
-            st = tip5_permute_wide(st, e, rcs, t5.lut);
+            st = tip5_permute_wide<true>(st, e, rcs, t5.lut);
             if (e < 5) plan.arena[5 * g + e] = st;
         }
         __syncthreads();

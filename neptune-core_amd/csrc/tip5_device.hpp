@@ -170,6 +170,52 @@ __device__ __forceinline__ void tip5_permute_raw(uint64_t s[16], const uint8_t* 
 
 namespace nhip {
 
+// MDS reduction + round-constant add of one word, for the latency-bound row forms below: the same
+// steps as mds_ark() (s = al + ah * 2^32; (res, over) = s_lo.overflowing_add(s_hi * (2^32 - 1));
+// y = res + over * (2^32 - 1); x1 = y - q with q = p - rc; + p on borrow), written with 64-bit sums
+// and two VCC tests instead of carry chains through SGPRs (see mont_mul_lat): nq = -q mod 2^64,
+// x1 = y + nq, and the borrow of y - q is x1 > y (q >= 1).  Checked against the step-by-step form
+// on 2 x 10^8 random and boundary inputs; the GPU tests compare every sample with the oracle.
+__device__ __forceinline__ uint64_t mds_reduce_ark_lat(uint64_t al, uint64_t ah, uint64_t nq) {
+    const uint64_t w = (uint64_t)(uint32_t)(al >> 32) + (uint32_t)ah;
+    const uint32_t sh = (uint32_t)(ah >> 32) + (uint32_t)(w >> 32);
+    const uint64_t slo = ((uint64_t)(uint32_t)w << 32) | (uint32_t)al;
+    const uint64_t res = slo + (uint64_t)sh * 0xFFFFFFFFull;
+    const uint64_t y = res + (res < slo ? GL_EPS : 0ull);
+    const uint64_t x1 = y + nq;
+    return x1 + (x1 > y ? GL_P : 0ull);
+}
+
+// The original carry-chain form of the same word (fewer instructions; the issue-bound callers).
+__device__ __forceinline__ uint64_t mds_reduce_ark_carry(uint64_t al, uint64_t ah, uint64_t rc) {
+    unsigned int k1, b1, over, c2, bb, ov2;
+    const uint32_t m1 = __builtin_addc((uint32_t)(al >> 32), (uint32_t)ah, 0u, &k1);
+    const uint32_t sh = (uint32_t)(ah >> 32) + k1;
+    const uint32_t tl = __builtin_subc(0u, sh, 0u, &b1);
+    unsigned int dummy;
+    const uint32_t th = __builtin_subc(sh, 0u, b1, &dummy);
+    uint32_t rl = __builtin_addc((uint32_t)al, tl, 0u, &k1);
+    uint32_t rh = __builtin_addc(m1, th, k1, &over);
+    rl = __builtin_addc(rl, 0u - over, 0u, &c2);
+    rh = rh + c2;
+    const uint64_t q = GL_P - rc;
+    rl = __builtin_subc(rl, (uint32_t)q, 0u, &bb);
+    rh = __builtin_subc(rh, (uint32_t)(q >> 32), bb, &ov2);
+    rl = __builtin_subc(rl, 0u - ov2, 0u, &bb);
+    return ((uint64_t)(rh - bb) << 32) | rl;
+}
+
+// LAT = true: the carry-light arithmetic (mont_mul_lat, mds_reduce_ark_lat) for callers bound by one
+// permutation's latency (small batches); false: the fewer-instruction carry-chain form for callers
+// that share the SIMDs with other work (the sponge replay of large batches, the wide Merkle levels).
+// Measured (A/B, tools/ab_latform.sh): carry-light rows cut the one-collection resident verify
+// 1.63 -> 1.44 ms but cost 0.7-2% at 512 / 4,096 proofs, whose row-form work is issue-bound.
+template <bool LAT>
+__device__ __forceinline__ uint64_t mont_mul_sel(uint64_t a, uint64_t b) {
+    if constexpr (LAT) return mont_mul_lat(a, b);
+    else return mont_mul(a, b);
+}
+
 // ---------------------------------------------------------------------------------------------
 // "Wide" Tip5: one state spread over a 16-lane DPP row (lane e of the row holds state[e]).
 // Used where latency, not throughput, matters (the sequential Fiat-Shamir sponge of one proof):
@@ -191,6 +237,7 @@ __device__ __forceinline__ void mds_term(uint32_t lo, uint32_t hi, uint64_t& al,
 
 // s: this lane's state word (raw Montgomery); e: lane index within the row; rc: this lane's 5
 // round constants (raw).
+template <bool LAT>
 __device__ __forceinline__ uint64_t tip5_permute_wide(uint64_t s, uint32_t e, const uint64_t rc[5],
                                                       const uint8_t* __restrict__ lut) {
 #pragma unroll
@@ -200,10 +247,10 @@ __device__ __forceinline__ uint64_t tip5_permute_wide(uint64_t s, uint32_t e, co
         // hides behind the x^7 chain; the lane picks its result at the end.
         {
             const uint64_t lk = split_and_lookup(lut, s);
-            const uint64_t x2 = mont_mul(s, s);
-            const uint64_t x4 = mont_mul(x2, x2);
-            const uint64_t x3 = mont_mul(s, x2);
-            const uint64_t x7 = mont_mul(x3, x4);
+            const uint64_t x2 = mont_mul_sel<LAT>(s, s);
+            const uint64_t x4 = mont_mul_sel<LAT>(x2, x2);
+            const uint64_t x3 = mont_mul_sel<LAT>(s, x2);
+            const uint64_t x7 = mont_mul_sel<LAT>(x3, x4);
             s = e < 4 ? lk : x7;
         }
         // MDS over the row
@@ -224,28 +271,15 @@ __device__ __forceinline__ uint64_t tip5_permute_wide(uint64_t s, uint32_t e, co
         mds_term<13>(lo, hi, al, ah);
         mds_term<14>(lo, hi, al, ah);
         mds_term<15>(lo, hi, al, ah);
-        // recombination + ARK, exactly as mds_ark()
-        unsigned int k1, b1, over, c2, bb, ov2;
-        const uint32_t m1 = __builtin_addc((uint32_t)(al >> 32), (uint32_t)ah, 0u, &k1);
-        const uint32_t sh = (uint32_t)(ah >> 32) + k1;
-        const uint32_t tl = __builtin_subc(0u, sh, 0u, &b1);
-        unsigned int dummy;
-        const uint32_t th = __builtin_subc(sh, 0u, b1, &dummy);
-        uint32_t rl = __builtin_addc((uint32_t)al, tl, 0u, &k1);
-        uint32_t rh = __builtin_addc(m1, th, k1, &over);
-        rl = __builtin_addc(rl, 0u - over, 0u, &c2);
-        rh = rh + c2;
-        const uint64_t q = GL_P - rc[r];
-        rl = __builtin_subc(rl, (uint32_t)q, 0u, &bb);
-        rh = __builtin_subc(rh, (uint32_t)(q >> 32), bb, &ov2);
-        rl = __builtin_subc(rl, 0u - ov2, 0u, &bb);
-        s = ((uint64_t)(rh - bb) << 32) | rl;
+        // recombination + ARK, the same words as mds_ark()
+        if constexpr (LAT) s = mds_reduce_ark_lat(al, ah, 0ull - (GL_P - rc[r]));
+        else s = mds_reduce_ark_carry(al, ah, rc[r]);
     }
     return s;
 }
 
 // ---------------------------------------------------------------------------------------------
-// "Pair" Tip5: one state on two 16-lane DPP rows (rows 2r and 2r+1 of a wave; lane e of both rows
+// "Pair" Tip5 (small batches only: always the carry-light arithmetic): one state on two 16-lane DPP rows (rows 2r and 2r+1 of a wave; lane e of both rows
 // holds state[e], so both rows keep the whole state).  The rows split each round's work, which
 // cuts the dependent instructions per round by about a quarter (for the sequential Fiat-Shamir
 // sponge of small batches, where most SIMDs are idle anyway):
@@ -278,11 +312,11 @@ __device__ __forceinline__ uint64_t tip5_permute_pair(uint64_t s, uint32_t e, ui
     for (int r = 0; r < TIP5_ROUNDS; ++r) {
         // S-box
         const uint32_t lk_mine = lookup4(lut, h ? (uint32_t)(s >> 32) : (uint32_t)s);
-        const uint64_t x2 = mont_mul(s, s);
-        const uint64_t m = mont_mul(h ? s : x2, x2);  // row 0: x^4, row 1: x^3
+        const uint64_t x2 = mont_mul_lat(s, s);
+        const uint64_t m = mont_mul_lat(h ? s : x2, x2);  // row 0: x^4, row 1: x^3
         uint64_t mr0, mr1;
         row_pair(m, mr0, mr1);
-        const uint64_t x7 = mont_mul(mr0, mr1);
+        const uint64_t x7 = mont_mul_lat(mr0, mr1);
         const auto lk = __builtin_amdgcn_permlane16_swap(lk_mine, lk_mine, false, false);
         s = e < 4 ? (((uint64_t)lk[1] << 32) | lk[0]) : x7;
         // MDS: half of the rotations per row
@@ -302,22 +336,8 @@ __device__ __forceinline__ uint64_t tip5_permute_pair(uint64_t s, uint32_t e, ui
         row_pair(ah, b0, b1);
         al = a0 + a1;
         ah = b0 + b1;
-        // recombination + ARK, exactly as mds_ark()
-        unsigned int k1, b1c, over, c2, bb, ov2;
-        const uint32_t m1 = __builtin_addc((uint32_t)(al >> 32), (uint32_t)ah, 0u, &k1);
-        const uint32_t sh = (uint32_t)(ah >> 32) + k1;
-        const uint32_t tl = __builtin_subc(0u, sh, 0u, &b1c);
-        unsigned int dummy;
-        const uint32_t th = __builtin_subc(sh, 0u, b1c, &dummy);
-        uint32_t rl = __builtin_addc((uint32_t)al, tl, 0u, &k1);
-        uint32_t rh = __builtin_addc(m1, th, k1, &over);
-        rl = __builtin_addc(rl, 0u - over, 0u, &c2);
-        rh = rh + c2;
-        const uint64_t q = GL_P - rc[r];
-        rl = __builtin_subc(rl, (uint32_t)q, 0u, &bb);
-        rh = __builtin_subc(rh, (uint32_t)(q >> 32), bb, &ov2);
-        rl = __builtin_subc(rl, 0u - ov2, 0u, &bb);
-        s = ((uint64_t)(rh - bb) << 32) | rl;
+        // recombination + ARK, the same words as mds_ark()
+        s = mds_reduce_ark_lat(al, ah, 0ull - (GL_P - rc[r]));
     }
     return s;
 }
