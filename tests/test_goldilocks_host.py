@@ -21,3 +21,17 @@ def test_to_mont_closed_form_matches_montgomery_product(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "bad 0" in out.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_mds_folded_round_constant_matches_stepwise(tmp_path):
+    """mds_ark's folded reduction (round constant in the accumulators, one multiply-add with carry-out)
+    equals twenty-first's reduce-then-add for every Tip5 round constant."""
+    exe = tmp_path / "mds_fold_check"
+    subprocess.check_call([HIPCC, "-O2", "-std=c++17", "-x", "hip", "--offload-arch=gfx950",
+                           "-I", os.path.join(ROOT, "neptune-core_amd", "csrc"),
+                           os.path.join(ROOT, "tests", "native", "mds_fold_check.cpp"), "-o", str(exe)],
+                          stderr=subprocess.DEVNULL)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "bad 0" in out.stdout
