@@ -274,6 +274,23 @@ __device__ __forceinline__ uint64_t mds_reduce_ark_carry(uint64_t al, uint64_t a
     return ((uint64_t)(rh - bb) << 32) | rl;
 }
 
+// mds_ark's folded reduction for one word (the row forms): al / ah started at the halves of
+// K = rc + 2^32 - 1.  One chain per lane, so the mask read waits out the two wait states itself.
+__device__ __forceinline__ uint64_t mds_reduce_fold(uint64_t al, uint64_t ah) {
+    unsigned int k;
+    const uint32_t m1 = __builtin_addc((uint32_t)(al >> 32), (uint32_t)ah, 0u, &k);
+    const uint32_t sh = (uint32_t)(ah >> 32) + k;
+    const uint64_t slo = ((uint64_t)m1 << 32) | (uint32_t)al;
+    uint64_t w, g;
+    uint32_t e;
+    asm("v_mad_u64_u32 %0, %2, %3, -1, %4\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %1, -1, 0, %2"
+        : "=&v"(w), "=v"(e), "=&s"(g)
+        : "v"(sh), "v"(slo));
+    return w - e;
+}
+
 // LAT = true: the carry-light arithmetic (mont_mul_lat, mds_reduce_ark_lat) for callers bound by one
 // permutation's latency (small batches); false: the fewer-instruction carry-chain form for callers
 // that share the SIMDs with other work (the sponge replay of large batches, the wide Merkle levels).
@@ -324,7 +341,15 @@ __device__ __forceinline__ uint64_t tip5_permute_wide(uint64_t s, uint32_t e, co
         }
         // MDS over the row
         const uint32_t lo = (uint32_t)s, hi = (uint32_t)(s >> 32);
-        uint64_t al = (uint64_t)TIP5_MDS[0] * lo, ah = (uint64_t)TIP5_MDS[0] * hi;
+        uint64_t al, ah;
+        if constexpr (LAT) {
+            al = (uint64_t)TIP5_MDS[0] * lo;
+            ah = (uint64_t)TIP5_MDS[0] * hi;
+        } else {  // the round constant folded into the sums (mds_reduce_fold)
+            const uint64_t K = rc[r] + GL_EPS;
+            al = (uint64_t)TIP5_MDS[0] * lo + (uint32_t)K;
+            ah = (uint64_t)TIP5_MDS[0] * hi + (K >> 32);
+        }
         mds_term<1>(lo, hi, al, ah);
         mds_term<2>(lo, hi, al, ah);
         mds_term<3>(lo, hi, al, ah);
@@ -342,7 +367,7 @@ __device__ __forceinline__ uint64_t tip5_permute_wide(uint64_t s, uint32_t e, co
         mds_term<15>(lo, hi, al, ah);
         // recombination + ARK, the same words as mds_ark()
         if constexpr (LAT) s = mds_reduce_ark_lat(al, ah, 0ull - (GL_P - rc[r]));
-        else s = mds_reduce_ark_carry(al, ah, rc[r]);
+        else s = mds_reduce_fold(al, ah);
     }
     return s;
 }
