@@ -76,9 +76,80 @@ __device__ __forceinline__ uint64_t pow7(uint64_t x) {
 #ifndef NHIP_POW7_GROUP
 #define NHIP_POW7_GROUP 6
 #endif
+// u = a1 * b0 + t as a 65-bit sum for three products: u (64 bits) and its carry c (0 / 1), with
+// v_mad_u64_u32's carry-out read by v_cndmask two instructions later (gfx950's two wait states).
+__device__ __forceinline__ void mad_carry3(const uint32_t* a1, const uint32_t* b0, const uint64_t* t, uint64_t* u,
+                                           uint32_t* c) {
+    uint64_t g0, g1, g2;
+    asm("v_mad_u64_u32 %0, %6, %9, %12, %15\n\t"
+        "v_mad_u64_u32 %1, %7, %10, %13, %16\n\t"
+        "v_mad_u64_u32 %2, %8, %11, %14, %17\n\t"
+        "v_cndmask_b32_e64 %3, 0, 1, %6\n\t"
+        "v_cndmask_b32_e64 %4, 0, 1, %7\n\t"
+        "v_cndmask_b32_e64 %5, 0, 1, %8"
+        : "=&v"(u[0]), "=&v"(u[1]), "=&v"(u[2]), "=v"(c[0]), "=v"(c[1]), "=v"(c[2]), "=&s"(g0), "=&s"(g1),
+          "=&s"(g2)
+        : "v"(a1[0]), "v"(a1[1]), "v"(a1[2]), "v"(b0[0]), "v"(b0[1]), "v"(b0[2]), "v"(t[0]), "v"(t[1]), "v"(t[2]));
+}
+
+// N independent Montgomery products (N a multiple of 3), the same words as mont_mul.  The 128-bit
+// product's middle column is summed as u = a1*b0 + t with t = a0*b1 + (p00 >> 32) taken whole
+// (u's low half is the product's bits 32..63 as before; its top 33 bits are t's and the old u's
+// high halves together), so xh = a1*b1 + (u >> 32, carry): two multiply-adds whose 64-bit addends
+// no longer need a 32-bit half zero-extended into a fresh register pair (gfx950 64-bit operands are
+// even-aligned pairs: one v_mov each), and no separate xh add.
+template <int N>
+__device__ __forceinline__ void mont_mul_n_dev(const uint64_t* a, const uint64_t* b, uint64_t* out) {
+    static_assert(N % 3 == 0, "groups of three");
+    uint64_t p00[N], t[N], u[N], xh[N];
+    uint32_t a1[N], b0[N], c[N];
+    uint32_t ah[N], e[N], bl[N], bh[N], rl[N], rh[N], c1[N], cc[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        a1[i] = (uint32_t)(a[i] >> 32);
+        b0[i] = (uint32_t)b[i];
+        p00[i] = (uint64_t)(uint32_t)a[i] * b0[i];
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) t[i] = (uint64_t)(uint32_t)a[i] * (uint32_t)(b[i] >> 32) + (p00[i] >> 32);
+#pragma unroll
+    for (int i = 0; i < N; i += 3) mad_carry3(a1 + i, b0 + i, t + i, u + i, c + i);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        xh[i] = (uint64_t)a1[i] * (uint32_t)(b[i] >> 32) + (((uint64_t)c[i] << 32) | (uint32_t)(u[i] >> 32));
+    // montyred, as mont_mul_n
+#pragma unroll
+    for (int i = 0; i < N; ++i) ah[i] = __builtin_addc((uint32_t)u[i], (uint32_t)p00[i], 0u, &e[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        unsigned int br1;
+        bl[i] = __builtin_subc((uint32_t)p00[i], ah[i], e[i], &br1);
+        e[i] = br1;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        unsigned int br2;
+        bh[i] = __builtin_subc(ah[i], 0u, e[i], &br2);
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) rl[i] = __builtin_subc((uint32_t)xh[i], bl[i], 0u, &c1[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) rh[i] = __builtin_subc((uint32_t)(xh[i] >> 32), bh[i], c1[i], &cc[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        unsigned int c2;
+        const uint32_t lo = __builtin_subc(rl[i], 0u - cc[i], 0u, &c2);
+        out[i] = ((uint64_t)(rh[i] - c2) << 32) | lo;
+    }
+}
+
 template <int G>
 __device__ __forceinline__ void pow7_mul(const uint64_t* a, const uint64_t* b, uint64_t* out) {
+#ifdef NHIP_POW7_PLAIN
     mont_mul_n<G>(a, b, out);
+#else
+    mont_mul_n_dev<G>(a, b, out);
+#endif
 }
 
 __device__ __forceinline__ void pow7_12(uint64_t* x) {
