@@ -39,6 +39,23 @@ __constant__ static uint64_t c_tip5_rc_raw[80] = {
 #undef NHIP_RC
 };
 
+// K = RC + 2^32 - 1 per round constant: the value mds_ark's folded reduction starts the low MDS
+// accumulator with (kept as a table so the addition is not redone on the vector unit every round)
+__constant__ static uint64_t c_tip5_rck_raw[80] = {
+#define NHIP_RC(i) (TIP5_RC_RAW[i] + 0xFFFFFFFFull)
+    NHIP_RC(0), NHIP_RC(1), NHIP_RC(2), NHIP_RC(3), NHIP_RC(4), NHIP_RC(5), NHIP_RC(6), NHIP_RC(7),
+    NHIP_RC(8), NHIP_RC(9), NHIP_RC(10), NHIP_RC(11), NHIP_RC(12), NHIP_RC(13), NHIP_RC(14), NHIP_RC(15),
+    NHIP_RC(16), NHIP_RC(17), NHIP_RC(18), NHIP_RC(19), NHIP_RC(20), NHIP_RC(21), NHIP_RC(22), NHIP_RC(23),
+    NHIP_RC(24), NHIP_RC(25), NHIP_RC(26), NHIP_RC(27), NHIP_RC(28), NHIP_RC(29), NHIP_RC(30), NHIP_RC(31),
+    NHIP_RC(32), NHIP_RC(33), NHIP_RC(34), NHIP_RC(35), NHIP_RC(36), NHIP_RC(37), NHIP_RC(38), NHIP_RC(39),
+    NHIP_RC(40), NHIP_RC(41), NHIP_RC(42), NHIP_RC(43), NHIP_RC(44), NHIP_RC(45), NHIP_RC(46), NHIP_RC(47),
+    NHIP_RC(48), NHIP_RC(49), NHIP_RC(50), NHIP_RC(51), NHIP_RC(52), NHIP_RC(53), NHIP_RC(54), NHIP_RC(55),
+    NHIP_RC(56), NHIP_RC(57), NHIP_RC(58), NHIP_RC(59), NHIP_RC(60), NHIP_RC(61), NHIP_RC(62), NHIP_RC(63),
+    NHIP_RC(64), NHIP_RC(65), NHIP_RC(66), NHIP_RC(67), NHIP_RC(68), NHIP_RC(69), NHIP_RC(70), NHIP_RC(71),
+    NHIP_RC(72), NHIP_RC(73), NHIP_RC(74), NHIP_RC(75), NHIP_RC(76), NHIP_RC(77), NHIP_RC(78), NHIP_RC(79),
+#undef NHIP_RC
+};
+
 // LDS copy of the byte lookup table, one per workgroup.  256 B = 64 dwords: a random byte
 // gather from a wave touches at most 2 distinct dwords per bank for ds_read_u8 (bank = dword % 32).
 struct Tip5Lds {
@@ -250,15 +267,20 @@ __device__ __forceinline__ void mds_fold4(const uint32_t* sh, const uint64_t* sl
 // (y = reduce(s), then the field add y + rc), the result is the canonical representative of
 // s + rc mod p whenever rc < p - 2^32 + 2, which every Tip5 round constant satisfies: if y >= q
 // the add gives y - q = y + rc - p < p, else y + rc < p.  So: accumulate s'' = s + K with
-// K = rc + 2^32 - 1 (K's halves start the two accumulators), W = s''_lo + s''_hi * (2^32 - 1)
+// K = rc + 2^32 - 1 (K starts the low accumulator: every Tip5 constant has K < 2^64 - 2^52, so
+// it never overflows), W = s''_lo + s''_hi * (2^32 - 1)
 // (= s'' mod p, 65 bits); if W >= 2^64 the result is W - 2^64 (= W - (2^32 - 1) - p, < 2^54),
 // else W - (2^32 - 1) (in [0, p): s'' >= 2^32 - 1 keeps W >= 2^32 - 1).  6 VALU instructions per
 // word after the accumulation instead of 15 (checked against the step-by-step form for every Tip5
 // round constant and 3 x 10^6 other in-range constants: tests/native/mds_fold_check.cpp).
-__device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restrict__ rc) {
+// rc: the round's 16 constants; rck: the same round's K = rc + 2^32 - 1 (c_tip5_rck_raw).
+__device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restrict__ rc,
+                                        const uint64_t* __restrict__ rck) {
 #ifdef NHIP_MDS_CARRY
+    (void)rck;
     mds_ark_carry(s, rc);
 #else
+    (void)rc;
     uint32_t lo[16], hi[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -268,9 +290,8 @@ __device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restri
     uint64_t al[16], ah[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        const uint64_t K = rc[i] + GL_EPS;
-        al[i] = (uint32_t)K;
-        ah[i] = K >> 32;
+        al[i] = rck[i];  // < 2^64 - 2^52 for every Tip5 constant: al never overflows
+        ah[i] = 0;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const uint64_t c = TIP5_MDS[(i - j) & 15];
@@ -302,7 +323,7 @@ __device__ __forceinline__ void tip5_permute_raw(uint64_t s[16], const uint8_t* 
 #pragma unroll
         for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
         pow7_12(s + 4);
-        mds_ark(s, c_tip5_rc_raw + r * 16);
+        mds_ark(s, c_tip5_rc_raw + r * 16, c_tip5_rck_raw + r * 16);
     }
 }
 
@@ -345,8 +366,7 @@ __device__ __forceinline__ uint64_t mds_reduce_ark_carry(uint64_t al, uint64_t a
     return ((uint64_t)(rh - bb) << 32) | rl;
 }
 
-// mds_ark's folded reduction for one word (the row forms): al / ah started at the halves of
-// K = rc + 2^32 - 1.  One chain per lane, so the mask read waits out the two wait states itself.
+// mds_ark's folded reduction for one word (the row forms): al started at K = rc + 2^32 - 1.  One chain per lane, so the mask read waits out the two wait states itself.
 __device__ __forceinline__ uint64_t mds_reduce_fold(uint64_t al, uint64_t ah) {
     unsigned int k;
     const uint32_t m1 = __builtin_addc((uint32_t)(al >> 32), (uint32_t)ah, 0u, &k);
@@ -417,9 +437,8 @@ __device__ __forceinline__ uint64_t tip5_permute_wide(uint64_t s, uint32_t e, co
             al = (uint64_t)TIP5_MDS[0] * lo;
             ah = (uint64_t)TIP5_MDS[0] * hi;
         } else {  // the round constant folded into the sums (mds_reduce_fold)
-            const uint64_t K = rc[r] + GL_EPS;
-            al = (uint64_t)TIP5_MDS[0] * lo + (uint32_t)K;
-            ah = (uint64_t)TIP5_MDS[0] * hi + (K >> 32);
+            al = (uint64_t)TIP5_MDS[0] * lo + (rc[r] + GL_EPS);
+            ah = (uint64_t)TIP5_MDS[0] * hi;
         }
         mds_term<1>(lo, hi, al, ah);
         mds_term<2>(lo, hi, al, ah);
