@@ -89,9 +89,11 @@ __device__ __forceinline__ uint64_t pow7(uint64_t x) {
 }
 
 // x -> x^7 on 12 words, NHIP_POW7_GROUP words at a time (stage-interleaved Montgomery
-// products: wider groups fill more carry-chain wait states but hold more VGPRs).
+// products: wider groups fill more carry-chain wait states but hold more VGPRs).  3: the Merkle
+// level kernel fits 95 VGPRs (5 waves per SIMD instead of 4 at 6), config 4 +1%
+// (profiles/r02h/ab_g3/).
 #ifndef NHIP_POW7_GROUP
-#define NHIP_POW7_GROUP 6
+#define NHIP_POW7_GROUP 3
 #endif
 // u = a1 * b0 + t as a 65-bit sum for three products: u (64 bits) and its carry c (0 / 1), with
 // v_mad_u64_u32's carry-out read by v_cndmask two instructions later (gfx950's two wait states).
