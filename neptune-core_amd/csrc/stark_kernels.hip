@@ -203,7 +203,10 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
 
 // ------------------------------------------------------------------ revealed-row hashing
 // grid.y = 0 main, 1 aux, 2 quotient; one lane per (proof, row).
-__global__ void __launch_bounds__(256) k_hash_rows(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+#ifndef NHIP_ROWS_WAVES
+#define NHIP_ROWS_WAVES
+#endif
+__global__ void __launch_bounds__(256) NHIP_ROWS_WAVES k_hash_rows(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                                    uint32_t n_proofs, uint32_t k, StarkDims dims,
                                                    uint64_t* __restrict__ dig, const uint32_t* __restrict__ fail) {
     __shared__ Tip5Lds lds;
