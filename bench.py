@@ -67,17 +67,33 @@ def log(*a):
 FETCH_CORRECTION = {"FETCH_SIZE": 2.0, "WRITE_SIZE": 1.0}
 
 
+LIB_PATH = os.path.join(ROOT, "neptune-core_amd", "neptune_hip", "libneptune_hip.so")
+
+
+def lib_sha256(path: str = LIB_PATH) -> str:
+    import hashlib
+    return hashlib.sha256(open(path, "rb").read()).hexdigest()
+
+
 def latest_profile(config: int, proofs: int):
     """profiles/LATEST = '<tag> <config> <proofs per GPU>': the committed rocprofv3 PMC passes and
     the workload they were taken on (none for another config or per-GPU batch size: the PMC
-    figures are per step of that workload)."""
+    figures are per step of that workload).  The passes count only for the library they were taken
+    with: profiles/<tag>/LIB_SHA256 must equal the hash of the library this run loads, else the
+    counters belong to another binary and are not attached."""
     try:
         parts = open(os.path.join(ROOT, "profiles", "LATEST")).read().split()
     except OSError:
         return None
     tag, cfg = parts[0], int(parts[1]) if len(parts) > 1 else 3
     n = int(parts[2]) if len(parts) > 2 else None
-    return tag if cfg == config and n in (None, proofs) else None
+    if cfg != config or n not in (None, proofs):
+        return None
+    try:
+        want = open(os.path.join(ROOT, "profiles", tag, "LIB_SHA256")).read().split()[0]
+    except (OSError, IndexError):
+        return None
+    return tag if want == lib_sha256() else None
 
 
 def pmc_traffic(kernel: str, config: int, proofs: int):
@@ -145,11 +161,23 @@ def pmc_bytes_per_step(config: int, proofs: int):
         return None, None
 
 
+def _assert_fracs(obj, path="res"):
+    """Every fraction of a ceiling in the result line is <= 1: a larger one means mismatched inputs
+    (counters of another binary, a wrong launch count), never a faster kernel."""
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            if (k == "frac" or k.endswith("_frac")) and isinstance(v, (int, float)):
+                assert 0.0 <= v <= 1.0, f"{path}.{k} = {v} is not a fraction of its ceiling"
+            _assert_fracs(v, f"{path}.{k}")
+
+
 HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md; 6.29 TB/s measured copy)
 
 # measured gfx950 issue ceiling for this instruction mix: ~1 wave64 VALU instruction per 4 clocks
 # per SIMD (DESIGN.md §3, tools/valu_microbench.hip)
 VALU_ISSUE_CEILING = 256 * 4 * 2.4e9 / 4
+# the fastest class measured (v_mov / v_add / logic: 1.4-1.7 wave64 instructions per CU-clock)
+VALU_ISSUE_MAX = 256 * 1.7 * 2.4e9
 
 
 # ------------------------------------------------------------------ config 3 batch
@@ -189,32 +217,62 @@ def make_batch(pool, collections: int, corrupt_frac: float, seed: int):
     return claims, proofs, np.array(expect, dtype=bool)
 
 
-def make_config4(pool, total: int, corrupt_frac: float, world: int, rank: int):
+def load_pool4():
+    """The 256 distinct accepting proofs config 4 draws from (oracle/pool4.py: the 5 committed full
+    proofs of c3_pool.npz + 251 sparse-prover proofs, distinct claims and seeds, every one verified
+    by both oracles, with its oracle transcript), built once per machine outside the timed region."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pool4  # test-data generator (proof construction only)
+    return pool4.load()
+
+
+def pool4_from_c3(pool):
+    """A pool in load_pool4()'s form holding only the 5 committed c3 proofs (CPU tests: the real
+    pool takes a minute of proving)."""
+    hs = sorted(pool)
+    return {"heights": hs, "proofs": [pool[h]["proof"] for h in hs], "claims": [pool[h]["claim"] for h in hs],
+            "main_rows": [pool[h]["main_rows"] for h in hs]}
+
+
+def make_config4(pool4, total: int, corrupt_frac: float, world: int, rank: int):
     """BASELINE config 4: `total` transaction proofs with log2 padded heights drawn uniformly from
-    the ProofCollection member mix (seed 0xC4), corrupt_frac of them with one flipped MainRows word,
-    LPT-sharded over the ranks by estimated Tip5 cost (neptune_hip.shard.lpt_shard).  Returns this
-    rank's (claims, proofs, expect), the shard assignment every rank agrees on, and the expected
-    verdict of every proof of the job."""
+    the ProofCollection member mix (seed 0xC4); the k-th proof of height h is distinct pool proof
+    k mod (pool proofs of height h), so the 256 distinct proofs (oracle/pool4.py) each appear
+    total / 256 times.  corrupt_frac of them get one flipped MainRows word.  LPT-sharded over the
+    ranks by estimated Tip5 cost (neptune_hip.shard.lpt_shard).  Returns this rank's (claims,
+    proofs, expect, pool index per proof), the shard assignment every rank agrees on, and the
+    expected verdict of every proof of the job."""
     from neptune_hip import shard
     rng = np.random.default_rng(0xC4)
     hs = rng.choice(COLLECTION_HEIGHTS, size=total)
     bad = set(rng.choice(total, size=int(round(total * corrupt_frac)), replace=False).tolist())
     cost = [10_000 + 600 * int(h) for h in hs]  # ~ Tip5 permutations per proof of that height
+    by_h = {}
+    for j, h in enumerate(pool4["heights"]):
+        by_h.setdefault(int(h), []).append(j)
+    seen = {}
+    src = []
+    for i in range(total):
+        h = int(hs[i])
+        k = seen.get(h, 0)
+        seen[h] = k + 1
+        src.append(by_h[h][k % len(by_h[h])])
     mine = shard.lpt_shard(cost, world)[rank]
-    claims, proofs, expect = [], [], []
+    claims, proofs, expect, srcs = [], [], [], []
     for i in mine:
-        e = pool[int(hs[i])]
-        proof = e["proof"]
+        j = src[i]
+        proof = pool4["proofs"][j]
         if i in bad:
             proof = proof.copy()
-            lo, hi = e["main_rows"]
+            lo, hi = pool4["main_rows"][j]
             pos = lo + (i * 7919) % (hi - lo)
             proof[pos] = np.uint64((int(proof[pos]) + 1) % P)
-        claims.append(e["claim"])
+        claims.append(pool4["claims"][j])
         proofs.append(proof)
         expect.append(i not in bad)
+        srcs.append(j)
     expect_all = np.array([i not in bad for i in range(total)], dtype=bool)
-    return claims, proofs, np.array(expect, dtype=bool), shard.lpt_shard(cost, world), expect_all
+    return claims, proofs, np.array(expect, dtype=bool), srcs, shard.lpt_shard(cost, world), expect_all
 
 
 def make_config5(air_words, total: int, log2_ph: int, world: int, rank: int):
@@ -268,6 +326,75 @@ def cpu_baseline(air_words, claims, proofs, expect, target_s: float, threads: in
             "sample": f"{passes} pass(es) over the first {m} of this batch's {len(proofs)} proofs ({m // 8} whole "
                       f"collections), C restatement of the verifier (oracle/stark_oracle.c, Tip5 "
                       f"oracle/tip5_oracle.c), {threads} threads, {dt:.1f} s"}
+
+
+# ------------------------------------------------------------------ config 1: single-proof latency
+def config1_case(air_words):
+    """BASELINE config 1 substitute (the reference's SingleProof is unavailable
+    offline): one SingleProof-shaped proof at log2 padded height 21, seed 0xC1 (the claim of
+    single_proof.rs:295-304: input = a 5-word kernel MAST hash reversed, output empty; synthetic
+    program digest).  Constant-codeword prover (oracle/stark_prover_const.py): the verifier's work
+    does not depend on the values, and the proof takes a second to make."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import stark_prover_const as K  # test-data generator (proof construction only)
+    import stark_ref as S
+    import tip5_ref as T
+    T.use_c_backend()
+    params = S.StarkParams()
+    _, recipe = S.synth_air(params, seed=1)
+    air = S.AirCircuit.from_words([int(w) for w in air_words])
+    rng = np.random.default_rng(0xC1)
+    kernel_mast_hash = [int(x) for x in rng.integers(0, P, size=5, dtype=np.uint64)]
+    program_digest = [int(x) for x in rng.integers(0, P, size=5, dtype=np.uint64)]
+    claim = (program_digest, 0, kernel_mast_hash[::-1], [])
+    proof, _ = K.prove(params, air, recipe, claim, 21, seed=0xC1)
+    return claim, np.asarray(proof, dtype=np.uint64)
+
+
+def config1_latency(ctx, gair, stark, air_words, cpu_seconds: float, reps: int = 50):
+    """Single-proof latency on the config-1 substitute: the GPU (one proof resident in HBM, launch to
+    verdict; and from host memory through nhip_verify_batch) beside the C restatement on ONE host
+    thread (config 1's CPU baseline is the restatement, 1 thread).  Medians."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle as C  # oracle: CPU baseline leg only
+    import neptune_hip.stark as NS
+    import stark_ref as S
+    claim, proof = config1_case(air_words)
+    ncl = NS.Claim(*claim)
+    b = NS.Batch(ctx, gair, stark, [ncl], [proof])
+    for _ in range(5):
+        v, _ = b.run()
+    res_ms = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        v, _ = b.run()
+        res_ms.append((time.perf_counter() - t) * 1e3)
+    ok = bool(v[0])
+    b.close()
+    host_ms = []
+    for _ in range(max(5, reps // 5)):
+        t = time.perf_counter()
+        ok = NS.verify_batch(ctx, gair, stark, [(ncl, proof)]) == [True] and ok
+        host_ms.append((time.perf_counter() - t) * 1e3)
+    args = C.stark_batch_args(air_words, S.StarkParams(), [claim], [proof])
+    ok = bool(C.stark_verify_args(args, 1)[0]) and ok  # warm, and the oracle's verdict
+    cpu_ms = []
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < cpu_seconds or len(cpu_ms) < 3:
+        t = time.perf_counter()
+        C.stark_verify_args(args, 1)
+        cpu_ms.append((time.perf_counter() - t) * 1e3)
+    gpu = float(np.median(res_ms))
+    cpu = float(np.median(cpu_ms))
+    return {"workload": "BASELINE config 1 substitute: one SingleProof-shaped proof, log2 padded height 21 "
+                        "(FRI domain 2^24, 15 FRI rounds), seed 0xC1, Stark::default()",
+            "proof_words": int(proof.size), "verdict_accept": ok,
+            "gpu_resident_ms": gpu, "gpu_from_host_ms": float(np.median(host_ms)),
+            "cpu_ms": cpu, "cpu_threads": 1, "cpu_kind": "port", "cpu_runs": len(cpu_ms),
+            "gpu_speedup": cpu / gpu,
+            "measured": f"medians: {reps} resident runs (launch to verdicts back), {len(host_ms)} nhip_verify_batch "
+                        f"calls from host memory, {len(cpu_ms)} single-thread runs of the C restatement "
+                        f"(oracle/stark_oracle.c)"}
 
 
 # ------------------------------------------------------------------ config 2 Tip5 path microbench
@@ -370,8 +497,10 @@ def pcie_stream(ctx, gair, stark, claims, proofs, expect, batches: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # default timed region: 200 config-4 steps, ~2 s of full VALU load (the clock settles under
+    # sustained load on this power-bound integer pipeline)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=4, choices=(3, 4, 5),
                     help="4 (default, the north-star workload): 4,096 mixed transaction proofs over all ranks, "
                          "LPT-sharded, strong scaling; 3: 256 ProofCollections (2,048 proofs) per GPU, weak "
@@ -390,6 +519,8 @@ def main():
                     help="steps run one at a time after the timed region for roofline_isolated (0 = none: a "
                          "profiled run's kernel statistics then hold only in-flight steps)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--config1-seconds", type=float, default=8.0,
+                    help="config-1 single-proof latency leg: CPU-restatement time budget (0 = skip the leg)")
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
     ap.add_argument("--stream-batches", type=int, default=6,
                     help="PCIe-inclusive leg: batches streamed from pinned host memory (0 = skip)")
@@ -428,7 +559,12 @@ def main():
         total = world * len(proofs)
     elif args.config == 4:
         total = args.proofs or 4096
-        claims, proofs, expect, shards, expect_all = make_config4(pool, total, 0.01, world, rank)
+        t = time.time()
+        pool4 = load_pool4()
+        log(f"[rank {rank}] config-4 pool: {len(pool4['proofs'])} distinct proofs ({time.time() - t:.1f}s)")
+        if args.air == "synthetic":
+            air_words = pool4["air"]
+        claims, proofs, expect, _, shards, expect_all = make_config4(pool4, total, 0.01, world, rank)
     else:
         total = args.proofs or 64
         claims, proofs, expect, shards, expect_all = make_config5(air_words, total, args.log2_height, world, rank)
@@ -625,12 +761,20 @@ def main():
         "dtype": "u64 (Goldilocks mod p; XFE = cubic extension)",
         "data": ("synthetic: one accepting proof per padded height (tests/golden/c3_pool.npz, synthetic AIR with "
                  "triton-vm column counts), 5% of collections with one flipped MainRows word" if args.config == 3 else
-                 "synthetic: proofs of the config-3 pool (tests/golden/c3_pool.npz), 1% with one flipped MainRows word"
+                 "synthetic: 256 distinct accepting proofs (oracle/pool4.py: the 5 full proofs of "
+                 "tests/golden/c3_pool.npz + 251 sparse-prover proofs, distinct claims and seeds), each used "
+                 f"{total // 256 if total >= 256 else 1}x, 1% with one flipped MainRows word"
                  if args.config == 4 else
                  "synthetic: constant-codeword proofs (oracle/stark_prover_const.py), synthetic AIR with triton-vm "
                  "column counts"),
         "config": {"workload": workload, "proofs_total": total, "proofs_rank0": n,
-                   "parallelism": f"proof-sharded x{world}", "air": args.air},
+                   "parallelism": f"proof-sharded x{world}", "air": args.air,
+                   # value's input: the raw proof words already in HBM when the timed region starts;
+                   # the host-memory (PCIe-inclusive) rate is pcie_inclusive, never value
+                   "input": "HBM-resident raw proof words (uploaded before the timed region; decoded on the "
+                            "device every step)",
+                   "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                   "lib_sha256": lib_sha256()[:16]},
         # what one step is: the raw proof words are resident in HBM when the step starts; the step
         # decodes every proof stream on the device (k_decode) and runs every verifier phase
         "step": "device proof-stream decode + Fiat-Shamir replay + row hashing + Merkle multiproofs + OOD AIR + "
@@ -661,9 +805,15 @@ def main():
     if valu_step:
         # the whole pipeline against the measured VALU issue ceiling: committed PMC instruction
         # count of one step (per GPU) / this run's step time
+        # frac: against the fastest issue rate measured for any instruction class (cheap movs /
+        # adds, 1.7 wave64 instructions per CU-clock), a hard ceiling; vs_regular_rate: against the
+        # rate of the regular and slow classes the Tip5 mix is made of (1 per CU-clock), which the
+        # mix's cheap instructions let it exceed slightly
+        rate = valu_step / (elapsed / K)
         res["valu_issue"] = {"wave_instr_per_step": valu_step, "profile": valu_tag,
-                             "ceiling_wave_instr_per_s": VALU_ISSUE_CEILING,
-                             "frac": valu_step / (elapsed / K) / VALU_ISSUE_CEILING}
+                             "ceiling_wave_instr_per_s": VALU_ISSUE_MAX, "frac": rate / VALU_ISSUE_MAX,
+                             "regular_rate_wave_instr_per_s": VALU_ISSUE_CEILING,
+                             "vs_regular_rate": rate / VALU_ISSUE_CEILING}
     # proof streaming: every proof word is read by the device at least once per step
     words_step = st0["proof_words"]
     step_s = elapsed / K
@@ -675,12 +825,16 @@ def main():
                            "pmc_frac": bytes_step / step_s / HBM_PEAK, "pmc_profile": bytes_tag})
     for b in ring:
         b.close()
+    _assert_fracs(res)
     # the PCIe-inclusive leg and the config-2 microbench belong to the one-GPU report (N = 1): with
     # several ranks, rank 0 would run them alone while the others tear down
     if world == 1 and args.stream_batches > 0:
         res["pcie_inclusive"] = pcie_stream(ctx, gair, stark, claims, proofs, expect, args.stream_batches)
     if world == 1 and args.paths_log2 > 0:
         res["tip5_paths"] = tip5_paths(ctx, args.paths_log2, 5)
+    if world == 1 and args.config1_seconds > 0 and not args.no_cpu:
+        res["config1_latency"] = config1_latency(ctx, gair, stark, air_words, args.config1_seconds)
+        correct = correct and res["config1_latency"]["verdict_accept"]
     if cpu is not None:
         res["cpu_baseline"] = cpu
     if rank == 0:

@@ -29,9 +29,14 @@
 
 #include "../../include/neptune_hip.h"
 
+// stark_host.cpp: true once every phase of a launched batch has completed (a stream query, no wait)
+extern "C" bool nhip_internal_batch_done(nhip_batch* b);
+
 namespace {
 
 using Clock = std::chrono::steady_clock;
+// how often the in-flight batch is polled while a coalescing window is open
+constexpr std::chrono::microseconds POLL_SLICE{25};
 
 struct Req {
     const nhip_claim* claims;
@@ -129,9 +134,22 @@ struct nhip_queue {
                 cv_in.wait(lk, [&] { return stop || !pending.empty(); });
                 if (pending.empty()) break;  // stop, drained
             }
-            // coalescing window from the oldest request's arrival, ended early by a full batch
+            // coalescing window from the oldest request's arrival, ended early by a full batch.  The
+            // batch still on the device is answered as soon as it completes, not after the window
+            // and the next batch's staging: while it runs the window is waited in short slices that
+            // poll its stream.
             const Clock::time_point deadline = pending.front()->arrived + max_wait;
-            cv_in.wait_until(lk, deadline, [&] { return stop || pending_proofs >= max_batch; });
+            for (;;) {
+                if (in_flight[s ^ 1] && nhip_internal_batch_done(slot[s ^ 1])) {
+                    lk.unlock();
+                    finish(s ^ 1);
+                    lk.lock();
+                }
+                if (stop || pending_proofs >= max_batch || Clock::now() >= deadline) break;
+                const Clock::time_point until =
+                    in_flight[s ^ 1] ? std::min(deadline, Clock::now() + POLL_SLICE) : deadline;
+                cv_in.wait_until(lk, until, [&] { return stop || pending_proofs >= max_batch; });
+            }
             size_t taken = 0;
             while (!pending.empty() && (taken == 0 || taken + pending.front()->n <= max_batch) &&
                    in_slot[s].size() < in_slot[s].capacity()) {

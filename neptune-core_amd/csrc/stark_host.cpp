@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/neptune_hip.h"
+#include "../../include/nhip_challenge_id.h"
 #include "goldilocks.hpp"
 #include "kernels.hpp"
 #include "stark.hpp"
@@ -341,7 +342,10 @@ int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
     const uint64_t M = w[1], A = w[2], K = w[3], NN = w[4];
     const uint64_t nc[4] = {w[5], w[6], w[7], w[8]};
     const uint64_t C = nc[0] + nc[1] + nc[2] + nc[3];
-    if (M > (1u << 20) || A > (1u << 20) || K < 16 || K > (1u << 20) || NN > (1u << 24) || C > (1u << 24)) return NHIP_ERR_ARG;
+    // K: the sampled challenges, triton-air's Challenges::SAMPLE_COUNT (include/nhip_challenge_id.h);
+    // the derived ones (K .. K + 3) read sampled ChallengeIds up to LookupTablePublicIndeterminate
+    if (M > (1u << 20) || A > (1u << 20) || K != NHIP_CHALLENGE_SAMPLE_COUNT || NN > (1u << 24) || C > (1u << 24))
+        return NHIP_ERR_ARG;
     if (n != 9 + 4 * NN + C) return NHIP_ERR_ARG;
     nhip_air* a = new (std::nothrow) nhip_air();
     if (!a) return NHIP_ERR_OOM;
@@ -360,7 +364,7 @@ int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
         bool ok = true;
         if (op == AIR_INPUT) {
             const uint64_t lim = x == IN_MAIN_CURR || x == IN_MAIN_NEXT ? M
-                                 : (x == IN_AUX_CURR || x == IN_AUX_NEXT ? A : (x == IN_CHALLENGE ? K + 4 : 0));
+                                 : (x == IN_AUX_CURR || x == IN_AUX_NEXT ? A : (x == IN_CHALLENGE ? K + NHIP_NUM_DERIVED_CHALLENGES : 0));
             ok = x <= IN_CHALLENGE && y < lim;
             nd.a = (uint32_t)x;
             nd.b = (uint32_t)y;
@@ -908,6 +912,14 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
     if (e != hipSuccess) return hipfail(e);
     b->in_flight = true;
     return NHIP_OK;
+}
+
+// Internal (queue.cpp): has every phase of a launched batch completed?  Its last packets (the verdict
+// copy) are on the main stream, which joins the aux chain before them.
+bool nhip_internal_batch_done(nhip_batch* b) {
+    if (!b || !b->in_flight) return true;
+    (void)hipSetDevice(b->device);
+    return hipStreamQuery(b->main) != hipErrorNotReady;
 }
 
 // Wait for a launched batch; verdicts (n bytes, nullable) and the batch AND (nullable).

@@ -1,12 +1,14 @@
 // Phase kernels of the batched STARK verifier (see stark.hpp for the phase list).
 //
-// Conventions: the batch word buffer holds canonical u64 field elements (proof words and staged
-// claims); every scratch value written by these kernels (samples, row digests, OOD sums) is a raw
-// Montgomery word.  Each failed check ORs a FailBits bit into fail[proof].
+// Conventions: the batch word buffer holds the proof words as the caller gave them (raw u64, any
+// value: BFieldElement::new semantics) and the staged claims; every load of a field element from it
+// reduces (to_mont / canon, proof_codec.hpp), structural words are read mod p by the decoder.  Every
+// scratch value written by these kernels (samples, row digests, OOD sums) is a raw Montgomery word.  Each failed check ORs a FailBits bit into fail[proof].
 #include <hip/hip_ext.h>
 
 #include <cstdlib>
 
+#include "../../include/nhip_challenge_id.h"
 #include "kernels.hpp"
 #include "proof_codec.hpp"
 #include "stark.hpp"
@@ -887,10 +889,16 @@ __device__ Xfe block_sum_xfe_waves(Xfe v, Xfe* sh) {
 }
 
 // ------------------------------------------------------------------ Challenges::new
-// triton-air 1.0 ChallengeId indices of the sampled indeterminates the derived challenges use
-// (public design, unpinned; oracle/stark_ref.py derive_challenges)
-static constexpr uint32_t CH_COMPRESS_PROGRAM_DIGEST = 0, CH_STANDARD_INPUT = 1, CH_STANDARD_OUTPUT = 2,
-                          CH_LOOKUP_TABLE_PUBLIC = 15;
+// triton-air 1.0 ChallengeId indices (include/nhip_challenge_id.h; public design, unpinned) of the
+// sampled indeterminates the derived challenges use
+static constexpr uint32_t CH_COMPRESS_PROGRAM_DIGEST = NHIP_CH_CompressProgramDigestIndeterminate,
+                          CH_STANDARD_INPUT = NHIP_CH_StandardInputIndeterminate,
+                          CH_STANDARD_OUTPUT = NHIP_CH_StandardOutputIndeterminate,
+                          CH_LOOKUP_TABLE_PUBLIC = NHIP_CH_LookupTablePublicIndeterminate;
+static_assert(CH_LOOKUP_TABLE_PUBLIC == 54 && NHIP_CHALLENGE_SAMPLE_COUNT == 59 && NHIP_CHALLENGE_COUNT == 63,
+              "triton-air ChallengeId layout");
+static_assert(NHIP_CH_StandardInputTerminal == NHIP_CHALLENGE_SAMPLE_COUNT && NHIP_CH_CompressedProgramDigest == 62,
+              "derived challenges follow the sampled ones");
 
 __device__ __forceinline__ Xfe shfl_xor_xfe(Xfe v, int m) {
     return {(uint64_t)__shfl_xor((long long)v.c0, m), (uint64_t)__shfl_xor((long long)v.c1, m),

@@ -13,12 +13,18 @@
 //! * The mock-proof gate and the claims cache (`verifier.rs:47-55`) stay in neptune-core, in front
 //!   of this crate.
 //! * The AIR is data: the descriptor words of triton-air 1.0.0's constraint circuits (format:
-//!   DESIGN.md §9 of the neptune-hip repository), built once at startup.
+//!   DESIGN.md §9 of the neptune-hip repository), exported from the circuits by [`air_export`] and
+//!   built once at startup ([`Air::triton`]).
+//! * Process-wide use: [`gpu_verifier`] / [`gpu_node`] create the verifier once, on first use,
+//!   from the environment (`NEPTUNE_HIP_DEVICE`, `NEPTUNE_HIP_DEVICES`); `None` means "no GPU"
+//!   and the callers take the CPU path.
 //!
 //! Not compiled in the build container (no Rust toolchain there); the C ABI underneath is
 //! exercised by the repository's Python and C99 tests.
 use std::ptr;
-use std::sync::Mutex;
+use std::sync::{Mutex, OnceLock};
+
+pub mod air_export;
 
 use neptune_hip_sys as sys;
 use triton_vm::prelude::{BFieldElement, Claim, Digest, Proof, Stark};
@@ -65,6 +71,13 @@ impl Air {
         let mut a = ptr::null_mut();
         ok(unsafe { sys::nhip_air_create(words.as_ptr(), words.len(), &mut a) })?;
         Ok(Air(a))
+    }
+
+    /// triton-air 1.0.0's constraints, the AIR `triton_vm::verify` evaluates.  An export failure
+    /// is reported as `NHIP_ERR_ARG` (the verifier never runs a partial circuit).
+    pub fn triton() -> Result<Self, GpuFault> {
+        let words = air_export::triton_air_descriptor().map_err(|_| GpuFault(sys::NHIP_ERR_ARG))?;
+        Self::from_descriptor(&words)
     }
 }
 impl Drop for Air {
@@ -120,6 +133,9 @@ impl Verifier {
     /// `device`: HIP ordinal.  `max_wait_us`: how long the queue may hold a single-proof call to
     /// coalesce it with concurrent ones (200 us is a good default: a lone proof takes ~1.7 ms).
     pub fn new(device: u32, air: Air, max_wait_us: u32) -> Result<Self, GpuFault> {
+        if device >= 32 {
+            return Err(GpuFault(sys::NHIP_ERR_ARG)); // the device mask is 32 bits
+        }
         let mut ctx = ptr::null_mut();
         ok(unsafe { sys::nhip_init(1u32 << device, &mut ctx) })?;
         let params = default_params();
@@ -208,6 +224,48 @@ impl Drop for GpuNode {
     }
 }
 
+/// Hardware queues the verifier's pipeline uses when it is the first HIP user of the process: two
+/// batches in flight, each with a hashing and a latency stream, plus the context stream and one
+/// spare (HIP serializes streams that share a queue; its default is 4).  Set only if the operator
+/// has not set `GPU_MAX_HW_QUEUES`, and only before the first HIP call (later it has no effect).
+pub const HW_QUEUES: u32 = 8;
+
+fn provision_hw_queues() {
+    if std::env::var_os("GPU_MAX_HW_QUEUES").is_none() {
+        std::env::set_var("GPU_MAX_HW_QUEUES", HW_QUEUES.to_string());
+    }
+}
+
+static GPU_VERIFIER: OnceLock<Option<Verifier>> = OnceLock::new();
+static GPU_NODE: OnceLock<Option<GpuNode>> = OnceLock::new();
+
+/// The process's single-GPU verifier (created on first use): device `NEPTUNE_HIP_DEVICE`
+/// (default 0), triton-air's AIR, a 200 us coalescing window.  `None` when there is no usable GPU.
+/// This is the `GPU_VERIFIER.get()` of INTEGRATION.md.
+pub fn gpu_verifier() -> Option<&'static Verifier> {
+    GPU_VERIFIER
+        .get_or_init(|| {
+            provision_hw_queues();
+            let dev = std::env::var("NEPTUNE_HIP_DEVICE").ok().and_then(|v| v.parse().ok()).unwrap_or(0);
+            Air::triton().and_then(|air| Verifier::new(dev, air, 200)).ok()
+        })
+        .as_ref()
+}
+
+/// Every GPU of the node (created on first use): the device mask `NEPTUNE_HIP_DEVICES` (hex or
+/// decimal, default 0 = every visible GPU).  `None` when there is no usable GPU.
+pub fn gpu_node() -> Option<&'static GpuNode> {
+    GPU_NODE
+        .get_or_init(|| {
+            provision_hw_queues();
+            let mask = std::env::var("NEPTUNE_HIP_DEVICES").ok().and_then(|v| {
+                v.strip_prefix("0x").map_or_else(|| v.parse().ok(), |h| u32::from_str_radix(h, 16).ok())
+            });
+            Air::triton().and_then(|air| GpuNode::init(mask.unwrap_or(0), air)).ok()
+        })
+        .as_ref()
+}
+
 /// The drop-in for `verifier.rs:60-63`: the GPU verdict, or on a GPU fault (or without a GPU)
 /// the CPU `triton_vm::verify`.  A fault is never turned into "accept".
 pub fn verify_or_cpu(gpu: Option<&Verifier>, claim: &Claim, proof: &Proof) -> bool {
@@ -237,10 +295,17 @@ mod tests {
     }
 
     #[test]
+    fn device_ordinals_past_the_mask_are_faults() {
+        if let Ok(air) = Air::from_descriptor(&[0x41495231, 1, 1, 59, 1, 0, 0, 0, 1, 1, 0, 0, 0, 0]) {
+            assert_eq!(Verifier::new(32, air, 200).err(), Some(GpuFault(sys::NHIP_ERR_ARG)));
+        }
+    }
+
+    #[test]
     fn no_gpu_is_a_fault_never_an_accept() {
         // on a host without a GPU: nhip_init fails, and the fallback is the CPU verifier, which
         // rejects the reference's bogus proofs (verifier.rs:95-118, neptune_proof.rs:118-133)
-        let air = Air::from_descriptor(&[0x41495231, 1, 1, 16, 1, 0, 0, 0, 1, 1, 0, 0, 0, 0]);
+        let air = Air::from_descriptor(&[0x41495231, 1, 1, 59, 1, 0, 0, 0, 1, 1, 0, 0, 0, 0]);
         if let Ok(air) = air {
             if let Err(fault) = Verifier::new(0, air, 200) {
                 assert_ne!(fault.0, sys::NHIP_OK);

@@ -23,6 +23,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* the ChallengeId table, shared with the kernels (stark_ref.CHALLENGE_IDS is the independent copy) */
+#include "../include/nhip_challenge_id.h"
+
 #define P 0xFFFFFFFF00000001ull
 #define EPS 0xFFFFFFFFull
 typedef unsigned __int128 u128;
@@ -390,18 +393,22 @@ static int verify_one(const params_t* pp, const air_t* air, const claim_t* cl, c
     if (!main_root) goto out;
     xfe* chal = smp;
     sp_sample_scalars(&ps->sp, air->num_sampled, chal);
-    if (air->num_sampled < 16) goto out;
+    if (air->num_sampled != NHIP_CHALLENGE_SAMPLE_COUNT) goto out;
     {   /* Challenges::new (stark_ref.derive_challenges): EvalArg terminals folded from 1 with the
-           named indeterminates (ChallengeId 0, 1, 2, 15), appended in ChallengeId order: input,
-           output, lookup-table public (over tip5::LOOKUP_TABLE), compressed program digest */
+           named indeterminates (ChallengeId table: include/nhip_challenge_id.h), appended in
+           ChallengeId order: input, output, lookup-table public (over tip5::LOOKUP_TABLE),
+           compressed program digest */
+        const xfe c_in = chal[NHIP_CH_StandardInputIndeterminate], c_out = chal[NHIP_CH_StandardOutputIndeterminate];
+        const xfe c_lut = chal[NHIP_CH_LookupTablePublicIndeterminate];
+        const xfe c_dig = chal[NHIP_CH_CompressProgramDigestIndeterminate];
         xfe ein = X1, eout = X1, lut = X1, comp = X1;
-        for (size_t i = 0; i < cl->input_len; ++i) ein = xadd(xmul(ein, chal[1]), xlift(cl->input[i] % P));
-        for (size_t i = 0; i < cl->output_len; ++i) eout = xadd(xmul(eout, chal[2]), xlift(cl->output[i] % P));
+        for (size_t i = 0; i < cl->input_len; ++i) ein = xadd(xmul(ein, c_in), xlift(cl->input[i] % P));
+        for (size_t i = 0; i < cl->output_len; ++i) eout = xadd(xmul(eout, c_out), xlift(cl->output[i] % P));
         for (uint64_t x = 0; x < 256; ++x) {
             const uint64_t y = x + 1;
-            lut = xadd(xmul(lut, chal[15]), xlift((y * y % 257u * y % 257u + 256u) % 257u));
+            lut = xadd(xmul(lut, c_lut), xlift((y * y % 257u * y % 257u + 256u) % 257u));
         }
-        for (int i = 0; i < 5; ++i) comp = xadd(xmul(comp, chal[0]), xlift(cl->digest[i] % P));
+        for (int i = 0; i < 5; ++i) comp = xadd(xmul(comp, c_dig), xlift(cl->digest[i] % P));
         chal[air->num_sampled] = ein;
         chal[air->num_sampled + 1] = eout;
         chal[air->num_sampled + 2] = lut;

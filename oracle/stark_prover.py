@@ -97,7 +97,7 @@ def prove(params: S.StarkParams, air: S.AirCircuit, recipe: S.SynthRecipe, claim
     main: List[list] = [None] * M
     aux: List[list] = [None] * A
     free_deg = max(1, Tlen // 4 - 1)
-    for c in recipe.free_main:
+    for c in recipe.free_columns:
         main[c] = rand_b(free_deg)
     quot_r = {}
 

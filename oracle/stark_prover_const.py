@@ -55,7 +55,7 @@ def prove(params: S.StarkParams, air: S.AirCircuit, recipe: S.SynthRecipe, claim
     ps.enqueue(S.LOG2_PADDED_HEIGHT, log2_ph)
 
     target_of = {(t["aux"], t["col"]): i for i, t in enumerate(recipe.targets)}
-    free = {c: rng.fe() for c in recipe.free_main}
+    free = {c: rng.fe() for c in recipe.free_columns}
     memo: Dict[tuple, tuple] = {}
 
     def col_value(is_aux: bool, col: int, chal):

@@ -200,7 +200,7 @@ def prove(params: S.StarkParams, air: S.AirCircuit, recipe: S.SynthRecipe, claim
     ps.absorb_words(S.encode_claim(digest, version, inp, out))
     ps.enqueue(S.LOG2_PADDED_HEIGHT, log2_ph)
 
-    free = {c: [rng.fe() for _ in range(DF + 1)] for c in recipe.free_main}
+    free = {c: [rng.fe() for _ in range(DF + 1)] for c in recipe.free_columns}
     main_cw = np.zeros((M, N), dtype=np.uint64)
     free_next = {}
     for c, co in free.items():

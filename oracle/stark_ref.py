@@ -421,16 +421,46 @@ class AirCircuit:
         return [[vals[i] for i in cs] for cs in self.constraints]
 
 
-# triton-air 1.0 `ChallengeId` (public design; unpinned offline): the sampled indeterminates that
-# Challenges::new reads, and the derived challenges it appends after the SAMPLE_COUNT = 59 sampled
-# ones, in ChallengeId order (StandardInputTerminal, StandardOutputTerminal,
-# LookupTablePublicTerminal, CompressedProgramDigest).
-CH_COMPRESS_PROGRAM_DIGEST_INDETERMINATE = 0
-CH_STANDARD_INPUT_INDETERMINATE = 1
-CH_STANDARD_OUTPUT_INDETERMINATE = 2
-CH_LOOKUP_TABLE_PUBLIC_INDETERMINATE = 15
+# triton-air 1.0 `ChallengeId` (triton-air 1.0.0, Cargo.lock:4194; the enum in its
+# challenge_id.rs, crates.io source not vendored under /root/reference; public design, PARITY
+# UNPINNED): the 59 challenges Stark::verify squeezes (Challenges::SAMPLE_COUNT), in declaration
+# order, then the 4 that Challenges::new derives, in declaration order.  This list is written out
+# independently of include/nhip_challenge_id.h (the table the kernels and the C oracle use);
+# tests/test_challenge_ids.py checks that the two agree.
+CHALLENGE_IDS = (
+    # 0-12: argument indeterminates
+    "CompressProgramDigestIndeterminate", "StandardInputIndeterminate", "StandardOutputIndeterminate",
+    "InstructionLookupIndeterminate", "HashInputIndeterminate", "HashDigestIndeterminate", "SpongeIndeterminate",
+    "OpStackIndeterminate", "RamIndeterminate", "JumpStackIndeterminate", "U32Indeterminate",
+    "ClockJumpDifferenceLookupIndeterminate", "RamTableBezoutRelationIndeterminate",
+    # 13-15: program table weights
+    "ProgramAddressWeight", "ProgramInstructionWeight", "ProgramNextInstructionWeight",
+    # 16-19: op stack
+    "OpStackClkWeight", "OpStackIb1Weight", "OpStackPointerWeight", "OpStackFirstUnderflowElementWeight",
+    # 20-23: RAM
+    "RamClkWeight", "RamPointerWeight", "RamValueWeight", "RamInstructionTypeWeight",
+    # 24-28: jump stack
+    "JumpStackClkWeight", "JumpStackCiWeight", "JumpStackJspWeight", "JumpStackJsoWeight", "JumpStackJsdWeight",
+    # 29-31: program attestation, hash table
+    "ProgramAttestationPrepareChunkIndeterminate", "ProgramAttestationSendChunkIndeterminate", "HashCIWeight",
+    # 32-47: stack weights
+    *[f"StackWeight{i}" for i in range(16)],
+    # 48-50: hash <-> cascade, 51: cascade <-> lookup, 52-54: lookup table
+    "HashCascadeLookupIndeterminate", "HashCascadeLookInWeight", "HashCascadeLookOutWeight",
+    "CascadeLookupIndeterminate",
+    "LookupTableInputWeight", "LookupTableOutputWeight", "LookupTablePublicIndeterminate",
+    # 55-58: U32 table
+    "U32LhsWeight", "U32RhsWeight", "U32CiWeight", "U32ResultWeight",
+    # 59-62: derived by Challenges::new
+    "StandardInputTerminal", "StandardOutputTerminal", "LookupTablePublicTerminal", "CompressedProgramDigest",
+)
+CHALLENGE_ID = {name: i for i, name in enumerate(CHALLENGE_IDS)}
 NUM_DERIVED_CHALLENGES = 4
-CHALLENGE_SAMPLE_COUNT = 59
+CHALLENGE_SAMPLE_COUNT = len(CHALLENGE_IDS) - NUM_DERIVED_CHALLENGES  # 59
+CH_COMPRESS_PROGRAM_DIGEST_INDETERMINATE = CHALLENGE_ID["CompressProgramDigestIndeterminate"]  # 0
+CH_STANDARD_INPUT_INDETERMINATE = CHALLENGE_ID["StandardInputIndeterminate"]  # 1
+CH_STANDARD_OUTPUT_INDETERMINATE = CHALLENGE_ID["StandardOutputIndeterminate"]  # 2
+CH_LOOKUP_TABLE_PUBLIC_INDETERMINATE = CHALLENGE_ID["LookupTablePublicIndeterminate"]  # 54
 
 
 def eval_arg_terminal(symbols, challenge, initial=X_ONE):
@@ -447,8 +477,8 @@ def derive_challenges(sampled, claim) -> List[Tuple[int, int, int]]:
     [input terminal, output terminal, lookup-table public terminal, compressed program digest],
     each an evaluation argument folded from 1 with its named indeterminate; the lookup terminal runs
     over twenty-first's tip5::LOOKUP_TABLE."""
-    if len(sampled) <= CH_LOOKUP_TABLE_PUBLIC_INDETERMINATE:
-        raise VerifyError("too few sampled challenges")
+    if len(sampled) != CHALLENGE_SAMPLE_COUNT:
+        raise VerifyError("Challenges::new takes exactly SAMPLE_COUNT sampled challenges")
     digest, _version, inp, out = claim
     ein = eval_arg_terminal(inp, sampled[CH_STANDARD_INPUT_INDETERMINATE])
     eout = eval_arg_terminal(out, sampled[CH_STANDARD_OUTPUT_INDETERMINATE])
@@ -482,9 +512,15 @@ class SynthRecipe:
     """Prover-side construction knowledge for a synthetic AIR (never given to the verifier)."""
 
     def __init__(self):
-        self.free_main: List[int] = []
+        self.free_main: List[int] = []       # free main columns the constraints read
+        self.unconstrained_main: List[int] = []  # free main columns no constraint reads (the last one)
         self.targets: List[dict] = []        # definitions in construction order
         self.combos: List[dict] = []         # combination constraints
+
+    @property
+    def free_columns(self) -> List[int]:
+        """Every main column whose values the prover chooses (the rest are constraint targets)."""
+        return self.free_main + self.unconstrained_main
 
 
 def synth_air(params: StarkParams, num_sampled: int = CHALLENGE_SAMPLE_COUNT, seed: int = 0x5EED, num_constraints: Optional[int] = None):
@@ -509,6 +545,10 @@ def synth_air(params: StarkParams, num_sampled: int = CHALLENGE_SAMPLE_COUNT, se
     recipe = SynthRecipe()
     n_free = max(4, (M * 2) // 5)
     recipe.free_main = list(range(n_free))
+    # the last main column is free and read by no constraint: the sparse prover
+    # (oracle/stark_prover_sparse.py) puts its one non-constant codeword there, in the row's last
+    # Tip5 absorption chunk
+    recipe.unconstrained_main = [M - 1]
     by_type: List[List[int]] = [[], [], [], []]
     base_by_type: List[List[int]] = [[], [], [], []]  # indices into recipe.targets
     type_weights = [C_CONS] * 10 + [C_TRANS] * 7 + [C_INIT] * 2 + [C_TERM]
@@ -529,7 +569,7 @@ def synth_air(params: StarkParams, num_sampled: int = CHALLENGE_SAMPLE_COUNT, se
         return node((OP_SUB, tnode, rhs, 0))
 
     # main targets: BFE-only products of free columns (+ optional linear earlier target)
-    for t in range(n_free, M):
+    for t in range(n_free, M - 1):
         ctype = pick_type()
         deg = 1 + rng.below(4)
         nxt = ctype == C_TRANS

@@ -252,6 +252,40 @@ void oracle_hash_varlen(const uint64_t *data, size_t len, uint64_t out[5]) {
     for (int i = 0; i < 5; ++i) out[i] = from_mont(s[i]);
 }
 
+/* The same sponge split in two (test-data generators: rows that share a long constant prefix).
+ * oracle_sponge_absorb_chunks: the raw Montgomery state of the VariableLength sponge after absorbing
+ * nchunks full rate chunks of data; oracle_hash_varlen_resume: hash_varlen of (those chunks ++ tail)
+ * continued from that state (tail absorbed and padded as oracle_hash_varlen does).  Both use the
+ * split-form permutation (bit-exact with perm_raw, tests/test_stark_oracle_c.py). */
+void oracle_sponge_absorb_chunks(const uint64_t *data, size_t nchunks, uint64_t s_raw[16]) {
+    memset(s_raw, 0, 16 * sizeof(uint64_t));
+    for (size_t c = 0; c < nchunks; ++c) {
+        for (int i = 0; i < 10; ++i) s_raw[i] = to_mont(data[10 * c + i] % P);
+        oracle_tip5_permutation_raw_fast(s_raw);
+    }
+}
+void oracle_hash_varlen_resume(const uint64_t s_raw[16], const uint64_t *tail, size_t len, uint64_t out[5]) {
+    uint64_t s[16];
+    memcpy(s, s_raw, sizeof(s));
+    size_t k = 0;
+    for (; k + 10 <= len; k += 10) {
+        for (int i = 0; i < 10; ++i) s[i] = to_mont(tail[k + i] % P);
+        oracle_tip5_permutation_raw_fast(s);
+    }
+    const size_t rem = len - k;
+    for (size_t i = 0; i < 10; ++i) s[i] = to_mont(i < rem ? tail[k + i] % P : (i == rem ? 1 : 0));
+    oracle_tip5_permutation_raw_fast(s);
+    for (int i = 0; i < 5; ++i) out[i] = from_mont(s[i]);
+}
+/* hash_pair with the split-form permutation */
+void oracle_hash_pair_fast(const uint64_t l[5], const uint64_t r[5], uint64_t out[5]) {
+    uint64_t s[16];
+    for (int i = 0; i < 5; ++i) { s[i] = to_mont(l[i] % P); s[5 + i] = to_mont(r[i] % P); }
+    for (int i = 10; i < 16; ++i) s[i] = to_mont(1);
+    oracle_tip5_permutation_raw_fast(s);
+    for (int i = 0; i < 5; ++i) out[i] = from_mont(s[i]);
+}
+
 void oracle_hash_varlen_batch(const uint64_t *data, const uint64_t *offsets, size_t n, uint64_t *out) {
     for (size_t i = 0; i < n; ++i)
         oracle_hash_varlen(data + offsets[i], (size_t)(offsets[i + 1] - offsets[i]), out + 5 * i);

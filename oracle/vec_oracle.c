@@ -204,8 +204,28 @@ void hash_rows_planes(const uint64_t *planes, size_t nplanes, size_t n, uint64_t
     parallel_for(n, th, rh_range, &r);
 }
 
+/* ---- row hashing when every row shares its first full rate chunks: s0 = the sponge state after
+ * them (oracle_sponge_absorb_chunks), row i's remaining words = [tail_plane_0[i], ...] */
+extern void oracle_hash_varlen_resume(const uint64_t s_raw[16], const uint64_t *tail, size_t len, uint64_t out[5]);
+typedef struct { const uint64_t *s0, *planes; size_t ntail, n; uint64_t *out; } rt_t;
+static void rt_range(void *v, size_t lo, size_t hi) {
+    rt_t *r = (rt_t *)v;
+    uint64_t tail[64];
+    for (size_t i = lo; i < hi; ++i) {
+        for (size_t j = 0; j < r->ntail; ++j) tail[j] = r->planes[j * r->n + i];
+        oracle_hash_varlen_resume(r->s0, tail, r->ntail, r->out + 5 * i);
+    }
+}
+int hash_rows_tail(const uint64_t s0[16], const uint64_t *tail_planes, size_t ntail, size_t n, uint64_t *out, int th) {
+    if (ntail > 64) return -1;
+    rt_t r = {s0, tail_planes, ntail, n, out};
+    parallel_for(n, th, rt_range, &r);
+    return 0;
+}
+
 /* ---- Merkle tree (pow.rs / twenty-first layout), level-parallel */
-extern void oracle_hash_pair(const uint64_t l[5], const uint64_t r[5], uint64_t out[5]);
+extern void oracle_hash_pair_fast(const uint64_t l[5], const uint64_t r[5], uint64_t out[5]);
+#define oracle_hash_pair oracle_hash_pair_fast
 typedef struct { const uint64_t *src; uint64_t *dst; } lv_t;
 static void lv_range(void *v, size_t lo, size_t hi) {
     lv_t *l = (lv_t *)v;

@@ -16,7 +16,7 @@ TINY = dict(num_main=24, num_aux=9, num_collinearity_checks=8)
 
 def main():
     params = S.StarkParams(**TINY)
-    air, recipe = S.synth_air(params, num_sampled=16, seed=7)
+    air, recipe = S.synth_air(params, num_sampled=S.CHALLENGE_SAMPLE_COUNT, seed=7)
     cases = []
     for lph, claim in [(3, ([1, 2, 3, 4, 5], 0, [7, 8, 9], [10])), (4, ([9, 9, 9, 9, 9], 0, [], [3, 1, 4])),
                        (6, ([5, 4, 3, 2, 1], 0, [2] * 12, []))]:
@@ -29,7 +29,7 @@ def main():
                                                            "input": claim[2], "output": claim[3]},
                       "proof": [str(w) for w in proof], "samples": [[str(c) for c in x] for x in samples],
                       "fri_indices": indices})
-    out = {"params": TINY, "air": [str(w) for w in air.to_words()], "num_sampled": 16, "seed": 7, "cases": cases}
+    out = {"params": TINY, "air": [str(w) for w in air.to_words()], "num_sampled": S.CHALLENGE_SAMPLE_COUNT, "seed": 7, "cases": cases}
     json.dump(out, open(os.path.join(HERE, "stark_tiny.json"), "w"))
     print("wrote stark_tiny.json", sum(len(c["proof"]) for c in cases), "proof words")
 

@@ -15,20 +15,44 @@ def _latest():
     return parts[0], int(parts[1]), int(parts[2])
 
 
-def test_latest_profile_is_keyed_by_workload():
+def _profiled_lib(tag):
+    import pytest
+    f = os.path.join(ROOT, "profiles", tag, "LIB_SHA256")
+    if not os.path.exists(f):
+        pytest.skip(f"profiles/{tag} predates library hashing: no PMC figure is attached from it")
+    return open(f).read().split()[0]
+
+
+def test_latest_profile_is_keyed_by_workload_and_library(monkeypatch):
     tag, cfg, n = _latest()
+    lib = _profiled_lib(tag)
+    monkeypatch.setattr(bench, "lib_sha256", lambda path=None: lib)
     assert bench.latest_profile(cfg, n) == tag
     assert bench.latest_profile(cfg, n // 8) is None  # another per-GPU batch size
     assert bench.latest_profile(3 if cfg != 3 else 4, n) is None
+    # counters of another binary are never attached
+    monkeypatch.setattr(bench, "lib_sha256", lambda path=None: "0" * 64)
+    assert bench.latest_profile(cfg, n) is None
+    assert bench.pmc_traffic("k_mp_hash", cfg, n) == (None, None)
+    assert bench.pmc_valu_per_step(cfg, n) == (None, None)
 
 
-def test_latest_profile_files_and_pmc_figures():
+def test_fraction_guard():
+    import pytest
+    bench._assert_fracs({"a": {"frac": 0.4, "tip5_valu_frac": 0.2, "vs_regular_rate": 1.03}})
+    with pytest.raises(AssertionError):
+        bench._assert_fracs({"valu_issue": {"frac": 1.024}})
+
+
+def test_latest_profile_files_and_pmc_figures(monkeypatch):
     tag, cfg, n = _latest()
+    _profiled_lib(tag)
     d = os.path.join(ROOT, "profiles", tag)
     for f in ("SUMMARY.md", "bench_default.json", "bench_trace.json", "trace_kernel_stats.csv",
               "pmc_valu_counter_collection.csv", "pmc_fetch_counter_collection.csv",
-              "pmc_write_counter_collection.csv"):
+              "pmc_write_counter_collection.csv", "LIB_SHA256"):
         assert os.path.exists(os.path.join(d, f)), f
+    monkeypatch.setattr(bench, "lib_sha256", lambda path=None: _profiled_lib(tag))
     traffic, t_tag = bench.pmc_traffic("k_mp_hash", cfg, n)
     valu, v_tag = bench.pmc_valu_per_step(cfg, n)
     nbytes, b_tag = bench.pmc_bytes_per_step(cfg, n)
@@ -41,11 +65,14 @@ def test_latest_profile_files_and_pmc_figures():
     assert b["config"]["workload"].startswith("BASELINE config 4") and b["n_gpus"] == 1
     assert rf["bound"] == "valu" and 0 < rf["frac"] < 1 and b["cpu_baseline"]["cores"] >= 1
     assert b["verdicts_correct"] is True
+    # the default bench line of the profile was made with the profiled library
+    assert b["config"]["lib_sha256"] == _profiled_lib(tag)[:16]
 
 
 def test_summary_reproduces_the_bench_roofline():
     """SUMMARY.md's figure from trace_kernel_stats.csv alone agrees with the bench's frac within 5%."""
     tag, _, _ = _latest()
+    _profiled_lib(tag)
     text = open(os.path.join(ROOT, "profiles", tag, "SUMMARY.md")).read()
     line = next(x for x in text.splitlines() if x.startswith("Merkle hash launches in trace_kernel_stats.csv"))
     frac_trace = float(line.split("T = ")[1].split(";")[0])

@@ -93,7 +93,8 @@ def _stark_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     air, pool = bench.load_pool()
     total = 48
-    claims, proofs, expect, shards, expect_all = bench.make_config4(pool, total, 0.1, world, rank)
+    claims, proofs, expect, _, shards, expect_all = bench.make_config4(bench.pool4_from_c3(pool), total, 0.1, world,
+                                                                       rank)
     v = C.stark_verify_batch(air, S.StarkParams(), claims, proofs, threads=2)
     rng = np.random.default_rng(0xC4)
     hs = rng.choice(bench.COLLECTION_HEIGHTS, size=total)

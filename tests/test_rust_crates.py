@@ -65,3 +65,29 @@ def test_safe_crate_covers_the_drop_in_surface():
     for f in ("Cargo.toml", "build.rs"):
         assert os.path.exists(os.path.join(ROOT, "neptune-core_amd", "rust", "neptune-hip-sys", f))
     assert os.path.exists(os.path.join(ROOT, "neptune-core_amd", "rust", "neptune-hip", "Cargo.toml"))
+
+
+def test_air_exporter_matches_the_python_mirror_and_the_descriptor_format():
+    """rust/neptune-hip/src/air_export.rs (not compiled here) and its Python mirror
+    neptune_hip.air_export (tested against the oracle in tests/test_air_export.py) use the same
+    descriptor constants and handle the same node kinds; the process-wide init is exported."""
+    from neptune_hip import air_export as E
+    src = open(os.path.join(ROOT, "neptune-core_amd", "rust", "neptune-hip", "src", "air_export.rs")).read()
+    consts = {m.group(1): int(m.group(2).replace("_", ""), 0)
+              for m in re.finditer(r"pub const ([A-Z_]+): u64 = (0x[0-9a-fA-F_]+|\d+);", src)}
+    for name in ("AIR_MAGIC", "OP_INPUT", "OP_CONST", "OP_ADD", "OP_MUL", "IN_MAIN_CURR", "IN_AUX_CURR",
+                 "IN_MAIN_NEXT", "IN_AUX_NEXT", "IN_CHALLENGE"):
+        assert consts[name] == getattr(E, name), name
+    for kind in ("BConst", "XConst", "Input", "Challenge", "BinOp"):
+        assert f"CircuitExpression::{kind}" in src, kind
+    for ind in ("SingleRowIndicator::Main", "SingleRowIndicator::Aux", "DualRowIndicator::CurrentMain",
+                "DualRowIndicator::CurrentAux", "DualRowIndicator::NextMain", "DualRowIndicator::NextAux"):
+        assert ind in src, ind
+    assert "ExportError::UnknownNode" in src and "Challenges::SAMPLE_COUNT" in src
+    safe = open(SAFE).read()
+    for must in ("pub mod air_export;", "pub fn triton() -> Result<Self, GpuFault>",
+                 "pub fn gpu_verifier() -> Option<&'static Verifier>", "pub fn gpu_node() -> Option<&'static GpuNode>",
+                 "if device >= 32"):
+        assert must in safe, must
+    toml = open(os.path.join(ROOT, "neptune-core_amd", "rust", "neptune-hip", "Cargo.toml")).read()
+    assert 'triton-constraint-builder = "1.0.0"' in toml and 'triton-constraint-circuit = "1.0.0"' in toml

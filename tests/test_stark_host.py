@@ -95,13 +95,19 @@ def test_air_descriptor_validation():
     import neptune_hip.stark as NS
     from neptune_hip import NhipError
     params = S.StarkParams(num_main=24, num_aux=9, num_collinearity_checks=8)
-    air, _ = S.synth_air(params, num_sampled=16, seed=7)
+    air, _ = S.synth_air(params, seed=7)
     w = air.to_words()
     NS.Air(w)
     bad = list(w)
     bad[0] = 0
     with pytest.raises(NhipError):
         NS.Air(bad)
+    # the challenge layout is triton-air's: exactly Challenges::SAMPLE_COUNT = 59 sampled challenges
+    for k in (16, 55, 58, 60):
+        bad = list(w)
+        bad[3] = k
+        with pytest.raises(NhipError):
+            NS.Air(bad)
     bad = list(w)
     # forward reference in an op node -> rejected
     first_op = next(i for i, nd in enumerate(air.nodes) if nd[0] in (S.OP_ADD, S.OP_SUB, S.OP_MUL))
