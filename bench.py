@@ -20,7 +20,9 @@ region (shard.VerdictExchange); config 3 one all-reduce(MIN) of the batch verdic
 of batches runs them (--inflight 2): resident copies alternate, step k+1 is launched before step k
 is waited on, so one step's latency-bound phases overlap the other's VALU-bound hashing; every timed
 step is launched and waited inside the timed region.  Two copies x 2 streams need more than HIP's
-default 4 hardware queues per process, so GPU_MAX_HW_QUEUES defaults to 8 here.
+default 4 hardware queues per process, so GPU_MAX_HW_QUEUES is raised here before HIP starts (to
+2 x in-flight + 2, at least 8); the library's nhip_init does the same when the variable is unset.
+The default timed region is 200 steps (~2 s of sustained load).
 
 Beside `value` (HBM-resident input, the contract):
   pcie_inclusive: the same batch arriving from host memory (pinned, DMA'd per refill, two batches
@@ -30,6 +32,12 @@ Beside `value` (HBM-resident input, the contract):
   tip5_paths: the config-2 Tip5 path microbench.
   cpu_baseline: the C restatement of the verifier (oracle/stark_oracle.c), one proof per host thread,
     over a bounded sample of this batch's proofs (the reference, Rust triton-vm, cannot be built here).
+  hw_queues_4: the same workload in a child process at HIP's default 4 hardware queues.
+  config1_latency: BASELINE config 1's single-proof latency (log2-21 substitute): GPU resident and
+    from host memory, beside the C restatement on ONE host thread.
+  roofline.traffic / valu_issue / hbm.pmc_*: from the committed rocprofv3 PMC passes of
+    profiles/LATEST, attached only when profiles/<tag>/LIB_SHA256 is the hash of the library this run
+    loaded; every fraction of a ceiling is asserted <= 1.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config {3,4,5}]
        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -519,6 +527,10 @@ def main():
                     help="steps run one at a time after the timed region for roofline_isolated (0 = none: a "
                          "profiled run's kernel statistics then hold only in-flight steps)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--hwq4-steps", type=int, default=100,
+                    help="N = 1: also run the workload in a child process at HIP's default 4 hardware queues "
+                         "(GPU_MAX_HW_QUEUES=4, what a process gets that does not provision queues) and report it "
+                         "as hw_queues_4 (0 = skip)")
     ap.add_argument("--config1-seconds", type=float, default=8.0,
                     help="config-1 single-proof latency leg: CPU-restatement time budget (0 = skip the leg)")
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
@@ -569,6 +581,26 @@ def main():
         total = args.proofs or 64
         claims, proofs, expect, shards, expect_all = make_config5(air_words, total, args.log2_height, world, rank)
     n = len(proofs)
+    hwq4 = None
+    if world == 1 and args.hwq4_steps > 0 and not os.environ.get("NHIP_BENCH_HWQ"):
+        # a child process, started before this one touches the GPU: the same workload with every
+        # stream on HIP's default 4 hardware queues (the library's own provisioning is overridden)
+        import subprocess
+        cmd = [sys.executable, os.path.abspath(__file__), "--config", str(args.config), "--steps", str(args.hwq4_steps),
+               "--warmup", str(min(args.warmup, 10)), "--no-cpu", "--paths-log2", "0", "--stream-batches", "0",
+               "--config1-seconds", "0", "--iso-steps", "0", "--hwq4-steps", "0", "--air", args.air]
+        if args.proofs:
+            cmd += ["--proofs", str(args.proofs)]
+        if args.inflight:
+            cmd += ["--inflight", str(args.inflight)]
+        env = dict(os.environ, NHIP_BENCH_HWQ="4")
+        t = time.time()
+        out = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=600, check=True)
+        h = json.loads(out.stdout.decode().strip().splitlines()[-1])
+        hwq4 = {"value": h["value"], "ms_per_step": h["ms_per_step"], "steps": h["steps"],
+                "gpu_max_hw_queues": h["config"]["gpu_max_hw_queues"], "verdicts_correct": h["verdicts_correct"],
+                "measured": "child process before this one initialised HIP, same workload, NHIP_BENCH_HWQ=4"}
+        log(f"[hwq4] {h['value']:.0f} proofs/s at 4 hardware queues ({time.time() - t:.1f}s)")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         t = time.time()
@@ -837,6 +869,9 @@ def main():
         correct = correct and res["config1_latency"]["verdict_accept"]
     if cpu is not None:
         res["cpu_baseline"] = cpu
+    if hwq4 is not None:
+        res["hw_queues_4"] = hwq4
+        correct = correct and hwq4["verdicts_correct"]
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()

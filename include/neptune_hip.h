@@ -53,7 +53,10 @@ enum {
 };
 
 /* ---- context --------------------------------------------------------------------------- */
-/* Bind to the lowest HIP device whose bit is set in device_mask (0 = device 0). */
+/* Bind to the lowest HIP device whose bit is set in device_mask (0 = device 0).  If the environment
+ * has no GPU_MAX_HW_QUEUES, sets it to 8 first (two batches in flight need more than HIP's default
+ * of 4 hardware queues); HIP reads it once, so this counts only when the library is the process's
+ * first HIP user, and an operator's value always stands. */
 int nhip_init(uint32_t device_mask, nhip_ctx **out);
 void nhip_destroy(nhip_ctx *ctx);
 const char *nhip_strerror(int code);

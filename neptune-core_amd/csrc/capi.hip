@@ -6,6 +6,7 @@
 // tokio tasks: neptune-core/src/protocol/proof_abstractions/verifier.rs:60-63).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -147,9 +148,17 @@ const char* nhip_strerror(int code) {
     }
 }
 
+// Hardware queues the verifier's pipeline wants: two batches in flight, each with a hashing and a
+// latency stream, plus the context stream (HIP serializes streams that share a queue; its default
+// is 4).  HIP reads GPU_MAX_HW_QUEUES once, when it initialises: nhip_init sets it before its first
+// HIP call if the operator has not, which counts when the library is the process's first HIP user
+// (the neptune-core node) and changes nothing otherwise.
+static constexpr const char* NHIP_HW_QUEUES = "8";
+
 int nhip_init(uint32_t device_mask, nhip_ctx** out) {
     if (!out) return NHIP_ERR_ARG;
     *out = nullptr;
+    (void)setenv("GPU_MAX_HW_QUEUES", NHIP_HW_QUEUES, 0);  // 0: an operator's value stands
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return NHIP_ERR_NO_DEVICE;
     int dev = 0;
