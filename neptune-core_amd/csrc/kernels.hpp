@@ -55,6 +55,7 @@ inline uint32_t climb_max_proofs() {  // NHIP_CLIMB_MAX overrides (A/B runs)
 // one-collection latency 1.89 -> 1.65 ms, while from 512 proofs on (several steps in flight) the
 // one-row form is 2-3% faster (profiles/r01i/ab_pair.log)
 static constexpr uint32_t FS_PAIR_MAX_PROOFS = 512;
+static constexpr uint32_t OOD_WIDE_MAX_PROOFS = 64;  // k_ood_air<1024> up to this many proofs per batch
 struct MpRoot {
     uint64_t code;  // source code of the tree's final node, ~0 = no check (skipped or already failed)
     uint64_t root_off;
@@ -151,6 +152,10 @@ inline uint32_t deep_chunks(const StarkDims& d) {
 }
 inline size_t deep_lds_bytes(const StarkDims& d) {
     return (size_t)(3 * d.num_main + 9 * d.num_aux) * 8 + (size_t)deep_chunks(d) * d.num_checks * 24;
+}
+// k_deep_rows8: the weights, then one XFE per revealed row
+inline size_t deep_rows8_lds_bytes(const StarkDims& d) {
+    return (size_t)(3 * d.num_main + 9 * d.num_aux) * 8 + (size_t)d.num_checks * 24;
 }
 
 }  // namespace nhip

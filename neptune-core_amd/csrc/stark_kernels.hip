@@ -928,7 +928,10 @@ __device__ Xfe eval_terminal_wave(uint32_t n, Xfe c, Sym sym) {
 // slot, and each constraint is folded into this thread's share of sum_i w_i * C_i * Z_type(i)^-1
 // one level after it is produced.  The sum is then compared with sum_k z^k * segment_k(z^4).  Also
 // stores the OOD linear combinations used by DEEP: [sum w*curr row, sum w*next row, sum w*segs].
-__global__ void __launch_bounds__(256) k_ood_air(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+// BLOCK = 256 for batches that fill the GPU (the hashing needs the wave slots); 1,024 for small ones
+// (OOD_WIDE_MAX_PROOFS), where one proof's evaluation is on the critical path and the CUs are idle.
+template <uint32_t BLOCK>
+__global__ void __launch_bounds__(BLOCK) k_ood_air(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                                  uint32_t n_proofs, StarkDims dims, const OodIns* __restrict__ prog,
                                                  const uint32_t* __restrict__ prog_off, uint32_t n_levels,
                                                  const Xfe* __restrict__ consts, uint4 cons_type_off,
@@ -1344,12 +1347,185 @@ __global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words
     if (f) atomicOr(&fail[p], f);
 }
 
+// DEEP with eight lanes per revealed row (the default; NHIP_DEEP_ROWS8=0 selects k_deep): lane (r, q) of a
+// 256-thread workgroup takes words q, q + 8, q + 16, ... of row r of the current pass (32 rows per
+// pass), so one load instruction of a wave reads 8 rows x 64 contiguous bytes instead of 64 rows x
+// 8 bytes.  The same lazy limb accumulation per lane; each lane reduces its three accumulators to
+// field elements, the 8 lanes of a row add them (3 xor shuffles), and the DEEP check is k_deep's.
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+    return (uint64_t)__shfl_xor((long long)v, m);
+}
+
+__global__ void __launch_bounds__(256) k_deep_rows8(const uint64_t* __restrict__ words,
+                                                    const ProofDesc* __restrict__ desc, uint32_t n_proofs,
+                                                    StarkDims dims, const uint64_t* __restrict__ xs,
+                                                    const uint64_t* __restrict__ xdom,
+                                                    const uint64_t* __restrict__ ood, uint32_t* __restrict__ fail) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t M = dims.num_main, A = dims.num_aux, Q = dims.num_quot_seg, k = dims.num_checks;
+    uint64_t* wm = reinterpret_cast<uint64_t*>(smem);  // [M][3] main weights (raw)
+    uint64_t* wa = wm + 3 * M;                         // [A][3 m][3 coeff] aux weights w X^m (raw)
+    Xfe* rowsum = reinterpret_cast<Xfe*>(wa + 9 * A);  // [k] row linear combinations (raw)
+    __shared__ Xfe s_quot[MAX_CHECKS];
+    __shared__ Xfe s_at[3];
+    const uint32_t p = blockIdx.x, tid = threadIdx.x;
+    if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
+    const ProofDesc& d = desc[p];
+    const SampleLayout sl = SampleLayout::of(dims, d.R);
+    const uint64_t xb = d.xs_off * 3;
+    const uint64_t* __restrict__ lw = xs + xb + 3ull * sl.lin_w;
+    for (uint32_t i = tid; i < 3 * M; i += blockDim.x) wm[i] = lw[i];
+    for (uint32_t c = tid; c < A; c += blockDim.x) {
+        const uint64_t w0 = lw[3 * (M + c)], w1 = lw[3 * (M + c) + 1], w2 = lw[3 * (M + c) + 2];
+        uint64_t* o = wa + 9 * c;
+        o[0] = w0, o[1] = w1, o[2] = w2;
+        o[3] = gl_sub(0, w2), o[4] = gl_add(w0, w2), o[5] = w1;
+        o[6] = gl_sub(0, w1), o[7] = gl_sub(w1, w2), o[8] = gl_add(w0, w2);
+    }
+    if (tid == blockDim.x - 1) {
+        const Xfe z = ld_xfe_raw(xs, xb + 3ull * sl.z);
+        s_at[0] = z;
+        s_at[1] = x_scale(z, root_of_unity(d.log2_ph));
+        Xfe zq = x_one();
+        for (uint32_t q = 0; q < Q; ++q) zq = x_mul(zq, z);
+        s_at[2] = zq;
+    }
+    __syncthreads();
+    const uint32_t q8 = tid & 7u, rloc = tid >> 3;
+    const uint32_t rows_per_pass = blockDim.x >> 3;
+    for (uint32_t j0 = 0; j0 < k; j0 += rows_per_pass) {
+        const uint32_t j = j0 + rloc;
+        uint64_t acc[3][8];
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[c][q] = 0;
+        if (j < k) {
+            const uint64_t* __restrict__ mrow = words + d.main_rows_off + (uint64_t)j * M;
+            uint32_t c = q8;
+            for (; c + 8 * (DEEP_UNROLL - 1) < M; c += 8 * DEEP_UNROLL) {
+                uint64_t xv[DEEP_UNROLL];
+#pragma unroll
+                for (uint32_t u = 0; u < DEEP_UNROLL; ++u) xv[u] = mrow[c + 8 * u];
+#pragma unroll
+                for (uint32_t u = 0; u < DEEP_UNROLL; ++u) {
+                    uint32_t xq[4];
+                    limbs16(xv[u], xq);
+                    const uint32_t cc = c + 8 * u;
+                    limb_mac(acc[0], wm[3 * cc], xq);
+                    limb_mac(acc[1], wm[3 * cc + 1], xq);
+                    limb_mac(acc[2], wm[3 * cc + 2], xq);
+                }
+            }
+            for (; c < M; c += 8) {
+                uint32_t xq[4];
+                limbs16(mrow[c], xq);
+                limb_mac(acc[0], wm[3 * c], xq);
+                limb_mac(acc[1], wm[3 * c + 1], xq);
+                limb_mac(acc[2], wm[3 * c + 2], xq);
+            }
+            // aux row: word w is coefficient m = w % 3 of column w / 3
+            const uint64_t* __restrict__ arow = words + d.aux_rows_off + (uint64_t)j * 3 * A;
+            const uint32_t WA = 3 * A;
+            uint32_t w = q8;
+            for (; w + 8 * (DEEP_UNROLL - 1) < WA; w += 8 * DEEP_UNROLL) {
+                uint64_t xv[DEEP_UNROLL];
+#pragma unroll
+                for (uint32_t u = 0; u < DEEP_UNROLL; ++u) xv[u] = arow[w + 8 * u];
+#pragma unroll
+                for (uint32_t u = 0; u < DEEP_UNROLL; ++u) {
+                    uint32_t xq[4];
+                    limbs16(xv[u], xq);
+                    const uint32_t ww = w + 8 * u, col = ww / 3, m = ww - 3 * col;
+                    const uint64_t* wt = wa + 9 * col + 3 * m;
+                    limb_mac(acc[0], wt[0], xq);
+                    limb_mac(acc[1], wt[1], xq);
+                    limb_mac(acc[2], wt[2], xq);
+                }
+            }
+            for (; w < WA; w += 8) {
+                uint32_t xq[4];
+                limbs16(arow[w], xq);
+                const uint32_t col = w / 3, m = w - 3 * col;
+                const uint64_t* wt = wa + 9 * col + 3 * m;
+                limb_mac(acc[0], wt[0], xq);
+                limb_mac(acc[1], wt[1], xq);
+                limb_mac(acc[2], wt[2], xq);
+            }
+        }
+        // the row's 8 lanes: reduce, then add (every lane of the wave takes part in the shuffles)
+        uint64_t v0 = limb_reduce(acc[0]), v1 = limb_reduce(acc[1]), v2 = limb_reduce(acc[2]);
+#pragma unroll
+        for (int m = 1; m < 8; m <<= 1) {
+            v0 = gl_add(v0, shfl_xor_u64(v0, m));
+            v1 = gl_add(v1, shfl_xor_u64(v1, m));
+            v2 = gl_add(v2, shfl_xor_u64(v2, m));
+        }
+        if (j < k && q8 == 0) rowsum[j] = {v0, v1, v2};
+        if (j < k && q8 == 1) {
+            // quotient segments: sum_q w_q * seg_q (canonical products of raw weights and words)
+            Xfe qv = x_zero();
+            for (uint32_t q = 0; q < Q; ++q)
+                qv = x_add(qv, x_mul(ld_xfe_raw(lw, 3ull * (M + A + q)),
+                                     ld_xfe_raw(words, d.quot_rows_off + (uint64_t)j * 3 * Q + 3ull * q)));
+            s_quot[j] = {to_mont(qv.c0), to_mont(qv.c1), to_mont(qv.c2)};
+        }
+    }
+    __syncthreads();
+    uint32_t f = 0;
+    for (uint32_t j2 = tid; j2 < k; j2 += blockDim.x) {
+        const Xfe row = rowsum[j2];
+        const Xfe x = x_lift(xdom[(uint64_t)p * k + j2]);
+        const Xfe d0 = x_sub(x, s_at[0]), d1 = x_sub(x, s_at[1]), d2 = x_sub(x, s_at[2]);
+        const Xfe d01 = x_mul(d0, d1);
+        const Xfe prod = x_mul(d01, d2);
+        if (x_is_zero(prod)) {
+            f |= FAIL_ZERO_INVERSE;
+            continue;
+        }
+        const Xfe inv = x_inv(prod);
+        const Xfe inv2 = x_mul(inv, d01);   // 1 / d2
+        const Xfe inv01 = x_mul(inv, d2);   // 1 / (d0 d1)
+        const Xfe inv0 = x_mul(inv01, d1);  // 1 / d0
+        const Xfe inv1 = x_mul(inv01, d0);  // 1 / d1
+        const uint64_t* __restrict__ oo = ood + (uint64_t)p * 9;
+        const uint64_t* __restrict__ wd = lw + 3ull * (M + A + Q);
+        const Xfe t0 = x_mul(x_mul(x_sub(row, ld_xfe_raw(oo, 0)), inv0), ld_xfe_raw(wd, 0));
+        const Xfe t1 = x_mul(x_mul(x_sub(row, ld_xfe_raw(oo, 3)), inv1), ld_xfe_raw(wd, 3));
+        const Xfe t2 = x_mul(x_mul(x_sub(s_quot[j2], ld_xfe_raw(oo, 6)), inv2), ld_xfe_raw(wd, 6));
+        const Xfe deep = x_add(x_add(t0, t1), t2);
+        const Xfe fri_v = ld_xfe_canon(words, d.fri[0].leaves_off + 3ull * j2);
+        if (!x_eq(deep, fri_v)) f |= FAIL_DEEP;
+    }
+    if (f) atomicOr(&fail[p], f);
+}
+
 __global__ void k_verdicts(const uint32_t* __restrict__ fail, uint32_t n, uint8_t* __restrict__ v) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = fail[i] == 0 ? 1 : 0;
 }
 
 // ------------------------------------------------------------------ launchers
+// OOD evaluator workgroup: 1,024 threads for batches of at most OOD_WIDE_MAX_PROOFS proofs
+// (NHIP_OOD_WIDE_MAX overrides, A/B runs), else 256
+static bool ood_wide(uint32_t n) {
+    static const uint32_t lim = [] {
+        const char* v = std::getenv("NHIP_OOD_WIDE_MAX");
+        return v ? (uint32_t)std::strtoul(v, nullptr, 10) : OOD_WIDE_MAX_PROOFS;
+    }();
+    return n <= lim;
+}
+
+// DEEP form: k_deep_rows8 (default; config 4 +0.3-1.0% at 512 / 1,024 / 4,096 proofs, 2 alternating
+// repetitions, profiles/r03c) or k_deep (NHIP_DEEP_ROWS8=0, A/B runs)
+static bool deep_rows8() {
+    static const bool on = [] {
+        const char* v = std::getenv("NHIP_DEEP_ROWS8");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 // Fiat-Shamir replay form for an n-proof batch (see k_fs_replay_wide).
 static bool fs_pair(uint32_t n) {
     static const int forced = [] {
@@ -1423,9 +1599,14 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         mark(10, st);
         if (!small) (void)hipStreamWaitEvent(sa, tm->ev[10], 0);  // small: OOD right after the plan
         mark(11, sa);
-        hipLaunchKernelGGL(k_ood_air, dim3(n), dim3(b.air_block), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims, b.air_prog,
-                           b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs, b.ood, b.fail,
-                           b.air_lds_slots, b.air_gslots, b.air_gslot_n);
+        if (ood_wide(n))
+            hipLaunchKernelGGL(k_ood_air<1024>, dim3(n), dim3(1024), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims,
+                               b.air_prog, b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs, b.ood,
+                               b.fail, b.air_lds_slots, b.air_gslots, b.air_gslot_n);
+        else
+            hipLaunchKernelGGL(k_ood_air<256>, dim3(n), dim3(b.air_block), b.air_lds_bytes, sa, b.words, b.desc, n,
+                               b.dims, b.air_prog, b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs,
+                               b.ood, b.fail, b.air_lds_slots, b.air_gslots, b.air_gslot_n);
         mark(6, sa);
         if (small) {
             (void)hipStreamWaitEvent(sa, tm->ev[7], 0);  // FRI done (main stream)
@@ -1433,9 +1614,14 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
             hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
             mark(7, sa);
         }
-        const uint32_t S = deep_chunks(b.dims);
-        hipLaunchKernelGGL(k_deep, dim3(n), dim3(S * k), deep_lds_bytes(b.dims), sa, b.words, b.desc, n, b.dims, S,
-                           b.xs, b.xdom, b.ood, b.fail);
+        if (deep_rows8()) {
+            hipLaunchKernelGGL(k_deep_rows8, dim3(n), dim3(256), deep_rows8_lds_bytes(b.dims), sa, b.words, b.desc, n,
+                               b.dims, b.xs, b.xdom, b.ood, b.fail);
+        } else {
+            const uint32_t S = deep_chunks(b.dims);
+            hipLaunchKernelGGL(k_deep, dim3(n), dim3(S * k), deep_lds_bytes(b.dims), sa, b.words, b.desc, n, b.dims, S,
+                               b.xs, b.xdom, b.ood, b.fail);
+        }
         mark(8, sa);
     };
     uint32_t launches = 0;
@@ -1507,9 +1693,13 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
 }
 
 hipError_t stark_set_kernel_attributes() {
-    hipError_t e = hipFuncSetAttribute((const void*)k_ood_air, hipFuncAttributeMaxDynamicSharedMemorySize, AIR_LDS_BUDGET);
+    hipError_t e = hipFuncSetAttribute((const void*)k_ood_air<256>, hipFuncAttributeMaxDynamicSharedMemorySize, AIR_LDS_BUDGET);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void*)k_ood_air<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, AIR_LDS_BUDGET);
     if (e != hipSuccess) return e;
     e = hipFuncSetAttribute((const void*)k_deep, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void*)k_deep_rows8, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
     if (e != hipSuccess) return e;
     return e;
 }

@@ -13,7 +13,7 @@ for n in ${SIZES:-4096 2048 512}; do
 for v in cur var; do
   if [ $v = var ]; then export NHIP_LIB=$PWD/$V; else unset NHIP_LIB; fi
   f=$OUT/n${n}_${v}_r$rep
-  timeout -k 10 200 python -u bench.py --no-cpu --config 4 --proofs $n --paths-log2 0 --stream-batches 0 > $f.json 2> $f.err || { tail -5 $f.err; exit 1; }
+  timeout -k 10 200 python -u bench.py --no-cpu --config 4 --proofs $n --paths-log2 0 --stream-batches 0 --hwq4-steps 0 --config1-seconds 0 --steps ${STEPS:-200} > $f.json 2> $f.err || { tail -5 $f.err; exit 1; }
   python3 -c "import json,sys;b=json.load(open(sys.argv[1]));print(sys.argv[2],round(b['value']),round(b['ms_per_step'],3),'fs',b['phase_ms']['fiat_shamir'],b['verdicts_correct'])" $f.json n${n}_${v}_r$rep
 done
 done
