@@ -55,6 +55,13 @@ inline uint32_t climb_max_proofs() {  // NHIP_CLIMB_MAX overrides (A/B runs)
 // one-collection latency 1.89 -> 1.65 ms, while from 512 proofs on (several steps in flight) the
 // one-row form is 2-3% faster (profiles/r01i/ab_pair.log)
 static constexpr uint32_t FS_PAIR_MAX_PROOFS = 512;
+// batches of at least this many proofs replay Fiat-Shamir on the quad Tip5 (k_fs_replay_quad);
+// NHIP_FS_QUAD_MIN overrides (A/B runs).  0.61x the row form's VALU instructions (profiles/r03g
+// PMC), but fewer, longer replay waves: with 256-thread workgroups (one replay wave per SIMD of the
+// CUs they land on) 4,096 proofs +1.5% and 2,048 +1.6% over the row form, 1,024 -3%; 64-thread
+// workgroups -7 to -9% at every size, 512 / 1,024 threads -1 to -25% (profiles/r03g, 2 repetitions)
+static constexpr uint32_t FS_QUAD_MIN_PROOFS = 2048;
+static constexpr uint32_t FS_QUAD_WG = 256;  // k_fs_replay_quad workgroup size
 static constexpr uint32_t OOD_WIDE_MAX_PROOFS = 64;  // k_ood_air<1024> up to this many proofs per batch
 struct MpRoot {
     uint64_t code;  // source code of the tree's final node, ~0 = no check (skipped or already failed)

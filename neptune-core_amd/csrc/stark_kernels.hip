@@ -203,6 +203,92 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
     }
 }
 
+// The same program on the quad Tip5 (tip5_permute_quad: one proof per 4 lanes, ~0.63x the 16-lane
+// row's lane-instructions per permutation at ~2.5x its dependent instructions), for large batches
+// whose sponge replays run beside the other in-flight step's hashing: the replay then costs fewer
+// of the issue slots the hashing needs.  Lane e of a proof's quad holds state words e + 4k (slot k);
+// rate word w = e + 4k < 10.  Workgroup size: quad_wg() (how the few replay waves are placed on the
+// SIMDs matters more than their count, see there).
+#ifndef NHIP_QUAD_PRIO
+#define NHIP_QUAD_PRIO NHIP_LAT_PRIO
+#endif
+__global__ void __launch_bounds__(1024) k_fs_replay_quad(const uint64_t* __restrict__ words,
+                                                       const ProofDesc* __restrict__ desc,
+                                                       const FsOp* __restrict__ ops, uint32_t n_proofs,
+                                                       uint64_t* __restrict__ xs, uint32_t* __restrict__ idx_out,
+                                                       const uint32_t* __restrict__ fail) {
+    if constexpr (NHIP_QUAD_PRIO > 0) __builtin_amdgcn_s_setprio(NHIP_QUAD_PRIO);
+    __shared__ Tip5Lds lds;
+    __shared__ uint64_t rck[80];
+    for (int i = threadIdx.x; i < 80; i += blockDim.x) rck[i] = c_tip5_rck_raw[i];
+    tip5_lds_init(lds);  // (its barrier also orders the rck stores)
+    const uint32_t e = threadIdx.x & 3u;
+    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+    if (g >= n_proofs || fail[g]) return;  // uniform within the proof's quad
+    uint32_t cq[3][4];
+    tip5_quad_coefs(e, cq);
+    const ProofDesc& d = desc[g];
+    uint64_t s[4] = {0, 0, 0, 0};
+    uint64_t xcur = d.xs_off * 3;
+    uint64_t icur = d.idx_off;
+    const uint32_t qb = threadIdx.x & 60u;  // first lane of this quad in its wave
+    // slots 0 and 1 are rate words for every lane (words e, 4 + e); slot 2 for lanes 0, 1 (8, 9)
+    const bool r2 = e < 2;
+    for (uint32_t o = 0; o < d.fs_op_n; ++o) {
+        const FsOp op = ops[d.fs_op_off + o];
+        if (op.kind == FS_ABSORB) {
+            const uint64_t* __restrict__ src = words + op.arg;
+            const uint32_t len = op.n;
+            const uint32_t nchunks = len / TIP5_RATE + 1;
+            uint64_t w0 = e < len ? src[e] : 0ull;
+            uint64_t w1 = 4 + e < len ? src[4 + e] : 0ull;
+            uint64_t w2 = (r2 && 8 + e < len) ? src[8 + e] : 0ull;
+            for (uint32_t c = 0; c < nchunks; ++c) {
+                const uint32_t pos = c * TIP5_RATE;
+                const uint32_t rem = len - pos;  // >= 10 except in the last chunk
+                const uint64_t c0 = w0, c1 = w1, c2 = w2;
+                const uint32_t nx = pos + TIP5_RATE;
+                w0 = nx + e < len ? src[nx + e] : 0ull;
+                w1 = nx + 4 + e < len ? src[nx + 4 + e] : 0ull;
+                w2 = (r2 && nx + 8 + e < len) ? src[nx + 8 + e] : 0ull;
+                s[0] = e < rem ? to_mont(c0) : (e == rem ? MONT_ONE : 0ull);
+                s[1] = 4 + e < rem ? to_mont(c1) : (4 + e == rem ? MONT_ONE : 0ull);
+                if (r2) s[2] = 8 + e < rem ? to_mont(c2) : (8 + e == rem ? MONT_ONE : 0ull);
+                tip5_permute_quad(s, cq, rck, e, lds.lut);
+            }
+        } else if (op.kind == FS_SQUEEZE_X) {
+            const uint32_t nwords = 3 * op.n;
+            for (uint32_t f = 0; f < nwords; f += TIP5_RATE) {
+                if (f + e < nwords) xs[xcur + f + e] = s[0];
+                if (f + 4 + e < nwords) xs[xcur + f + 4 + e] = s[1];
+                if (r2 && f + 8 + e < nwords) xs[xcur + f + 8 + e] = s[2];
+                tip5_permute_quad(s, cq, rck, e, lds.lut);
+            }
+            xcur += nwords;
+        } else {  // FS_SAMPLE_IDX: the valid rate words in word order, as k_fs_replay_wide
+            const uint64_t bound = op.arg;
+            uint32_t got = 0;
+            while (got < op.n) {
+                const uint64_t v0 = from_mont(s[0]), v1 = from_mont(s[1]), v2 = from_mont(s[2]);
+                tip5_permute_quad(s, cq, rck, e, lds.lut);
+                const bool ok0 = v0 != GL_P - 1, ok1 = v1 != GL_P - 1, ok2 = r2 && v2 != GL_P - 1;
+                const uint64_t b0 = __ballot(ok0), b1 = __ballot(ok1), b2 = __ballot(ok2);
+                const uint32_t bits = ((uint32_t)(b0 >> qb) & 0xFu) | (((uint32_t)(b1 >> qb) & 0xFu) << 4) |
+                                      (((uint32_t)(b2 >> qb) & 0x3u) << 8);
+                auto put = [&](bool ok, uint32_t w, uint64_t v) {
+                    const uint32_t rank = __popc(bits & ((1u << w) - 1u));
+                    if (ok && got + rank < op.n) idx_out[icur + got + rank] = (uint32_t)((v & 0xFFFFFFFFull) % bound);
+                };
+                put(ok0, e, v0);
+                put(ok1, 4 + e, v1);
+                put(ok2, 8 + e, v2);
+                got += __popc(bits);
+            }
+            icur += op.n;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ revealed-row hashing
 // grid.y = 0 main, 1 aux, 2 quotient; one lane per (proof, row).
 #ifndef NHIP_ROWS_WAVES
@@ -1526,14 +1612,37 @@ static bool deep_rows8() {
     return on;
 }
 
-// Fiat-Shamir replay form for an n-proof batch (see k_fs_replay_wide).
-static bool fs_pair(uint32_t n) {
-    static const int forced = [] {
-        const char* v = std::getenv("NHIP_FS_PAIR");
-        return v ? (v[0] == '1' ? 1 : 0) : -1;
+// Fiat-Shamir replay form for an n-proof batch (see k_fs_replay_wide / k_fs_replay_quad):
+// 0 = 16-lane row, 1 = two-row pair, 2 = quad.  NHIP_FS_FORM=row|pair|quad forces one (A/B runs;
+// the older NHIP_FS_PAIR=0/1 still selects row / pair).  Read at every launch (one getenv per step)
+// so a test process can run every form on the same proofs.
+enum FsForm { FS_ROW = 0, FS_PAIR = 1, FS_QUAD = 2 };
+// k_fs_replay_quad workgroup size (NHIP_QUAD_WG = 64..1024 overrides, A/B runs)
+static uint32_t quad_wg() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("NHIP_QUAD_WG");
+        const uint32_t w = e ? (uint32_t)std::strtoul(e, nullptr, 10) : FS_QUAD_WG;
+        return (w >= 64 && w <= 1024 && w % 64 == 0) ? w : FS_QUAD_WG;
     }();
-    if (forced >= 0) return forced == 1;
-    return n < FS_PAIR_MAX_PROOFS;
+    return v;
+}
+static FsForm fs_form(uint32_t n) {
+    const int forced = [] {
+        if (const char* v = std::getenv("NHIP_FS_FORM")) {
+            if (v[0] == 'q') return (int)FS_QUAD;
+            if (v[0] == 'p') return (int)FS_PAIR;
+            if (v[0] == 'r') return (int)FS_ROW;
+        }
+        const char* v = std::getenv("NHIP_FS_PAIR");
+        return v ? (v[0] == '1' ? (int)FS_PAIR : (int)FS_ROW) : -1;
+    }();
+    static const uint32_t quad_min = [] {
+        const char* v = std::getenv("NHIP_FS_QUAD_MIN");
+        return v ? (uint32_t)std::strtoul(v, nullptr, 10) : FS_QUAD_MIN_PROOFS;
+    }();
+    if (forced >= 0) return (FsForm)forced;
+    if (n < FS_PAIR_MAX_PROOFS) return FS_PAIR;
+    return n >= quad_min ? FS_QUAD : FS_ROW;
 }
 
 hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream_t sa, StarkPhaseTimer* tm) {
@@ -1562,10 +1671,15 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     // ---- aux stream: latency-bound chain
     // small batches: the sponge replay is the critical path and most SIMDs are idle, so two rows
     // per proof (pair form) for a shorter permutation; large ones: one row per proof (fewer
-    // lane-instructions while the other steps' hashing fills the GPU).  NHIP_FS_PAIR=0/1 forces one.
-    if (fs_pair(n))
+    // lane-instructions while the other steps' hashing fills the GPU); the largest: four lanes per
+    // proof (quad form, fewer lane-instructions again).  NHIP_FS_FORM forces one.
+    const FsForm ff = fs_form(n);
+    if (ff == FS_PAIR)
         hipLaunchKernelGGL(k_fs_replay_wide<true>, dim3((n * 32 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
                            b.ops, n, b.xs, b.idx, b.fail);
+    else if (ff == FS_QUAD)
+        hipLaunchKernelGGL(k_fs_replay_quad, dim3((n * 4 + quad_wg() - 1) / quad_wg()), dim3(quad_wg()), 0, sa, b.words, b.desc, b.ops, n,
+                           b.xs, b.idx, b.fail);
     else
         hipLaunchKernelGGL(k_fs_replay_wide<false>, dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
                            b.ops, n, b.xs, b.idx, b.fail);

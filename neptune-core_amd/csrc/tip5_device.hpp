@@ -546,4 +546,96 @@ __device__ __forceinline__ uint64_t tip5_permute_pair(uint64_t s, uint32_t e, ui
     return s;
 }
 
+// ---------------------------------------------------------------------------------------------
+// "Quad" Tip5 (the sponge replay of large batches): one state on the 4 lanes of a DPP quad, lane e
+// holding words e, e + 4, e + 8, e + 12 in slots 0..3.  Every lane then has one split-and-lookup
+// word (slot 0) and three x^7 words (slots 1..3), so no lane computes an S-box result it throws
+// away (the 16-lane row computes both on every lane), and the three x^7 chains are the lane form's
+// three-product groups.  MDS: output slot k of lane e is word i = e + 4k; writing the circulant's
+// shift as m = 4a + b, the b = 0 terms are the lane's own slots (k - a) & 3 with the uniform
+// coefficient MDS[4a]; for b = 1..3 the term is slot (k - a) & 3 of lane (e - b) & 3 when e >= b,
+// and slot (k - a - 1) & 3 of that lane when e < b.  With X^b = the lane (e - b) & 3 slots (one
+// quad_perm DPP move per dword) the slot is (k - a') & 3 for both cases once the coefficient is
+// per lane: cq[b - 1][a'] = MDS[(4a' + b - 4 [e < b]) & 15].  16 terms per output as in the lane
+// form (128 multiply-adds per lane and round), then mds_ark's folded reduction four words at a
+// time.  Per round and lane ~380 VALU (1,520 per state, 1.08x the lane form's, vs 2,400 for the
+// 16-lane row) at a quarter of the lane form's dependent instructions.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void tip5_quad_coefs(uint32_t e, uint32_t cq[3][4]) {
+#pragma unroll
+    for (int b = 1; b < 4; ++b)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) cq[b - 1][a] = TIP5_MDS[(4 * a + b - (e < (uint32_t)b ? 4 : 0)) & 15];
+}
+
+// lane e of the quad reads lane (e - B) & 3: quad_perm [(0-B)&3, (1-B)&3, (2-B)&3, (3-B)&3]
+template <int B>
+__device__ __forceinline__ uint32_t quad_from(uint32_t v) {
+    constexpr int ctrl = ((0 - B) & 3) | (((1 - B) & 3) << 2) | (((2 - B) & 3) << 4) | (((3 - B) & 3) << 6);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xF, 0xF, false);
+}
+
+// s: this lane's 4 slots (raw Montgomery); rck: the 80 K = RC + 2^32 - 1 constants (c_tip5_rck_raw
+// order, staged in LDS by the caller); e: lane within the quad.
+__device__ __forceinline__ void tip5_permute_quad(uint64_t s[4], const uint32_t cq[3][4],
+                                                  const uint64_t* __restrict__ rck, uint32_t e,
+                                                  const uint8_t* __restrict__ lut) {
+#pragma unroll 1
+    for (int r = 0; r < TIP5_ROUNDS; ++r) {
+        uint64_t al[4], ah[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) al[k] = rck[r * 16 + 4 * k + e];  // LDS, issued before the S-box
+        s[0] = split_and_lookup(lut, s[0]);
+        {
+            uint64_t x2[3], x4[3], x3[3];
+            mont_mul_n_dev<3>(s + 1, s + 1, x2);
+            mont_mul_n_dev<3>(x2, x2, x4);
+            mont_mul_n_dev<3>(s + 1, x2, x3);
+            mont_mul_n_dev<3>(x3, x4, s + 1);
+        }
+        uint32_t lo[4], hi[4], xl[3][4], xh[3][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            lo[k] = (uint32_t)s[k];
+            hi[k] = (uint32_t)(s[k] >> 32);
+            xl[0][k] = quad_from<1>(lo[k]);
+            xh[0][k] = quad_from<1>(hi[k]);
+            xl[1][k] = quad_from<2>(lo[k]);
+            xh[1][k] = quad_from<2>(hi[k]);
+            xl[2][k] = quad_from<3>(lo[k]);
+            xh[2][k] = quad_from<3>(hi[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            ah[k] = 0;
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const uint64_t c = TIP5_MDS[4 * a];
+                al[k] += c * lo[(k - a) & 3];
+                ah[k] += c * hi[(k - a) & 3];
+            }
+#pragma unroll
+            for (int b = 0; b < 3; ++b)
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    al[k] += (uint64_t)cq[b][a] * xl[b][(k - a) & 3];
+                    ah[k] += (uint64_t)cq[b][a] * xh[b][(k - a) & 3];
+                }
+        }
+        // mds_ark's folded reduction (al started at K = RC + 2^32 - 1)
+        uint32_t sh[4], e4[4];
+        uint64_t slo[4], w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            unsigned int c;
+            const uint32_t m1 = __builtin_addc((uint32_t)(al[k] >> 32), (uint32_t)ah[k], 0u, &c);
+            sh[k] = (uint32_t)(ah[k] >> 32) + c;
+            slo[k] = ((uint64_t)m1 << 32) | (uint32_t)al[k];
+        }
+        mds_fold4(sh, slo, w, e4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s[k] = w[k] - e4[k];
+    }
+}
+
 }  // namespace nhip

@@ -34,6 +34,7 @@ def pytest_collection_modifyitems(session, config, items):
     """The config-4 GPU tests draw from oracle/pool4.py's 256 distinct proofs, built once per machine
     in a child process: build it here, after collection and before any test creates a GPU context,
     so the child is never forked from a process that has initialised HIP."""
-    if any(it.get_closest_marker("gpu") and "test_gpu_config4" in it.nodeid for it in items):
+    if any(it.get_closest_marker("gpu") and ("test_gpu_config4" in it.nodeid or "test_gpu_fs_forms" in it.nodeid)
+           for it in items):
         import pool4  # oracle/: test-data generator
         pool4.load()
