@@ -160,9 +160,9 @@ inline uint32_t deep_chunks(const StarkDims& d) {
 inline size_t deep_lds_bytes(const StarkDims& d) {
     return (size_t)(3 * d.num_main + 9 * d.num_aux) * 8 + (size_t)deep_chunks(d) * d.num_checks * 24;
 }
-// k_deep_rows8: the weights, then one XFE per revealed row
+// k_deep_rows8: the weights (one uint4 of limbs per coefficient), then one XFE per revealed row
 inline size_t deep_rows8_lds_bytes(const StarkDims& d) {
-    return (size_t)(3 * d.num_main + 9 * d.num_aux) * 8 + (size_t)d.num_checks * 24;
+    return (size_t)(3 * d.num_main + 9 * d.num_aux) * 16 + (size_t)d.num_checks * 24;
 }
 
 }  // namespace nhip

@@ -206,7 +206,7 @@ bool dims_from(const nhip_stark_params* sp, const nhip_air* air, Dims& D) {
     d.num_sampled = air->dims_air.num_sampled;
     d.num_constraints = air->dims_air.num_constraints;
     D.expansion = 1u << sp->log2_fri_expansion;
-    if (deep_lds_bytes(d) > 160 * 1024 - 8192) return false;
+    if (deep_lds_bytes(d) > 160 * 1024 - 8192 || deep_rows8_lds_bytes(d) > 160 * 1024 - 8192) return false;
     // the last FRI codeword has at most 2^(floor(log2 k) + 1 + log2 expansion) XFEs; bound its
     // Merkle-tree scratch (n x max_len digests)
     if ((1ull << (log2_u64(d.num_checks) + 1 + d.log2_expansion)) > 4096) return false;

@@ -1442,6 +1442,31 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
     return (uint64_t)__shfl_xor((long long)v, m);
 }
 
+// k_deep_rows8's accumulation: each weight (raw Montgomery, < 2^64) split into limbs of 22, 22 and
+// 20 bits (held in LDS as one uint4 per XFE coefficient), each proof word into its two 32-bit halves
+// (no extraction instructions); every partial product is < 2^54, so a lane's 81 words per row
+// (379 / 8 main + 264 / 8 aux; at most 2048 / 8 + 2 under dims_from's M + 3A < 2048) fit a 64-bit
+// accumulator per (limb, half) without carries (< 2^62): 6
+// multiply-adds per (word, coefficient) instead of 8 with 16-bit word limbs.
+__device__ __forceinline__ uint4 w_limbs(uint64_t w) {
+    return make_uint4((uint32_t)w & 0x3FFFFFu, (uint32_t)(w >> 22) & 0x3FFFFFu, (uint32_t)(w >> 44), 0u);
+}
+__device__ __forceinline__ void wl_mac(uint64_t (&a)[6], uint4 wl, uint32_t x0, uint32_t x1) {
+    a[0] += (uint64_t)wl.x * x0;
+    a[1] += (uint64_t)wl.y * x0;
+    a[2] += (uint64_t)wl.z * x0;
+    a[3] += (uint64_t)wl.x * x1;
+    a[4] += (uint64_t)wl.y * x1;
+    a[5] += (uint64_t)wl.z * x1;
+}
+// (sum_{i<3, h<2} a[3h + i] * 2^(22 i + 32 h)) mod p, a < 2^62 (U, W < 2^107)
+__device__ __forceinline__ uint64_t wl_reduce(const uint64_t (&a)[6]) {
+    const u128_t U = (u128_t)a[0] + ((u128_t)a[1] << 22) + ((u128_t)a[2] << 44);
+    const u128_t W = (u128_t)a[3] + ((u128_t)a[4] << 22) + ((u128_t)a[5] << 44);
+    const uint64_t ur = reduce_u108(U), wr = reduce_u108(W);
+    return gl_add(ur, reduce96(wr << 32, (uint32_t)(wr >> 32)));  // + wr * 2^32
+}
+
 __global__ void __launch_bounds__(256) k_deep_rows8(const uint64_t* __restrict__ words,
                                                     const ProofDesc* __restrict__ desc, uint32_t n_proofs,
                                                     StarkDims dims, const uint64_t* __restrict__ xs,
@@ -1449,8 +1474,8 @@ __global__ void __launch_bounds__(256) k_deep_rows8(const uint64_t* __restrict__
                                                     const uint64_t* __restrict__ ood, uint32_t* __restrict__ fail) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t M = dims.num_main, A = dims.num_aux, Q = dims.num_quot_seg, k = dims.num_checks;
-    uint64_t* wm = reinterpret_cast<uint64_t*>(smem);  // [M][3] main weights (raw)
-    uint64_t* wa = wm + 3 * M;                         // [A][3 m][3 coeff] aux weights w X^m (raw)
+    uint4* wm = reinterpret_cast<uint4*>(smem);        // [M][3 coeff] main weights (raw), w_limbs
+    uint4* wa = wm + 3 * M;                            // [A][3 m][3 coeff] aux weights w X^m (raw), w_limbs
     Xfe* rowsum = reinterpret_cast<Xfe*>(wa + 9 * A);  // [k] row linear combinations (raw)
     __shared__ Xfe s_quot[MAX_CHECKS];
     __shared__ Xfe s_at[3];
@@ -1460,13 +1485,13 @@ __global__ void __launch_bounds__(256) k_deep_rows8(const uint64_t* __restrict__
     const SampleLayout sl = SampleLayout::of(dims, d.R);
     const uint64_t xb = d.xs_off * 3;
     const uint64_t* __restrict__ lw = xs + xb + 3ull * sl.lin_w;
-    for (uint32_t i = tid; i < 3 * M; i += blockDim.x) wm[i] = lw[i];
+    for (uint32_t i = tid; i < 3 * M; i += blockDim.x) wm[i] = w_limbs(lw[i]);
     for (uint32_t c = tid; c < A; c += blockDim.x) {
         const uint64_t w0 = lw[3 * (M + c)], w1 = lw[3 * (M + c) + 1], w2 = lw[3 * (M + c) + 2];
-        uint64_t* o = wa + 9 * c;
-        o[0] = w0, o[1] = w1, o[2] = w2;
-        o[3] = gl_sub(0, w2), o[4] = gl_add(w0, w2), o[5] = w1;
-        o[6] = gl_sub(0, w1), o[7] = gl_sub(w1, w2), o[8] = gl_add(w0, w2);
+        uint4* o = wa + 9 * c;
+        o[0] = w_limbs(w0), o[1] = w_limbs(w1), o[2] = w_limbs(w2);
+        o[3] = w_limbs(gl_sub(0, w2)), o[4] = w_limbs(gl_add(w0, w2)), o[5] = w_limbs(w1);
+        o[6] = w_limbs(gl_sub(0, w1)), o[7] = w_limbs(gl_sub(w1, w2)), o[8] = w_limbs(gl_add(w0, w2));
     }
     if (tid == blockDim.x - 1) {
         const Xfe z = ld_xfe_raw(xs, xb + 3ull * sl.z);
@@ -1481,11 +1506,11 @@ __global__ void __launch_bounds__(256) k_deep_rows8(const uint64_t* __restrict__
     const uint32_t rows_per_pass = blockDim.x >> 3;
     for (uint32_t j0 = 0; j0 < k; j0 += rows_per_pass) {
         const uint32_t j = j0 + rloc;
-        uint64_t acc[3][8];
+        uint64_t acc[3][6];
 #pragma unroll
         for (int c = 0; c < 3; ++c)
 #pragma unroll
-            for (int q = 0; q < 8; ++q) acc[c][q] = 0;
+            for (int q = 0; q < 6; ++q) acc[c][q] = 0;
         if (j < k) {
             const uint64_t* __restrict__ mrow = words + d.main_rows_off + (uint64_t)j * M;
             uint32_t c = q8;
@@ -1495,20 +1520,18 @@ __global__ void __launch_bounds__(256) k_deep_rows8(const uint64_t* __restrict__
                 for (uint32_t u = 0; u < DEEP_UNROLL; ++u) xv[u] = mrow[c + 8 * u];
 #pragma unroll
                 for (uint32_t u = 0; u < DEEP_UNROLL; ++u) {
-                    uint32_t xq[4];
-                    limbs16(xv[u], xq);
-                    const uint32_t cc = c + 8 * u;
-                    limb_mac(acc[0], wm[3 * cc], xq);
-                    limb_mac(acc[1], wm[3 * cc + 1], xq);
-                    limb_mac(acc[2], wm[3 * cc + 2], xq);
+                    const uint32_t cc = c + 8 * u, x0 = (uint32_t)xv[u], x1 = (uint32_t)(xv[u] >> 32);
+                    wl_mac(acc[0], wm[3 * cc], x0, x1);
+                    wl_mac(acc[1], wm[3 * cc + 1], x0, x1);
+                    wl_mac(acc[2], wm[3 * cc + 2], x0, x1);
                 }
             }
             for (; c < M; c += 8) {
-                uint32_t xq[4];
-                limbs16(mrow[c], xq);
-                limb_mac(acc[0], wm[3 * c], xq);
-                limb_mac(acc[1], wm[3 * c + 1], xq);
-                limb_mac(acc[2], wm[3 * c + 2], xq);
+                const uint64_t xw = mrow[c];
+                const uint32_t x0 = (uint32_t)xw, x1 = (uint32_t)(xw >> 32);
+                wl_mac(acc[0], wm[3 * c], x0, x1);
+                wl_mac(acc[1], wm[3 * c + 1], x0, x1);
+                wl_mac(acc[2], wm[3 * c + 2], x0, x1);
             }
             // aux row: word w is coefficient m = w % 3 of column w / 3
             const uint64_t* __restrict__ arow = words + d.aux_rows_off + (uint64_t)j * 3 * A;
@@ -1520,27 +1543,25 @@ __global__ void __launch_bounds__(256) k_deep_rows8(const uint64_t* __restrict__
                 for (uint32_t u = 0; u < DEEP_UNROLL; ++u) xv[u] = arow[w + 8 * u];
 #pragma unroll
                 for (uint32_t u = 0; u < DEEP_UNROLL; ++u) {
-                    uint32_t xq[4];
-                    limbs16(xv[u], xq);
-                    const uint32_t ww = w + 8 * u, col = ww / 3, m = ww - 3 * col;
-                    const uint64_t* wt = wa + 9 * col + 3 * m;
-                    limb_mac(acc[0], wt[0], xq);
-                    limb_mac(acc[1], wt[1], xq);
-                    limb_mac(acc[2], wt[2], xq);
+                    // aux word ww is coefficient m = ww % 3 of column ww / 3: weight row 3 ww of wa
+                    const uint4* wt = wa + 3 * (w + 8 * u);
+                    const uint32_t x0 = (uint32_t)xv[u], x1 = (uint32_t)(xv[u] >> 32);
+                    wl_mac(acc[0], wt[0], x0, x1);
+                    wl_mac(acc[1], wt[1], x0, x1);
+                    wl_mac(acc[2], wt[2], x0, x1);
                 }
             }
             for (; w < WA; w += 8) {
-                uint32_t xq[4];
-                limbs16(arow[w], xq);
-                const uint32_t col = w / 3, m = w - 3 * col;
-                const uint64_t* wt = wa + 9 * col + 3 * m;
-                limb_mac(acc[0], wt[0], xq);
-                limb_mac(acc[1], wt[1], xq);
-                limb_mac(acc[2], wt[2], xq);
+                const uint4* wt = wa + 3 * w;
+                const uint64_t xw = arow[w];
+                const uint32_t x0 = (uint32_t)xw, x1 = (uint32_t)(xw >> 32);
+                wl_mac(acc[0], wt[0], x0, x1);
+                wl_mac(acc[1], wt[1], x0, x1);
+                wl_mac(acc[2], wt[2], x0, x1);
             }
         }
         // the row's 8 lanes: reduce, then add (every lane of the wave takes part in the shuffles)
-        uint64_t v0 = limb_reduce(acc[0]), v1 = limb_reduce(acc[1]), v2 = limb_reduce(acc[2]);
+        uint64_t v0 = wl_reduce(acc[0]), v1 = wl_reduce(acc[1]), v2 = wl_reduce(acc[2]);
 #pragma unroll
         for (int m = 1; m < 8; m <<= 1) {
             v0 = gl_add(v0, shfl_xor_u64(v0, m));
