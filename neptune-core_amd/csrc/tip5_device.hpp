@@ -85,6 +85,21 @@ __device__ __forceinline__ void tip5_lds_init(Tip5Lds& lds) {
     __syncthreads();
 }
 
+// NHIP_LUT_PERM_PACK builds pack the four looked-up bytes (each zero-extended in its own register)
+// with two v_perm_b32 (bytes 0-1 and 2-3, the selector zero-filling the other half) and one v_or_b32:
+// 2 regular + 1 cheap VALU per dword instead of the shift / or chain's 4 regular ones (a row-hashing
+// round 1,301 -> 1,285 regular instructions), yet config 4 ran 1.4% slower with it (418.5-420.5k vs
+// 424.9-426.2k proofs/s, 512-proof shares equal; 3 repetitions, profiles/r03i): not the default.
+#ifdef NHIP_LUT_PERM_PACK
+__device__ __forceinline__ uint32_t lookup4(const uint8_t* __restrict__ lut, uint32_t w) {
+    const uint32_t b0 = lut[w & 0xFFu];
+    const uint32_t b1 = lut[(w >> 8) & 0xFFu];
+    const uint32_t b2 = lut[(w >> 16) & 0xFFu];
+    const uint32_t b3 = lut[w >> 24];
+    // v_perm_b32(s0, s1, sel): byte i of the result = byte sel_i of {s0 : s1} (0-3 s1, 4-7 s0), 0x0C = 0
+    return __builtin_amdgcn_perm(b1, b0, 0x0C0C0400u) | __builtin_amdgcn_perm(b3, b2, 0x04000C0Cu);
+}
+#else  // the shift / or form (default)
 __device__ __forceinline__ uint32_t lookup4(const uint8_t* __restrict__ lut, uint32_t w) {
     const uint32_t b0 = lut[w & 0xFFu];
     const uint32_t b1 = lut[(w >> 8) & 0xFFu];
@@ -92,6 +107,7 @@ __device__ __forceinline__ uint32_t lookup4(const uint8_t* __restrict__ lut, uin
     const uint32_t b3 = lut[w >> 24];
     return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
 }
+#endif
 
 __device__ __forceinline__ uint64_t split_and_lookup(const uint8_t* __restrict__ lut, uint64_t r) {
     const uint32_t lo = lookup4(lut, (uint32_t)r);
