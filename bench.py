@@ -17,11 +17,12 @@ verdict copy back (nhip_batch_launch / nhip_batch_wait) and, for N > 1, the verd
 verdict is the MIN of the leading bytes; block validation needs every transaction's verdict:
 SURVEY.md §8e), posted without waiting and completed one step later, the last one inside the timed
 region (shard.VerdictExchange); config 3 one all-reduce(MIN) of the batch verdict.  Steps are pipelined as a node verifying a stream
-of batches runs them (--inflight 2): resident copies alternate, step k+1 is launched before step k
+of batches runs them (--inflight; 2 at >= 4,096 proofs per GPU, 8 below): resident copies rotate, step k+1 is launched before step k
 is waited on, so one step's latency-bound phases overlap the other's VALU-bound hashing; every timed
 step is launched and waited inside the timed region.  Two copies x 2 streams need more than HIP's
 default 4 hardware queues per process, so GPU_MAX_HW_QUEUES is raised here before HIP starts (to
-2 x in-flight + 2, at least 8); the library's nhip_init does the same when the variable is unset.
+2 x in-flight + 2, at least 8, at most 24); the library's nhip_init provisions 8 when the variable is
+unset.
 The default timed region is 200 steps (~2 s of sustained load).
 
 Beside `value` (HBM-resident input, the contract):
@@ -536,23 +537,11 @@ def main():
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
     ap.add_argument("--stream-batches", type=int, default=6,
                     help="PCIe-inclusive leg: batches streamed from pinned host memory (0 = skip)")
-    ap.add_argument("--inflight", type=int, default=None, choices=(1, 2, 3, 4, 5, 6),
+    ap.add_argument("--inflight", type=int, default=None, choices=tuple(range(1, 17)),
                     help="R > 1: R resident copies of the batch in rotation, up to R steps in flight (step k+1 is "
                          "launched before step k is waited on, so its row hashing fills step k's latency-bound "
-                         "phases). Default: 2 for >= 4,096 proofs per GPU (2 and 4: 366k proofs/s), 4 below "
-                         "(512 proofs: 243k / 274k / 269k proofs/s with 3 / 4 / 5; 1,024: 300k / 325k / 316k; "
-                         "2,048: 336k / 351k / 344k)")
+                         "phases). Default: 2 for >= 4,096 proofs per GPU, 8 below (profiles/r03j)")
     args = ap.parse_args()
-    # before anything initialises HIP: R resident batches x 2 streams + the context stream need
-    # their own hardware queues (streams sharing a queue serialize); the GPU boxes export HIP's
-    # default of 4.  With several ranks, two more for torch's stream and RCCL's, so that no batch
-    # stream queues behind a collective waiting for the other ranks.
-    multi_rank = int(os.environ.get("WORLD_SIZE", "1")) > 1
-    want_q = max(8, 2 * (args.inflight or 4) + 2 + (2 if multi_rank else 0))
-    if os.environ.get("NHIP_BENCH_HWQ"):  # A/B runs: exactly this many
-        os.environ["GPU_MAX_HW_QUEUES"] = os.environ["NHIP_BENCH_HWQ"]
-    elif int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < want_q:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -581,6 +570,21 @@ def main():
         total = args.proofs or 64
         claims, proofs, expect, shards, expect_all = make_config5(air_words, total, args.log2_height, world, rank)
     n = len(proofs)
+    # steps in flight: 2 from 4,096 proofs per GPU, 8 below (the N = 2 / 4 / 8 shares of config 4):
+    # 512 proofs 342-348k (4) -> 366-367k (8) proofs/s, 1,024 388-390k -> 393-397k, 2,048 412-414k
+    # -> 416-417k, 4,096 423-426k (2) vs 421-422k (4); 12 or more in flight (24 hardware queues)
+    # collapse to ~120k (profiles/r03j, 2 repetitions each)
+    R = args.inflight or (2 if n >= 4096 else 8)
+    # before anything initialises HIP (nothing above has): R resident batches x 2 streams + the
+    # context stream need their own hardware queues (streams sharing a queue serialize); the GPU
+    # boxes export HIP's default of 4.  With several ranks, two more for torch's stream and RCCL's,
+    # so that no batch stream queues behind a collective waiting for the other ranks.
+    multi_rank = world > 1
+    want_q = min(24, max(8, 2 * R + 2 + (2 if multi_rank else 0)))
+    if os.environ.get("NHIP_BENCH_HWQ"):  # A/B runs: exactly this many
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ["NHIP_BENCH_HWQ"]
+    elif int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < want_q:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
     hwq4 = None
     if world == 1 and args.hwq4_steps > 0 and not os.environ.get("NHIP_BENCH_HWQ"):
         # a child process, started before this one touches the GPU: the same workload with every
@@ -628,7 +632,6 @@ def main():
     gair = NS.Air([int(w) for w in air_words])
     stark = NS.Stark.default()
     ncl = [NS.Claim(*c) for c in claims]
-    R = args.inflight or (2 if n >= 4096 else 4)
     # R resident copies of the raw proof words (each step decodes them on the device again)
     ring = [NS.Batch(ctx, gair, stark, ncl, proofs) for _ in range(R)]
     prep_s = time.time() - t0
