@@ -537,6 +537,9 @@ def main():
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
     ap.add_argument("--stream-batches", type=int, default=6,
                     help="PCIe-inclusive leg: batches streamed from pinned host memory (0 = skip)")
+    ap.add_argument("--shuffle", action="store_true",
+                    help="config 4, one rank: verify the batch in a random order instead of the LPT order (heights "
+                         "mixed within every wave: the order a node's batch arrives in)")
     ap.add_argument("--inflight", type=int, default=None, choices=tuple(range(1, 17)),
                     help="R > 1: R resident copies of the batch in rotation, up to R steps in flight (step k+1 is "
                          "launched before step k is waited on, so its row hashing fills step k's latency-bound "
@@ -566,6 +569,11 @@ def main():
         if args.air == "synthetic":
             air_words = pool4["air"]
         claims, proofs, expect, _, shards, expect_all = make_config4(pool4, total, 0.01, world, rank)
+        if args.shuffle and world == 1:
+            order = np.random.default_rng(0x5F).permutation(len(proofs))
+            claims = [claims[i] for i in order]
+            proofs = [proofs[i] for i in order]
+            expect = expect[order]
     else:
         total = args.proofs or 64
         claims, proofs, expect, shards, expect_all = make_config5(air_words, total, args.log2_height, world, rank)
@@ -778,7 +786,8 @@ def main():
                     f"{COLLECTION_HEIGHTS}) = {n} STARK verifications per GPU, Stark::default()")
     elif args.config == 4:
         workload = (f"BASELINE config 4: {total} transaction proofs (log2 padded heights drawn from "
-                    f"{COLLECTION_HEIGHTS}, 1% corrupted), LPT-sharded over {world} GPU(s), Stark::default()")
+                    f"{COLLECTION_HEIGHTS}, 1% corrupted), LPT-sharded over {world} GPU(s), Stark::default()"
+                    + (", verified in a random order" if args.shuffle and world == 1 else ""))
     else:
         workload = (f"BASELINE config 5: {total} proofs at log2 padded height {args.log2_height} (FRI domain "
                     f"2^{args.log2_height + 3}), sharded over {world} GPU(s), Stark::default()")

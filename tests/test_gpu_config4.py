@@ -71,3 +71,27 @@ def test_config4_transcripts_vs_oracle(ctx, c4):
     for i in np.flatnonzero(~expect)[:8]:
         assert b.transcript(int(i))[2] != 0
     b.close()
+
+
+def test_config4_shuffled_order(ctx, c4):
+    """The batch in a random order (the heights mixed, as a node's batch arrives): the library
+    verifies it in shape-grouped device order (stark_host.cpp batch_prepare) and maps every verdict
+    and transcript back to the caller's index."""
+    import neptune_hip.stark as NS
+    air_words, pool4, claims, proofs, expect, srcs = c4
+    order = np.random.default_rng(0x5F).permutation(len(proofs))
+    gair = NS.Air([int(w) for w in air_words])
+    b = NS.Batch(ctx, gair, NS.Stark.default(), [NS.Claim(*claims[i]) for i in order], [proofs[i] for i in order])
+    v, ok = b.run()
+    assert [bool(x) for x in v] == [bool(expect[i]) for i in order] and not ok
+    for pos in range(0, len(order), 37):
+        i = int(order[pos])
+        xs, idx, fail = b.transcript(pos)
+        if expect[i]:
+            want_xs, want_idx = pool4["transcripts"][srcs[i]]
+            assert fail == 0 and xs == want_xs and idx == want_idx, (pos, i)
+        else:
+            assert fail != 0, (pos, i)
+    b.close()
+    got = NS.verify_batch(ctx, gair, NS.Stark.default(), [(NS.Claim(*claims[i]), proofs[i]) for i in order])
+    assert got == [bool(expect[i]) for i in order]
