@@ -340,9 +340,7 @@ __device__ __forceinline__ void hash_pair_raw(const uint64_t* l, const uint64_t*
         s[q] = l[q];
         s[5 + q] = r[q];
     }
-#pragma unroll
-    for (int q = 10; q < 16; ++q) s[q] = MONT_ONE;
-    tip5_permute_raw(s, lut);
+    tip5_permute_fixed_raw(s, lut);  // capacity 1: FixedLength domain
 #pragma unroll
     for (int q = 0; q < 5; ++q) out[q] = s[q];
 }
@@ -630,7 +628,12 @@ __device__ __forceinline__ void lcw_node(const uint64_t* __restrict__ words, con
     }
 }
 
-__global__ void __launch_bounds__(256) k_mp_hash(const uint64_t* __restrict__ words, const uint64_t* __restrict__ dig,
+// at least 5 waves per SIMD (<= 96 VGPRs): the FixedLength permutation's separate round 0 would
+// otherwise take the kernel to 109 VGPRs and 4 waves
+#ifndef NHIP_MP_WAVES
+#define NHIP_MP_WAVES 5
+#endif
+__global__ void __launch_bounds__(256, NHIP_MP_WAVES) k_mp_hash(const uint64_t* __restrict__ words, const uint64_t* __restrict__ dig,
                                                  MpPlan plan, uint32_t lvl, uint32_t mp_blocks,
                                                  const ProofDesc* __restrict__ desc, uint32_t n_proofs,
                                                  const uint32_t* __restrict__ fail, LcwTree lcw) {
@@ -685,9 +688,7 @@ __global__ void __launch_bounds__(256) k_mp_hash(const uint64_t* __restrict__ wo
         }
     }
     if (!work) return;
-#pragma unroll
-    for (int q = 10; q < 16; ++q) s[q] = MONT_ONE;
-    tip5_permute_raw(s, t5.lut);
+    tip5_permute_fixed_raw(s, t5.lut);  // capacity 1: FixedLength domain
 #pragma unroll
     for (int q = 0; q < 5; ++q) o[q] = s[q];
 }

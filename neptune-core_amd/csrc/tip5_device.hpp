@@ -310,16 +310,13 @@ __device__ __forceinline__ void mds_fold4(const uint32_t* sh, const uint64_t* sl
 // word after the accumulation instead of 15 (checked against the step-by-step form for every Tip5
 // round constant and 3 x 10^6 other in-range constants: tests/native/mds_fold_check.cpp).
 // rc: the round's 16 constants; rck: the same round's K = rc + 2^32 - 1 (c_tip5_rck_raw).
-__device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restrict__ rc,
-                                        const uint64_t* __restrict__ rck) {
-#ifdef NHIP_MDS_CARRY
-    (void)rck;
-    mds_ark_carry(s, rc);
-#else
-    (void)rc;
-    uint32_t lo[16], hi[16];
+// mds_ark's folded form over the first NIN state words (the others are known constants whose MDS
+// contribution the caller has folded into rck, see tip5_permute_fixed_raw).
+template <int NIN>
+__device__ __forceinline__ void mds_ark_fold(uint64_t s[16], const uint64_t* __restrict__ rck) {
+    uint32_t lo[NIN], hi[NIN];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < NIN; ++j) {
         lo[j] = (uint32_t)s[j];
         hi[j] = (uint32_t)(s[j] >> 32);
     }
@@ -329,7 +326,7 @@ __device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restri
         al[i] = rck[i];  // < 2^64 - 2^52 for every Tip5 constant: al never overflows
         ah[i] = 0;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < NIN; ++j) {
             const uint64_t c = TIP5_MDS[(i - j) & 15];
             al[i] += c * lo[j];
             ah[i] += c * hi[j];
@@ -349,6 +346,16 @@ __device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restri
     for (int i = 0; i < 16; i += 4) mds_fold4(sh + i, slo + i, w + i, e + i);
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[i] = w[i] - e[i];
+}
+
+__device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restrict__ rc,
+                                        const uint64_t* __restrict__ rck) {
+#ifdef NHIP_MDS_CARRY
+    (void)rck;
+    mds_ark_carry(s, rc);
+#else
+    (void)rc;
+    mds_ark_fold<16>(s, rck);
 #endif
 }
 
@@ -356,6 +363,56 @@ __device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restri
 __device__ __forceinline__ void tip5_permute_raw(uint64_t s[16], const uint8_t* __restrict__ lut) {
 #pragma unroll 1
     for (int r = 0; r < TIP5_ROUNDS; ++r) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
+        pow7_12(s + 4);
+        mds_ark(s, c_tip5_rc_raw + r * 16, c_tip5_rck_raw + r * 16);
+    }
+}
+
+
+// FixedLength-domain (hash_pair) round-0 accumulator starts: K = RC + 2^32 - 1 plus the MDS
+// contribution of the six capacity words, which enter round 0 as 1 (raw MONT_ONE = 2^32 - 1: low
+// half 2^32 - 1, high half 0) and leave its S-box as 1 (1^7 = 1).  The integer sum s of a round is
+// the same whichever part of it starts the accumulator, so the words the permutation produces are
+// bit-identical to tip5_permute_raw on a state whose words 10..15 are MONT_ONE.
+__host__ __device__ constexpr uint64_t tip5_rck0_fixed(int i) {
+    uint64_t k = TIP5_RC_RAW[i] + 0xFFFFFFFFull;
+    for (int j = 10; j < 16; ++j) k += (uint64_t)TIP5_MDS[(i - j) & 15] * 0xFFFFFFFFull;
+    return k;
+}
+constexpr bool tip5_rck0_fixed_in_range() {  // the accumulator bound mds_ark relies on
+    for (int i = 0; i < 16; ++i)
+        if (tip5_rck0_fixed(i) >= 0xFFF0000000000000ull || tip5_rck0_fixed(i) < TIP5_RC_RAW[i]) return false;
+    return true;
+}
+static_assert(tip5_rck0_fixed_in_range(), "round-0 FixedLength accumulator start below 2^64 - 2^52");
+__constant__ static uint64_t c_tip5_rck0_fixed[16] = {
+    tip5_rck0_fixed(0),  tip5_rck0_fixed(1),  tip5_rck0_fixed(2),  tip5_rck0_fixed(3),
+    tip5_rck0_fixed(4),  tip5_rck0_fixed(5),  tip5_rck0_fixed(6),  tip5_rck0_fixed(7),
+    tip5_rck0_fixed(8),  tip5_rck0_fixed(9),  tip5_rck0_fixed(10), tip5_rck0_fixed(11),
+    tip5_rck0_fixed(12), tip5_rck0_fixed(13), tip5_rck0_fixed(14), tip5_rck0_fixed(15),
+};
+
+// Tip5::hash_pair's permutation (FixedLength domain) on s[0..10] = left, right digests (raw): the
+// capacity words 10..15 are 1 on entry and are not read.  Round 0 runs x^7 on words 4..9 only and
+// the MDS over 10 inputs (the capacity's share is in c_tip5_rck0_fixed); rounds 1-4 as
+// tip5_permute_raw.  Round 0: 552 fewer VALU instructions (6 x^7 chains of 4 Montgomery products,
+// 6 x 16 x 2 MDS multiply-adds), ~7.5% of a permutation.
+__device__ __forceinline__ void tip5_permute_fixed_raw(uint64_t s[16], const uint8_t* __restrict__ lut) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
+#pragma unroll
+    for (int g = 4; g < 10; g += 3) {
+        uint64_t x2[3], x4[3], x3[3];
+        pow7_mul<3>(s + g, s + g, x2);
+        pow7_mul<3>(x2, x2, x4);
+        pow7_mul<3>(s + g, x2, x3);
+        pow7_mul<3>(x3, x4, s + g);
+    }
+    mds_ark_fold<10>(s, c_tip5_rck0_fixed);
+#pragma unroll 1
+    for (int r = 1; r < TIP5_ROUNDS; ++r) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
         pow7_12(s + 4);
