@@ -40,7 +40,7 @@ __global__ void __launch_bounds__(256) k_mast_roots(const uint64_t* __restrict__
                 s[q] = stack[lvl][q];
                 s[5 + q] = cur[q];
             }
-            tip5_permute_fixed_raw(s, t5.lut);  // capacity 1: FixedLength domain
+            tip5_hash_pair_digest(s, t5.lut);  // capacity 1: FixedLength domain
 #pragma unroll
             for (int q = 0; q < 5; ++q) cur[q] = s[q];
         }

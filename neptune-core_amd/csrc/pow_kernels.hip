@@ -28,7 +28,7 @@ __device__ __forceinline__ void hp_raw(const uint64_t* l, const uint64_t* r, uin
         s[q] = l[q];
         s[5 + q] = r[q];
     }
-    tip5_permute_fixed_raw(s, lut);  // capacity 1: FixedLength domain
+    tip5_hash_pair_digest(s, lut);  // capacity 1: FixedLength domain
 #pragma unroll
     for (int q = 0; q < 5; ++q) out[q] = s[q];
 }

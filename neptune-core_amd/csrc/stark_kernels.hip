@@ -340,7 +340,7 @@ __device__ __forceinline__ void hash_pair_raw(const uint64_t* l, const uint64_t*
         s[q] = l[q];
         s[5 + q] = r[q];
     }
-    tip5_permute_fixed_raw(s, lut);  // capacity 1: FixedLength domain
+    tip5_hash_pair_digest(s, lut);  // capacity 1: FixedLength domain
 #pragma unroll
     for (int q = 0; q < 5; ++q) out[q] = s[q];
 }
@@ -688,7 +688,7 @@ __global__ void __launch_bounds__(256, NHIP_MP_WAVES) k_mp_hash(const uint64_t* 
         }
     }
     if (!work) return;
-    tip5_permute_fixed_raw(s, t5.lut);  // capacity 1: FixedLength domain
+    tip5_hash_pair_digest(s, t5.lut);  // capacity 1: FixedLength domain
 #pragma unroll
     for (int q = 0; q < 5; ++q) o[q] = s[q];
 }

@@ -311,8 +311,10 @@ __device__ __forceinline__ void mds_fold4(const uint32_t* sh, const uint64_t* sl
 // round constant and 3 x 10^6 other in-range constants: tests/native/mds_fold_check.cpp).
 // rc: the round's 16 constants; rck: the same round's K = rc + 2^32 - 1 (c_tip5_rck_raw).
 // mds_ark's folded form over the first NIN state words (the others are known constants whose MDS
-// contribution the caller has folded into rck, see tip5_permute_fixed_raw).
-template <int NIN>
+// contribution the caller has folded into rck, see tip5_hash_pair_digest).
+// NOUT < 16: only outputs 0..NOUT-1 are computed (a digest read after the last round).
+__device__ __forceinline__ uint64_t mds_reduce_fold(uint64_t al, uint64_t ah);
+template <int NIN, int NOUT = 16>
 __device__ __forceinline__ void mds_ark_fold(uint64_t s[16], const uint64_t* __restrict__ rck) {
     uint32_t lo[NIN], hi[NIN];
 #pragma unroll
@@ -320,9 +322,9 @@ __device__ __forceinline__ void mds_ark_fold(uint64_t s[16], const uint64_t* __r
         lo[j] = (uint32_t)s[j];
         hi[j] = (uint32_t)(s[j] >> 32);
     }
-    uint64_t al[16], ah[16];
+    uint64_t al[NOUT], ah[NOUT];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < NOUT; ++i) {
         al[i] = rck[i];  // < 2^64 - 2^52 for every Tip5 constant: al never overflows
         ah[i] = 0;
 #pragma unroll
@@ -332,20 +334,23 @@ __device__ __forceinline__ void mds_ark_fold(uint64_t s[16], const uint64_t* __r
             ah[i] += c * hi[j];
         }
     }
-    uint32_t sh[16];
-    uint64_t slo[16], w[16];
-    uint32_t e[16];
+    constexpr int N4 = NOUT & ~3;
+    uint32_t sh[N4 > 0 ? N4 : 1];
+    uint64_t slo[N4 > 0 ? N4 : 1], w[N4 > 0 ? N4 : 1];
+    uint32_t e[N4 > 0 ? N4 : 1];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < N4; ++i) {
         unsigned int k;
         const uint32_t m1 = __builtin_addc((uint32_t)(al[i] >> 32), (uint32_t)ah[i], 0u, &k);
         sh[i] = (uint32_t)(ah[i] >> 32) + k;
         slo[i] = ((uint64_t)m1 << 32) | (uint32_t)al[i];
     }
 #pragma unroll
-    for (int i = 0; i < 16; i += 4) mds_fold4(sh + i, slo + i, w + i, e + i);
+    for (int i = 0; i < N4; i += 4) mds_fold4(sh + i, slo + i, w + i, e + i);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) s[i] = w[i] - e[i];
+    for (int i = 0; i < N4; ++i) s[i] = w[i] - e[i];
+#pragma unroll
+    for (int i = N4; i < NOUT; ++i) s[i] = mds_reduce_fold(al[i], ah[i]);
 }
 
 __device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restrict__ rc,
@@ -394,12 +399,14 @@ __constant__ static uint64_t c_tip5_rck0_fixed[16] = {
     tip5_rck0_fixed(12), tip5_rck0_fixed(13), tip5_rck0_fixed(14), tip5_rck0_fixed(15),
 };
 
-// Tip5::hash_pair's permutation (FixedLength domain) on s[0..10] = left, right digests (raw): the
-// capacity words 10..15 are 1 on entry and are not read.  Round 0 runs x^7 on words 4..9 only and
+// Tip5::hash_pair's permutation (FixedLength domain) on s[0..10] = left, right digests (raw),
+// producing the digest s[0..5] (the rest of the state is not the permutation's: callers read the
+// digest only).  The capacity words 10..15 are 1 on entry and are not read.  Round 0 runs x^7 on words 4..9 only and
 // the MDS over 10 inputs (the capacity's share is in c_tip5_rck0_fixed); rounds 1-4 as
-// tip5_permute_raw.  Round 0: 552 fewer VALU instructions (6 x^7 chains of 4 Montgomery products,
-// 6 x 16 x 2 MDS multiply-adds), ~7.5% of a permutation.
-__device__ __forceinline__ void tip5_permute_fixed_raw(uint64_t s[16], const uint8_t* __restrict__ lut) {
+// tip5_permute_raw, the last of them computing the digest words only.  Round 0: 552 fewer VALU
+// instructions (6 x^7 chains of 4 Montgomery products, 6 x 16 x 2 MDS multiply-adds); round 4: ~420
+// fewer (11 of 16 MDS outputs).
+__device__ __forceinline__ void tip5_hash_pair_digest(uint64_t s[16], const uint8_t* __restrict__ lut) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
 #pragma unroll
@@ -412,12 +419,18 @@ __device__ __forceinline__ void tip5_permute_fixed_raw(uint64_t s[16], const uin
     }
     mds_ark_fold<10>(s, c_tip5_rck0_fixed);
 #pragma unroll 1
-    for (int r = 1; r < TIP5_ROUNDS; ++r) {
+    for (int r = 1; r < TIP5_ROUNDS - 1; ++r) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
         pow7_12(s + 4);
         mds_ark(s, c_tip5_rc_raw + r * 16, c_tip5_rck_raw + r * 16);
     }
+    // last round: the caller reads the digest s[0..5] only, so the MDS computes those 5 outputs
+    // (11 x 16 x 2 multiply-adds and 11 reductions fewer); s[5..16] are left stale
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
+    pow7_12(s + 4);
+    mds_ark_fold<16, 5>(s, c_tip5_rck_raw + (TIP5_ROUNDS - 1) * 16);
 }
 
 }  // namespace nhip

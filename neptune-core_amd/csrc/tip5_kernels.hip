@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(256, NHIP_MINWAVES) k_hash_pair(const uint64_t
         uint64_t s[16];
         load_digest_mont(left + 5 * i, s);
         load_digest_mont(right + 5 * i, s + 5);
-        tip5_permute_fixed_raw(s, lds.lut);  // capacity 1: FixedLength domain
+        tip5_hash_pair_digest(s, lds.lut);  // capacity 1: FixedLength domain
         store_digest_canon(out + 5 * i, s);
     }
 }
@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(256, NHIP_MINWAVES) k_mtree_level(const uint64
         uint64_t s[16];
         load_digest_mont(children + 10 * i, s);
         load_digest_mont(children + 10 * i + 5, s + 5);
-        tip5_permute_fixed_raw(s, lds.lut);  // capacity 1: FixedLength domain
+        tip5_hash_pair_digest(s, lds.lut);  // capacity 1: FixedLength domain
         store_digest_canon(parents + 5 * i, s);
     }
 }
@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(256, NHIP_MINWAVES) k_mtree_verify(const uint6
                 s[k] = odd ? sib[k] : run[k];      // pow.rs:171-175: odd => hash_pair(sibling, running)
                 s[5 + k] = odd ? run[k] : sib[k];
             }
-            tip5_permute_fixed_raw(s, lds.lut);  // capacity 1: FixedLength domain
+            tip5_hash_pair_digest(s, lds.lut);  // capacity 1: FixedLength domain
 #pragma unroll
             for (int k = 0; k < 5; ++k) run[k] = s[k];
             ri >>= 1;
