@@ -312,19 +312,28 @@ __global__ void __launch_bounds__(256) NHIP_ROWS_WAVES k_hash_rows(const uint64_
         uint64_t s[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) s[q] = 0;
-        uint32_t pos = 0;
-        for (; pos + TIP5_RATE <= width; pos += TIP5_RATE) {
+        // width / 10 full chunks, then the padded one (always present); the wave's rows are of one
+        // tree, so `last` is uniform.  Every permutation but the last is followed by an absorb that
+        // overwrites the rate, so its last round computes the capacity words only.
+        const uint32_t nchunks = width / TIP5_RATE + 1;
+        for (uint32_t c = 0; c < nchunks; ++c) {
+            const uint32_t pos = c * TIP5_RATE;
+            const bool last = c + 1 == nchunks;
+            if (!last) {
 #pragma unroll
-            for (int q = 0; q < TIP5_RATE; ++q) s[q] = to_mont(row[pos + q]);
-            tip5_permute_raw(s, lds.lut);
-        }
-        const uint32_t rem = width - pos;
+                for (int q = 0; q < TIP5_RATE; ++q) s[q] = to_mont(row[pos + q]);
+            } else {
+                const uint32_t rem = width - pos;
 #pragma unroll
-        for (int q = 0; q < TIP5_RATE; ++q) {
-            const uint32_t qq = (uint32_t)q;
-            s[q] = qq < rem ? to_mont(row[pos + qq]) : (qq == rem ? MONT_ONE : 0ull);
+                for (int q = 0; q < TIP5_RATE; ++q) {
+                    const uint32_t qq = (uint32_t)q;
+                    s[q] = qq < rem ? to_mont(row[pos + qq]) : (qq == rem ? MONT_ONE : 0ull);
+                }
+            }
+            tip5_rounds_0_3(s, lds.lut);
+            if (!last) tip5_last_round<10, 16>(s, lds.lut);
+            else tip5_last_round<0, 5>(s, lds.lut);
         }
-        tip5_permute_raw(s, lds.lut);
         uint64_t* __restrict__ o = dig + (((uint64_t)p * 3 + tree) * k + j) * 5;
 #pragma unroll
         for (int q = 0; q < 5; ++q) o[q] = s[q];

@@ -312,10 +312,12 @@ __device__ __forceinline__ void mds_fold4(const uint32_t* sh, const uint64_t* sl
 // rc: the round's 16 constants; rck: the same round's K = rc + 2^32 - 1 (c_tip5_rck_raw).
 // mds_ark's folded form over the first NIN state words (the others are known constants whose MDS
 // contribution the caller has folded into rck, see tip5_hash_pair_digest).
-// NOUT < 16: only outputs 0..NOUT-1 are computed (a digest read after the last round).
+// [OBEG, OEND) != [0, 16): only those outputs are computed (a digest read after the last round,
+// or the capacity words a sponge keeps when the next absorb overwrites the rate).
 __device__ __forceinline__ uint64_t mds_reduce_fold(uint64_t al, uint64_t ah);
-template <int NIN, int NOUT = 16>
+template <int NIN, int OBEG = 0, int OEND = 16>
 __device__ __forceinline__ void mds_ark_fold(uint64_t s[16], const uint64_t* __restrict__ rck) {
+    constexpr int NOUT = OEND - OBEG;
     uint32_t lo[NIN], hi[NIN];
 #pragma unroll
     for (int j = 0; j < NIN; ++j) {
@@ -324,14 +326,15 @@ __device__ __forceinline__ void mds_ark_fold(uint64_t s[16], const uint64_t* __r
     }
     uint64_t al[NOUT], ah[NOUT];
 #pragma unroll
-    for (int i = 0; i < NOUT; ++i) {
-        al[i] = rck[i];  // < 2^64 - 2^52 for every Tip5 constant: al never overflows
-        ah[i] = 0;
+    for (int o = 0; o < NOUT; ++o) {
+        const int i = OBEG + o;
+        al[o] = rck[i];  // < 2^64 - 2^52 for every Tip5 constant: al never overflows
+        ah[o] = 0;
 #pragma unroll
         for (int j = 0; j < NIN; ++j) {
             const uint64_t c = TIP5_MDS[(i - j) & 15];
-            al[i] += c * lo[j];
-            ah[i] += c * hi[j];
+            al[o] += c * lo[j];
+            ah[o] += c * hi[j];
         }
     }
     constexpr int N4 = NOUT & ~3;
@@ -339,18 +342,18 @@ __device__ __forceinline__ void mds_ark_fold(uint64_t s[16], const uint64_t* __r
     uint64_t slo[N4 > 0 ? N4 : 1], w[N4 > 0 ? N4 : 1];
     uint32_t e[N4 > 0 ? N4 : 1];
 #pragma unroll
-    for (int i = 0; i < N4; ++i) {
+    for (int o = 0; o < N4; ++o) {
         unsigned int k;
-        const uint32_t m1 = __builtin_addc((uint32_t)(al[i] >> 32), (uint32_t)ah[i], 0u, &k);
-        sh[i] = (uint32_t)(ah[i] >> 32) + k;
-        slo[i] = ((uint64_t)m1 << 32) | (uint32_t)al[i];
+        const uint32_t m1 = __builtin_addc((uint32_t)(al[o] >> 32), (uint32_t)ah[o], 0u, &k);
+        sh[o] = (uint32_t)(ah[o] >> 32) + k;
+        slo[o] = ((uint64_t)m1 << 32) | (uint32_t)al[o];
     }
 #pragma unroll
-    for (int i = 0; i < N4; i += 4) mds_fold4(sh + i, slo + i, w + i, e + i);
+    for (int o = 0; o < N4; o += 4) mds_fold4(sh + o, slo + o, w + o, e + o);
 #pragma unroll
-    for (int i = 0; i < N4; ++i) s[i] = w[i] - e[i];
+    for (int o = 0; o < N4; ++o) s[OBEG + o] = w[o] - e[o];
 #pragma unroll
-    for (int i = N4; i < NOUT; ++i) s[i] = mds_reduce_fold(al[i], ah[i]);
+    for (int o = N4; o < NOUT; ++o) s[OBEG + o] = mds_reduce_fold(al[o], ah[o]);
 }
 
 __device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restrict__ rc,
@@ -430,7 +433,28 @@ __device__ __forceinline__ void tip5_hash_pair_digest(uint64_t s[16], const uint
 #pragma unroll
     for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
     pow7_12(s + 4);
-    mds_ark_fold<16, 5>(s, c_tip5_rck_raw + (TIP5_ROUNDS - 1) * 16);
+    mds_ark_fold<16, 0, 5>(s, c_tip5_rck_raw + (TIP5_ROUNDS - 1) * 16);
+}
+
+// Rounds 0..3 of the permutation, then the last round computing only the state words
+// [OBEG, OEND) (the sponge's kept words): hash_varlen's absorbs overwrite the rate s[0..10], so a
+// permutation followed by another absorb needs s[10..16] only (<10, 16>: 10 x 16 x 2 multiply-adds
+// and 10 reductions fewer), and the one before the digest is read needs s[0..5] (<0, 5>).
+__device__ __forceinline__ void tip5_rounds_0_3(uint64_t s[16], const uint8_t* __restrict__ lut) {
+#pragma unroll 1
+    for (int r = 0; r < TIP5_ROUNDS - 1; ++r) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
+        pow7_12(s + 4);
+        mds_ark(s, c_tip5_rc_raw + r * 16, c_tip5_rck_raw + r * 16);
+    }
+}
+template <int OBEG, int OEND>
+__device__ __forceinline__ void tip5_last_round(uint64_t s[16], const uint8_t* __restrict__ lut) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
+    pow7_12(s + 4);
+    mds_ark_fold<16, OBEG, OEND>(s, c_tip5_rck_raw + (TIP5_ROUNDS - 1) * 16);
 }
 
 }  // namespace nhip
