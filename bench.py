@@ -17,7 +17,7 @@ verdict copy back (nhip_batch_launch / nhip_batch_wait) and, for N > 1, the verd
 verdict is the MIN of the leading bytes; block validation needs every transaction's verdict:
 SURVEY.md §8e), posted without waiting and completed one step later, the last one inside the timed
 region (shard.VerdictExchange); config 3 one all-reduce(MIN) of the batch verdict.  Steps are pipelined as a node verifying a stream
-of batches runs them (--inflight; 2 at >= 4,096 proofs per GPU, 8 below): resident copies rotate, step k+1 is launched before step k
+of batches runs them (--inflight; 2 at >= 4,096 proofs per GPU, 8 from 1,024, 10 below): resident copies rotate, step k+1 is launched before step k
 is waited on, so one step's latency-bound phases overlap the other's VALU-bound hashing; every timed
 step is launched and waited inside the timed region.  Two copies x 2 streams need more than HIP's
 default 4 hardware queues per process, so GPU_MAX_HW_QUEUES is raised here before HIP starts (to
@@ -578,11 +578,12 @@ def main():
         total = args.proofs or 64
         claims, proofs, expect, shards, expect_all = make_config5(air_words, total, args.log2_height, world, rank)
     n = len(proofs)
-    # steps in flight: 2 from 4,096 proofs per GPU, 8 below (the N = 2 / 4 / 8 shares of config 4):
+    # steps in flight: 2 from 4,096 proofs per GPU, 8 from 1,024, 10 below (the N = 2 / 4 / 8 shares
+    # of config 4; config 5's 8-64 proofs: 10 vs 8 in flight +10-11%, profiles/r03s):
     # 512 proofs 342-348k (4) -> 366-367k (8) proofs/s, 1,024 388-390k -> 393-397k, 2,048 412-414k
     # -> 416-417k, 4,096 423-426k (2) vs 421-422k (4); 12 or more in flight (24 hardware queues)
     # collapse to ~120k (profiles/r03j, 2 repetitions each)
-    R = args.inflight or (2 if n >= 4096 else 8)
+    R = args.inflight or (2 if n >= 4096 else (8 if n >= 1024 else 10))
     # before anything initialises HIP (nothing above has): R resident batches x 2 streams + the
     # context stream need their own hardware queues (streams sharing a queue serialize); the GPU
     # boxes export HIP's default of 4.  With several ranks, two more for torch's stream and RCCL's,
