@@ -226,6 +226,25 @@ def make_batch(pool, collections: int, corrupt_frac: float, seed: int):
     return claims, proofs, np.array(expect, dtype=bool)
 
 
+def default_inflight(n: int) -> int:
+    """Steps in flight for an n-proof batch per GPU: 2 from 4,096 proofs, 8 from 1,024, 10 below
+    (the N = 2 / 4 / 8 shares of config 4; config 5's 8-64 proofs: 10 vs 8 in flight +10-11%,
+    profiles/r03s).  512 proofs 342-348k (4) -> 366-367k (8) proofs/s, 1,024 388-390k -> 393-397k,
+    2,048 412-414k -> 416-417k, 4,096 423-426k (2) vs 421-422k (4); 12 or more in flight (24
+    hardware queues) collapse to ~120k (profiles/r03j, 2 repetitions each)."""
+    return 2 if n >= 4096 else (8 if n >= 1024 else 10)
+
+
+def hw_queues_wanted(inflight: int, multi_rank: bool) -> int:
+    """GPU_MAX_HW_QUEUES for R steps in flight: R resident batches x 2 streams + the context stream
+    need their own hardware queues (streams sharing a queue serialize; the GPU boxes export HIP's
+    default of 4); with several ranks two more for torch's stream and RCCL's, so that no batch stream
+    queues behind a collective waiting for the other ranks.  At least 8, at most 24 (past that the
+    device's queues are time-sliced: profiles/r03j)."""
+    return min(24, max(8, 2 * inflight + 2 + (2 if multi_rank else 0)))
+
+
+
 def load_pool4():
     """The 256 distinct accepting proofs config 4 draws from (oracle/pool4.py: the 5 committed full
     proofs of c3_pool.npz + 251 sparse-prover proofs, distinct claims and seeds, every one verified
@@ -578,18 +597,9 @@ def main():
         total = args.proofs or 64
         claims, proofs, expect, shards, expect_all = make_config5(air_words, total, args.log2_height, world, rank)
     n = len(proofs)
-    # steps in flight: 2 from 4,096 proofs per GPU, 8 from 1,024, 10 below (the N = 2 / 4 / 8 shares
-    # of config 4; config 5's 8-64 proofs: 10 vs 8 in flight +10-11%, profiles/r03s):
-    # 512 proofs 342-348k (4) -> 366-367k (8) proofs/s, 1,024 388-390k -> 393-397k, 2,048 412-414k
-    # -> 416-417k, 4,096 423-426k (2) vs 421-422k (4); 12 or more in flight (24 hardware queues)
-    # collapse to ~120k (profiles/r03j, 2 repetitions each)
-    R = args.inflight or (2 if n >= 4096 else (8 if n >= 1024 else 10))
-    # before anything initialises HIP (nothing above has): R resident batches x 2 streams + the
-    # context stream need their own hardware queues (streams sharing a queue serialize); the GPU
-    # boxes export HIP's default of 4.  With several ranks, two more for torch's stream and RCCL's,
-    # so that no batch stream queues behind a collective waiting for the other ranks.
-    multi_rank = world > 1
-    want_q = min(24, max(8, 2 * R + 2 + (2 if multi_rank else 0)))
+    R = args.inflight or default_inflight(n)
+    # before anything initialises HIP (nothing above has)
+    want_q = hw_queues_wanted(R, world > 1)
     if os.environ.get("NHIP_BENCH_HWQ"):  # A/B runs: exactly this many
         os.environ["GPU_MAX_HW_QUEUES"] = os.environ["NHIP_BENCH_HWQ"]
     elif int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < want_q:

@@ -78,3 +78,17 @@ def test_summary_reproduces_the_bench_roofline():
     frac_trace = float(line.split("T = ")[1].split(";")[0])
     frac_bench = float(line.rsplit("frac ", 1)[1])
     assert abs(frac_trace / frac_bench - 1) < 0.05, (frac_trace, frac_bench)
+
+
+def test_inflight_defaults_and_queue_budget():
+    """Steps in flight per per-GPU batch size (the driver's N = 1 / 2 / 4 / 8 shares of config 4
+    and config 5's small batches) and the hardware queues bench.py provisions for them: every batch
+    stream keeps its own queue, below the 24 past which the device time-slices queues."""
+    assert [bench.default_inflight(n) for n in (4096, 2048, 1024, 512, 64, 8)] == [2, 8, 8, 10, 10, 10]
+    for n in (4096, 2048, 1024, 512, 64, 8):
+        for multi in (False, True):
+            r = bench.default_inflight(n)
+            q = bench.hw_queues_wanted(r, multi)
+            streams = 2 * r + 1 + (2 if multi else 0)  # batch streams, the context's, torch + RCCL
+            assert 8 <= q <= 24 and q >= streams, (n, multi, q, streams)
+    assert bench.hw_queues_wanted(16, True) == 24
