@@ -1232,12 +1232,34 @@ __global__ void __launch_bounds__(256) k_fri(const uint64_t* __restrict__ words,
     if (tid < L) {
         uint64_t wi = lds_pow(wsq, tid);
         const uint64_t wstep = blockDim.x < L ? wsq[31 - __clz(blockDim.x)] : MONT_ONE;
-        for (uint32_t i = tid; i < L; i += blockDim.x, wi = mont_mul(wi, wstep)) {
-            const Xfe diff = x_sub(t, x_lift(wi));
-            if (x_is_zero(diff)) atomicOr(&lflag, 1u);
-            const Xfe q = x_scale(x_inv(diff), wi);
+        // the lane's points two at a time with one inversion (Montgomery's trick: 1/d0 = d1 / (d0 d1));
+        // a zero difference (t on the domain: the proof is rejected either way) takes the one-at-a-time
+        // form, so num / den are those of the reference's per-point inverses in every case
+        auto term = [&](uint32_t i, uint64_t w, Xfe inv) {
+            const Xfe q = x_scale(inv, w);
             num = x_add(num, x_mul(q, ld_xfe_canon(words, d.last_cw_off + 3ull * i)));
             den = x_add(den, q);
+        };
+        uint32_t i = tid;
+        for (; i + blockDim.x < L; i += 2 * blockDim.x) {
+            const uint64_t w1 = mont_mul(wi, wstep);
+            const Xfe d0 = x_sub(t, x_lift(wi)), d1 = x_sub(t, x_lift(w1));
+            const Xfe pr = x_mul(d0, d1);
+            if (x_is_zero(pr)) {
+                atomicOr(&lflag, 1u);
+                term(i, wi, x_inv(d0));
+                term(i + blockDim.x, w1, x_inv(d1));
+            } else {
+                const Xfe inv = x_inv(pr);
+                term(i, wi, x_mul(inv, d1));
+                term(i + blockDim.x, w1, x_mul(inv, d0));
+            }
+            wi = mont_mul(w1, wstep);
+        }
+        if (i < L) {
+            const Xfe diff = x_sub(t, x_lift(wi));
+            if (x_is_zero(diff)) atomicOr(&lflag, 1u);
+            term(i, wi, x_inv(diff));
         }
     }
     const Xfe snum = block_sum_xfe(num, red);
