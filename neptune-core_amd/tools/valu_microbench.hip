@@ -101,6 +101,47 @@ K32(k_subb_e32, "v_subb_co_u32_e32 %0, vcc, %1, %0, vcc")
 K32(k_subbrev_e32, "v_subbrev_co_u32_e32 %0, vcc, 0, %0, vcc")
 K64(k_mov64, "v_mov_b64 %0, %1")
 K64(k_lshl64, "v_lshlrev_b64 %0, 3, %0")
+#define K32Q(NAME, ASM)                                                                 \
+    __global__ void NAME(uint32_t* out, uint32_t s) {                                   \
+        uint32_t r[8]; uint32_t a = threadIdx.x * 0x01010101u + 7u;                     \
+        for (int k = 0; k < 8; ++k) r[k] = threadIdx.x + k;                             \
+        for (int i = 0; i < ITERS; ++i) {                                               \
+            _Pragma("unroll") for (int k = 0; k < 8; ++k) asm volatile(ASM : "+v"(r[k]) : "v"(a), "s"(s)); \
+        }                                                                               \
+        uint32_t x = 0; for (int k = 0; k < 8; ++k) x ^= r[k];                          \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = x;                                 \
+    }
+#define K64CS(NAME, ASM)                                                                \
+    __global__ void NAME(uint32_t* out, uint32_t s) {                                   \
+        uint64_t r[8]; uint32_t a = threadIdx.x | 1u; uint64_t s64 = (uint64_t)s * 0x100000001ull; \
+        for (int k = 0; k < 8; ++k) r[k] = threadIdx.x + k;                             \
+        for (int i = 0; i < ITERS; ++i) {                                               \
+            _Pragma("unroll") for (int k = 0; k < 8; ++k) { uint64_t sd; asm volatile(ASM : "+v"(r[k]), "=s"(sd) : "v"(a), "s"(s), "s"(s64)); } \
+        }                                                                               \
+        uint32_t x = 0; for (int k = 0; k < 8; ++k) x ^= (uint32_t)r[k];                \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = x;                                 \
+    }
+K64CS(k_mad64_smul, "v_mad_u64_u32 %0, %1, %2, %3, %0")
+K64CS(k_mad64_sadd, "v_mad_u64_u32 %0, %1, %2, %2, %4")
+K64CS(k_mad64_cmul, "v_mad_u64_u32 %0, %1, %2, -1, %0")
+// third batch: does the operand kind (VGPR / inline constant / literal / SGPR) set the issue class?
+K32(k_lshl_v, "v_lshlrev_b32_e32 %0, %1, %0")
+K32(k_lshr_c, "v_lshrrev_b32_e32 %0, 3, %0")
+K32(k_add_c, "v_add_u32_e32 %0, 3, %0")
+K32(k_add_lit, "v_add_u32_e32 %0, 0x12345, %0")
+K32(k_and_lit, "v_and_b32_e32 %0, 0xff, %0")
+K32(k_and_c, "v_and_b32_e32 %0, 63, %0")
+K32Q(k_add_s, "v_add_u32_e64 %0, %2, %0")
+K32Q(k_xor_s, "v_xor_b32_e64 %0, %2, %0")
+K32(k_sub_c, "v_sub_u32_e32 %0, 7, %0")
+K32(k_mov_c, "v_mov_b32_e32 %0, 7")
+K32Q(k_mov_s, "v_mov_b32_e32 %0, %2")
+K32(k_lshr_v64, "v_lshrrev_b32_e64 %0, %1, %0")
+K32(k_lshl_v64, "v_lshlrev_b32_e64 %0, %1, %0")
+K32(k_bfe_v, "v_bfe_u32 %0, %0, %1, %1")
+K32(k_cndmask_v, "v_cndmask_b32_e64 %0, %1, %0, s[40:41]")
+K32(k_min_v, "v_min_u32_e32 %0, %1, %0")
+K32(k_not_v, "v_not_b32_e32 %0, %0")
 
 __global__ void k_ds_u8(uint32_t* out, uint32_t s) {
     __shared__ uint8_t lut[256];
@@ -150,6 +191,17 @@ int main() {
         {"v_lshrrev_b32_e32(vgpr)", k_lshr_e32, 8, 0}, {"v_max_u32_e32", k_max_e32, 8, 0},
         {"v_sub_co_u32_e32(vcc)", k_subco_e32, 8, 0}, {"v_subb_co_u32_e32 chain", k_subb_e32, 8, 0},
         {"v_subbrev_co_u32_e32 chain", k_subbrev_e32, 8, 0}, {"v_mov_b64", k_mov64, 8, 0},
+        {"v_mad_u64_u32(sgpr mul)", k_mad64_smul, 8, 0}, {"v_mad_u64_u32(sgpr addend)", k_mad64_sadd, 8, 0},
+        {"v_mad_u64_u32(const -1 mul)", k_mad64_cmul, 8, 0},
+        {"v_lshlrev_b32_e32(vgpr)", k_lshl_v, 8, 0}, {"v_lshrrev_b32_e32(const)", k_lshr_c, 8, 0},
+        {"v_add_u32_e32(const)", k_add_c, 8, 0}, {"v_add_u32_e32(literal)", k_add_lit, 8, 0},
+        {"v_and_b32_e32(literal 0xff)", k_and_lit, 8, 0}, {"v_and_b32_e32(const 63)", k_and_c, 8, 0},
+        {"v_add_u32_e64(sgpr)", k_add_s, 8, 0}, {"v_xor_b32_e64(sgpr)", k_xor_s, 8, 0},
+        {"v_sub_u32_e32(const)", k_sub_c, 8, 0}, {"v_mov_b32_e32(const)", k_mov_c, 8, 0},
+        {"v_mov_b32_e32(sgpr)", k_mov_s, 8, 0}, {"v_lshrrev_b32_e64(vgpr)", k_lshr_v64, 8, 0},
+        {"v_lshlrev_b32_e64(vgpr)", k_lshl_v64, 8, 0}, {"v_bfe_u32(vgpr)", k_bfe_v, 8, 0},
+        {"v_cndmask_b32_e64(vgpr,s40)", k_cndmask_v, 8, 0}, {"v_min_u32_e32", k_min_v, 8, 0},
+        {"v_not_b32_e32", k_not_v, 8, 0},
         {"ds_read_u8 256B (+3 valu)", k_ds_u8, 8, 0}, {"ds_read_u16 128KiB (+3 valu)", k_ds_u16_128k, 8, 131072}};
     hipEvent_t a, b; CHECK(hipEventCreate(&a)); CHECK(hipEventCreate(&b));
     CHECK(hipFuncSetAttribute((const void*)k_ds_u16_128k, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
