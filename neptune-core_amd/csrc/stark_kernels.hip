@@ -637,10 +637,11 @@ __device__ __forceinline__ void lcw_node(const uint64_t* __restrict__ words, con
     }
 }
 
-// at least 5 waves per SIMD (<= 96 VGPRs): the FixedLength permutation's separate round 0 would
-// otherwise take the kernel to 109 VGPRs and 4 waves
+// 6 waves per SIMD (<= 80 VGPRs): with hash_pair's MDS finished two outputs at a time
+// (NHIP_PAIR_MDS_GROUP) the kernel needs 77 VGPRs and no scratch (5 waves and a 20-byte spill before,
+// 109 VGPRs unconstrained).  Config 4 +1.1-1.4% at 4,096 proofs, +2.3-3.4% at 512 (profiles/r03x).
 #ifndef NHIP_MP_WAVES
-#define NHIP_MP_WAVES 5
+#define NHIP_MP_WAVES 6
 #endif
 __global__ void __launch_bounds__(256, NHIP_MP_WAVES) k_mp_hash(const uint64_t* __restrict__ words, const uint64_t* __restrict__ dig,
                                                  MpPlan plan, uint32_t lvl, uint32_t mp_blocks,

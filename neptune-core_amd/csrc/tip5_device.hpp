@@ -315,19 +315,14 @@ __device__ __forceinline__ void mds_fold4(const uint32_t* sh, const uint64_t* sl
 // [OBEG, OEND) != [0, 16): only those outputs are computed (a digest read after the last round,
 // or the capacity words a sponge keeps when the next absorb overwrites the rate).
 __device__ __forceinline__ uint64_t mds_reduce_fold(uint64_t al, uint64_t ah);
-template <int NIN, int OBEG = 0, int OEND = 16>
-__device__ __forceinline__ void mds_ark_fold(uint64_t s[16], const uint64_t* __restrict__ rck) {
-    constexpr int NOUT = OEND - OBEG;
-    uint32_t lo[NIN], hi[NIN];
+// Outputs I0 .. I0 + N of the folded MDS (accumulate, then reduce four words at a time).
+template <int NIN, int I0, int N>
+__device__ __forceinline__ void mds_fold_outputs(const uint32_t* lo, const uint32_t* hi,
+                                                 const uint64_t* __restrict__ rck, uint64_t* out) {
+    uint64_t al[N], ah[N];
 #pragma unroll
-    for (int j = 0; j < NIN; ++j) {
-        lo[j] = (uint32_t)s[j];
-        hi[j] = (uint32_t)(s[j] >> 32);
-    }
-    uint64_t al[NOUT], ah[NOUT];
-#pragma unroll
-    for (int o = 0; o < NOUT; ++o) {
-        const int i = OBEG + o;
+    for (int o = 0; o < N; ++o) {
+        const int i = I0 + o;
         al[o] = rck[i];  // < 2^64 - 2^52 for every Tip5 constant: al never overflows
         ah[o] = 0;
 #pragma unroll
@@ -337,7 +332,7 @@ __device__ __forceinline__ void mds_ark_fold(uint64_t s[16], const uint64_t* __r
             ah[o] += c * hi[j];
         }
     }
-    constexpr int N4 = NOUT & ~3;
+    constexpr int N4 = N & ~3;
     uint32_t sh[N4 > 0 ? N4 : 1];
     uint64_t slo[N4 > 0 ? N4 : 1], w[N4 > 0 ? N4 : 1];
     uint32_t e[N4 > 0 ? N4 : 1];
@@ -351,11 +346,46 @@ __device__ __forceinline__ void mds_ark_fold(uint64_t s[16], const uint64_t* __r
 #pragma unroll
     for (int o = 0; o < N4; o += 4) mds_fold4(sh + o, slo + o, w + o, e + o);
 #pragma unroll
-    for (int o = 0; o < N4; ++o) s[OBEG + o] = w[o] - e[o];
+    for (int o = 0; o < N4; ++o) out[o] = w[o] - e[o];
 #pragma unroll
-    for (int o = N4; o < NOUT; ++o) s[OBEG + o] = mds_reduce_fold(al[o], ah[o]);
+    for (int o = N4; o < N; ++o) out[o] = mds_reduce_fold(al[o], ah[o]);
 }
 
+// G < 16: the outputs are finished G at a time, a scheduling barrier between groups, so that only
+// one group's accumulators are live (fewer VGPRs at the MDS peak).  NHIP_PAIR_MDS_GROUP: hash_pair
+// (the Merkle level kernels); NHIP_SPONGE_MDS_GROUP: the sponge permutations (row hashing).
+#ifndef NHIP_PAIR_MDS_GROUP
+#define NHIP_PAIR_MDS_GROUP 2
+#endif
+#ifndef NHIP_SPONGE_MDS_GROUP
+#define NHIP_SPONGE_MDS_GROUP 16
+#endif
+template <int NIN, int OBEG, int OEND, int G>
+__device__ __forceinline__ void mds_fold_groups(const uint32_t* lo, const uint32_t* hi,
+                                                const uint64_t* __restrict__ rck, uint64_t* out) {
+    constexpr int N = (OEND - OBEG) < G ? (OEND - OBEG) : G;
+    mds_fold_outputs<NIN, OBEG, N>(lo, hi, rck, out);
+    if constexpr (OBEG + N < OEND) {
+        __builtin_amdgcn_sched_barrier(0);
+        mds_fold_groups<NIN, OBEG + N, OEND, G>(lo, hi, rck, out + N);
+    }
+}
+
+template <int NIN, int OBEG = 0, int OEND = 16, int G = 16>
+__device__ __forceinline__ void mds_ark_fold(uint64_t s[16], const uint64_t* __restrict__ rck) {
+    uint32_t lo[NIN], hi[NIN];
+#pragma unroll
+    for (int j = 0; j < NIN; ++j) {
+        lo[j] = (uint32_t)s[j];
+        hi[j] = (uint32_t)(s[j] >> 32);
+    }
+    uint64_t out[OEND - OBEG];
+    mds_fold_groups<NIN, OBEG, OEND, G>(lo, hi, rck, out);
+#pragma unroll
+    for (int o = 0; o < OEND - OBEG; ++o) s[OBEG + o] = out[o];
+}
+
+template <int G = NHIP_SPONGE_MDS_GROUP>
 __device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restrict__ rc,
                                         const uint64_t* __restrict__ rck) {
 #ifdef NHIP_MDS_CARRY
@@ -363,7 +393,7 @@ __device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restri
     mds_ark_carry(s, rc);
 #else
     (void)rc;
-    mds_ark_fold<16>(s, rck);
+    mds_ark_fold<16, 0, 16, G>(s, rck);
 #endif
 }
 
@@ -420,20 +450,20 @@ __device__ __forceinline__ void tip5_hash_pair_digest(uint64_t s[16], const uint
         pow7_mul<3>(s + g, x2, x3);
         pow7_mul<3>(x3, x4, s + g);
     }
-    mds_ark_fold<10>(s, c_tip5_rck0_fixed);
+    mds_ark_fold<10, 0, 16, NHIP_PAIR_MDS_GROUP>(s, c_tip5_rck0_fixed);
 #pragma unroll 1
     for (int r = 1; r < TIP5_ROUNDS - 1; ++r) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
         pow7_12(s + 4);
-        mds_ark(s, c_tip5_rc_raw + r * 16, c_tip5_rck_raw + r * 16);
+        mds_ark<NHIP_PAIR_MDS_GROUP>(s, c_tip5_rc_raw + r * 16, c_tip5_rck_raw + r * 16);
     }
     // last round: the caller reads the digest s[0..5] only, so the MDS computes those 5 outputs
     // (11 x 16 x 2 multiply-adds and 11 reductions fewer); s[5..16] are left stale
 #pragma unroll
     for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
     pow7_12(s + 4);
-    mds_ark_fold<16, 0, 5>(s, c_tip5_rck_raw + (TIP5_ROUNDS - 1) * 16);
+    mds_ark_fold<16, 0, 5, NHIP_PAIR_MDS_GROUP>(s, c_tip5_rck_raw + (TIP5_ROUNDS - 1) * 16);
 }
 
 // Rounds 0..3 of the permutation, then the last round computing only the state words
@@ -454,7 +484,7 @@ __device__ __forceinline__ void tip5_last_round(uint64_t s[16], const uint8_t* _
 #pragma unroll
     for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
     pow7_12(s + 4);
-    mds_ark_fold<16, OBEG, OEND>(s, c_tip5_rck_raw + (TIP5_ROUNDS - 1) * 16);
+    mds_ark_fold<16, OBEG, OEND, NHIP_SPONGE_MDS_GROUP>(s, c_tip5_rck_raw + (TIP5_ROUNDS - 1) * 16);
 }
 
 }  // namespace nhip

@@ -18,6 +18,9 @@
 #ifndef NHIP_MINWAVES
 #define NHIP_MINWAVES 1  // min waves per SIMD requested from the register allocator
 #endif
+#ifndef NHIP_PAIR_WAVES
+#define NHIP_PAIR_WAVES 6  // the hash_pair-only kernels (80 VGPRs with the MDS finished in pairs)
+#endif
 
 namespace nhip {
 
@@ -44,7 +47,7 @@ __global__ void __launch_bounds__(256, NHIP_MINWAVES) k_permutation(uint64_t* __
     }
 }
 
-__global__ void __launch_bounds__(256, NHIP_MINWAVES) k_hash_pair(const uint64_t* __restrict__ left, const uint64_t* __restrict__ right,
+__global__ void __launch_bounds__(256, NHIP_PAIR_WAVES) k_hash_pair(const uint64_t* __restrict__ left, const uint64_t* __restrict__ right,
                                                    uint64_t* __restrict__ out, size_t n) {
     __shared__ Tip5Lds lds;
     tip5_lds_init(lds);
@@ -85,7 +88,7 @@ __global__ void __launch_bounds__(256, NHIP_MINWAVES) k_hash_varlen(const uint64
     }
 }
 
-__global__ void __launch_bounds__(256, NHIP_MINWAVES) k_mtree_level(const uint64_t* __restrict__ children, uint64_t* __restrict__ parents,
+__global__ void __launch_bounds__(256, NHIP_PAIR_WAVES) k_mtree_level(const uint64_t* __restrict__ children, uint64_t* __restrict__ parents,
                                                      size_t n_parents) {
     __shared__ Tip5Lds lds;
     tip5_lds_init(lds);
@@ -99,7 +102,7 @@ __global__ void __launch_bounds__(256, NHIP_MINWAVES) k_mtree_level(const uint64
     }
 }
 
-__global__ void __launch_bounds__(256, NHIP_MINWAVES) k_mtree_verify(const uint64_t* __restrict__ roots, int per_path_root,
+__global__ void __launch_bounds__(256, NHIP_PAIR_WAVES) k_mtree_verify(const uint64_t* __restrict__ roots, int per_path_root,
                                                       const uint64_t* __restrict__ indices,
                                                       const uint64_t* __restrict__ leaves,
                                                       const uint64_t* __restrict__ paths, uint32_t depth, size_t n,
