@@ -291,10 +291,13 @@ __global__ void __launch_bounds__(1024) k_fs_replay_quad(const uint64_t* __restr
 
 // ------------------------------------------------------------------ revealed-row hashing
 // grid.y = 0 main, 1 aux, 2 quotient; one lane per (proof, row).
+// 5 waves per SIMD: 84 VGPRs, no scratch, with the sponge MDS finished four outputs at a time and
+// the last round branching on its MDS only (122-128 VGPRs and 4 waves before): config 4 equal at
+// 4,096 proofs, +3.5-5% at 512 (profiles/r03za; 6 waves with pairs: -0.7% at 4,096)
 #ifndef NHIP_ROWS_WAVES
-#define NHIP_ROWS_WAVES
+#define NHIP_ROWS_WAVES 5
 #endif
-__global__ void __launch_bounds__(256) NHIP_ROWS_WAVES k_hash_rows(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+__global__ void __launch_bounds__(256, NHIP_ROWS_WAVES) k_hash_rows(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                                    uint32_t n_proofs, uint32_t k, StarkDims dims,
                                                    uint64_t* __restrict__ dig, const uint32_t* __restrict__ fail) {
     __shared__ Tip5Lds lds;
@@ -331,8 +334,9 @@ __global__ void __launch_bounds__(256) NHIP_ROWS_WAVES k_hash_rows(const uint64_
                 }
             }
             tip5_rounds_0_3(s, lds.lut);
-            if (!last) tip5_last_round<10, 16>(s, lds.lut);
-            else tip5_last_round<0, 5>(s, lds.lut);
+            tip5_last_sbox(s, lds.lut);
+            if (!last) tip5_last_mds<10, 16>(s);
+            else tip5_last_mds<0, 5>(s);
         }
         uint64_t* __restrict__ o = dig + (((uint64_t)p * 3 + tree) * k + j) * 5;
 #pragma unroll

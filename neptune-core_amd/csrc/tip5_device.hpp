@@ -358,7 +358,7 @@ __device__ __forceinline__ void mds_fold_outputs(const uint32_t* lo, const uint3
 #define NHIP_PAIR_MDS_GROUP 2
 #endif
 #ifndef NHIP_SPONGE_MDS_GROUP
-#define NHIP_SPONGE_MDS_GROUP 16
+#define NHIP_SPONGE_MDS_GROUP 4
 #endif
 template <int NIN, int OBEG, int OEND, int G>
 __device__ __forceinline__ void mds_fold_groups(const uint32_t* lo, const uint32_t* hi,
@@ -479,12 +479,22 @@ __device__ __forceinline__ void tip5_rounds_0_3(uint64_t s[16], const uint8_t* _
         mds_ark(s, c_tip5_rc_raw + r * 16, c_tip5_rck_raw + r * 16);
     }
 }
-template <int OBEG, int OEND>
-__device__ __forceinline__ void tip5_last_round(uint64_t s[16], const uint8_t* __restrict__ lut) {
+// The last round's S-box layer; the caller then keeps the MDS outputs it needs
+// (tip5_last_mds<OBEG, OEND>).  A caller choosing between two output ranges at run time branches on
+// the MDS only: with the whole last round in each branch the row kernel needed ~40 more VGPRs.
+__device__ __forceinline__ void tip5_last_sbox(uint64_t s[16], const uint8_t* __restrict__ lut) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) s[i] = split_and_lookup(lut, s[i]);
     pow7_12(s + 4);
+}
+template <int OBEG, int OEND>
+__device__ __forceinline__ void tip5_last_mds(uint64_t s[16]) {
     mds_ark_fold<16, OBEG, OEND, NHIP_SPONGE_MDS_GROUP>(s, c_tip5_rck_raw + (TIP5_ROUNDS - 1) * 16);
+}
+template <int OBEG, int OEND>
+__device__ __forceinline__ void tip5_last_round(uint64_t s[16], const uint8_t* __restrict__ lut) {
+    tip5_last_sbox(s, lut);
+    tip5_last_mds<OBEG, OEND>(s);
 }
 
 }  // namespace nhip
