@@ -1504,7 +1504,13 @@ __device__ __forceinline__ uint64_t wl_reduce(const uint64_t (&a)[6]) {
     return gl_add(ur, reduce96(wr << 32, (uint32_t)(wr >> 32)));  // + wr * 2^32
 }
 
-__global__ void __launch_bounds__(256) k_deep_rows8(const uint64_t* __restrict__ words,
+// 6 waves per SIMD (80 VGPRs with a 64-byte spill; 127 VGPRs and 4 waves unconstrained): the
+// kernel waits on its row loads, and more waves cover the wait: config 4 +0.9% at 4,096 proofs,
+// 512 equal (profiles/r03zc; 5 waves +0.5%)
+#ifndef NHIP_DEEP_WAVES
+#define NHIP_DEEP_WAVES 6
+#endif
+__global__ void __launch_bounds__(256, NHIP_DEEP_WAVES) k_deep_rows8(const uint64_t* __restrict__ words,
                                                     const ProofDesc* __restrict__ desc, uint32_t n_proofs,
                                                     StarkDims dims, const uint64_t* __restrict__ xs,
                                                     const uint64_t* __restrict__ xdom,
