@@ -1031,8 +1031,11 @@ __device__ Xfe eval_terminal_wave(uint32_t n, Xfe c, Sym sym) {
 // stores the OOD linear combinations used by DEEP: [sum w*curr row, sum w*next row, sum w*segs].
 // BLOCK = 256 for batches that fill the GPU (the hashing needs the wave slots); 1,024 for small ones
 // (OOD_WIDE_MAX_PROOFS), where one proof's evaluation is on the critical path and the CUs are idle.
+#ifndef NHIP_OOD_WAVES
+#define NHIP_OOD_WAVES 1
+#endif
 template <uint32_t BLOCK>
-__global__ void __launch_bounds__(BLOCK) k_ood_air(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+__global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_ood_air(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                                  uint32_t n_proofs, StarkDims dims, const OodIns* __restrict__ prog,
                                                  const uint32_t* __restrict__ prog_off, uint32_t n_levels,
                                                  const Xfe* __restrict__ consts, uint4 cons_type_off,
@@ -1186,7 +1189,10 @@ __device__ __forceinline__ uint64_t lds_pow(const uint64_t* __restrict__ sq, uin
     return r;
 }
 
-__global__ void __launch_bounds__(256) k_fri(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+#ifndef NHIP_FRI_WAVES
+#define NHIP_FRI_WAVES 1
+#endif
+__global__ void __launch_bounds__(256, NHIP_FRI_WAVES) k_fri(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                              uint32_t n_proofs, StarkDims dims, const uint64_t* __restrict__ xs,
                                              const uint32_t* __restrict__ idx_all, uint64_t* __restrict__ xdom,
                                              uint32_t* __restrict__ fail) {
