@@ -18,7 +18,9 @@ MERKLE = ("k_mp_hash", "k_mp_hash_wide", "k_mp_hash_tail", "k_mp_climb")
 
 def kname(full):
     full = full.replace("(anonymous namespace)::", "")
-    return full.split("(")[0]
+    full = full.split("(")[0]
+    # template instances (k_mp_hash<6>, k_mp_hash<7>) count as their kernel for the Merkle roofline
+    return full.split("<")[0] if full.split("<")[0].endswith(MERKLE) else full
 
 
 def frac_of(rf, avg_ms):
