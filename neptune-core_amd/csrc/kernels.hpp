@@ -62,6 +62,10 @@ static constexpr uint32_t FS_PAIR_MAX_PROOFS = 512;
 // workgroups -7 to -9% at every size, 512 / 1,024 threads -1 to -25% (profiles/r03g, 2 repetitions)
 static constexpr uint32_t FS_QUAD_MIN_PROOFS = 2048;
 static constexpr uint32_t FS_QUAD_WG = 256;  // k_fs_replay_quad workgroup size
+// batches below this many proofs hash their Merkle levels with the 7-wave k_mp_hash instance, larger
+// ones with the 6-wave one; NHIP_MP_SMALL_MAX overrides (A/B runs).  7 waves: 2,048 proofs +1.3%,
+// 1,024 +1.2%, 512 +3%; 4,096 -0.6% (profiles/r03ze, r03zf)
+static constexpr uint32_t MP_SMALL_MAX_PROOFS = 4096;
 static constexpr uint32_t OOD_WIDE_MAX_PROOFS = 64;  // k_ood_air<1024> up to this many proofs per batch
 struct MpRoot {
     uint64_t code;  // source code of the tree's final node, ~0 = no check (skipped or already failed)

@@ -644,10 +644,16 @@ __device__ __forceinline__ void lcw_node(const uint64_t* __restrict__ words, con
 // 6 waves per SIMD (<= 80 VGPRs): with hash_pair's MDS finished two outputs at a time
 // (NHIP_PAIR_MDS_GROUP) the kernel needs 77 VGPRs and no scratch (5 waves and a 20-byte spill before,
 // 109 VGPRs unconstrained).  Config 4 +1.1-1.4% at 4,096 proofs, +2.3-3.4% at 512 (profiles/r03x).
+// Batches below MP_SMALL_MAX_PROOFS (kernels.hpp) launch the 7-wave instance (72 VGPRs, a 24-byte
+// spill): 512 to 2,048 proofs +1.2-4.3%, 4,096 proofs -0.6% (profiles/r03ze, r03zf).
 #ifndef NHIP_MP_WAVES
 #define NHIP_MP_WAVES 6
 #endif
-__global__ void __launch_bounds__(256, NHIP_MP_WAVES) k_mp_hash(const uint64_t* __restrict__ words, const uint64_t* __restrict__ dig,
+#ifndef NHIP_MP_WAVES_SMALL
+#define NHIP_MP_WAVES_SMALL 7
+#endif
+template <int WAVES>
+__global__ void __launch_bounds__(256, WAVES) k_mp_hash(const uint64_t* __restrict__ words, const uint64_t* __restrict__ dig,
                                                  MpPlan plan, uint32_t lvl, uint32_t mp_blocks,
                                                  const ProofDesc* __restrict__ desc, uint32_t n_proofs,
                                                  const uint32_t* __restrict__ fail, LcwTree lcw) {
@@ -1822,6 +1828,10 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     const LcwTree lcw{b.lcw, b.max_lcw};
     const uint32_t log2_lcw = 31 - __builtin_clz(b.max_lcw);
     const uint32_t hash_levels = b.mp.levels > log2_lcw ? b.mp.levels : log2_lcw;
+    static const uint32_t mp_small_max = [] {
+        const char* v = std::getenv("NHIP_MP_SMALL_MAX");
+        return v ? (uint32_t)std::strtoul(v, nullptr, 10) : MP_SMALL_MAX_PROOFS;
+    }();
     // first level of the tail climbed in one launch (every level from it on is small)
     uint32_t tail0 = hash_levels;
     while (tail0 > 0 && hash_levels - tail0 < MP_TAIL_LEVELS_MAX) {
@@ -1858,9 +1868,12 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         if (wide)
             hipExtLaunchKernelGGL(k_mp_hash_wide, dim3((unsigned)(((cap + per * n) * 16 + 255) / 256)), dim3(256), 0,
                                   st, e0, e1, 0, b.words, b.dig, b.mp, l, cap, b.desc, n, (const uint32_t*)b.fail, lcw);
+        else if (n < mp_small_max)
+            hipExtLaunchKernelGGL(k_mp_hash<NHIP_MP_WAVES_SMALL>, dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0,
+                                  e1, 0, b.words, b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw);
         else
-            hipExtLaunchKernelGGL(k_mp_hash, dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0, e1, 0, b.words,
-                                  b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw);
+            hipExtLaunchKernelGGL(k_mp_hash<NHIP_MP_WAVES>, dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0, e1, 0,
+                                  b.words, b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw);
         ++launches;
     }
     if (!aux_started) launch_aux_chain();
