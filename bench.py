@@ -25,15 +25,27 @@ default 4 hardware queues per process, so GPU_MAX_HW_QUEUES is raised here befor
 unset.
 The default timed region is 200 steps (~2 s of sustained load).
 
+Defaults (round 4): the AIR is the synthetic constraints bloated to triton-air's size class
+(--air triton-size, ~21.7k nodes: the OOD work timed is at least the reference's), and the proof /
+claim words are given as twenty-first's in-memory Montgomery words (--input-form montgomery: the
+form the Rust drop-in hands over without a copy; converted on the host before anything is timed).
+
 Beside `value` (HBM-resident input, the contract):
+  roofline: the dominant kernel, the per-level Merkle hash launches (k_mp_hash), as Tip5 VALU
+    lane-ops/s against the gfx950 VALU peak, from its launches in steps run one at a time right
+    after the timed region (the kernel's own rate: launches x average <= step time).
+    roofline.inflight: the same launches inside the timed region, where launches of the steps in
+    flight overlap each other and the other kernels (labelled, not the kernel's rate).
   pcie_inclusive: the same batch arriving from host memory (pinned, DMA'd per refill, two batches
     alternating) with the host-to-device link's measured ceiling; never `value`.
-  roofline: the dominant kernel, the per-level Merkle hash launches (k_mp_hash), as Tip5 VALU
-    lane-ops/s against the gfx950 VALU peak over the timed region.
+  group_stream: the same batches through the in-process multi-GPU form neptune-core uses
+    (nhip_group_stream over every GPU of the job from rank 0, from pinned host memory).
   tip5_paths: the config-2 Tip5 path microbench.
   cpu_baseline: the C restatement of the verifier (oracle/stark_oracle.c), one proof per host thread,
     over a bounded sample of this batch's proofs (the reference, Rust triton-vm, cannot be built here).
-  hw_queues_4: the same workload in a child process at HIP's default 4 hardware queues.
+  hw_queues_4 (opt-in, --hwq4-steps): the same workload in a child process at HIP's default 4
+    hardware queues (never under a profiler: the child would be started from a process whose GPU
+    the profiler's library has already initialised).
   config1_latency: BASELINE config 1's single-proof latency (log2-21 substitute): GPU resident and
     from host memory, beside the C restatement on ONE host thread.
   roofline.traffic / valu_issue / hbm.pmc_*: from the committed rocprofv3 PMC passes of
@@ -63,6 +75,9 @@ COLLECTION_HEIGHTS = [16, 10, 11, 12, 12, 11, 9, 9]
 # Algorithmic VALU work of one Tip5 permutation in 32-bit VALU lane-ops: a fixed analytic count of
 # a minimal implementation: per round S-box 64 + x^7 672 + MDS 512+160 + ARK 96.
 TIP5_VALU_OPS_PER_PERM = 5 * 1504
+# VALU instructions a hash_pair permutation needs in the kernel's form (round 0 without the constant
+# capacity's x^7 and MDS terms, the last round's 5 digest outputs only: DESIGN.md §3)
+PAIR_HASH_VALU_OPS = 6070
 # gfx950: 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz (wave64 VALU issues over 2 cycles on SIMD-32)
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
 
@@ -84,19 +99,25 @@ def lib_sha256(path: str = LIB_PATH) -> str:
     return hashlib.sha256(open(path, "rb").read()).hexdigest()
 
 
+WORKLOAD = {"air": "triton-size", "input_form": "montgomery"}  # set by main() from the arguments
+
+
 def latest_profile(config: int, proofs: int):
-    """profiles/LATEST = '<tag> <config> <proofs per GPU>': the committed rocprofv3 PMC passes and
-    the workload they were taken on (none for another config or per-GPU batch size: the PMC
-    figures are per step of that workload).  The passes count only for the library they were taken
-    with: profiles/<tag>/LIB_SHA256 must equal the hash of the library this run loads, else the
-    counters belong to another binary and are not attached."""
+    """profiles/LATEST = '<tag> <config> <proofs per GPU> [<air> <input form>]': the committed
+    rocprofv3 PMC passes and the workload they were taken on (none for another config, per-GPU batch
+    size, AIR or input form: the PMC figures are per step of that workload; a line without the last
+    two fields is the synthetic AIR, canonical input).  The passes count only for the library they
+    were taken with: profiles/<tag>/LIB_SHA256 must equal the hash of the library this run loads,
+    else the counters belong to another binary and are not attached."""
     try:
         parts = open(os.path.join(ROOT, "profiles", "LATEST")).read().split()
     except OSError:
         return None
     tag, cfg = parts[0], int(parts[1]) if len(parts) > 1 else 3
     n = int(parts[2]) if len(parts) > 2 else None
-    if cfg != config or n not in (None, proofs):
+    air = parts[3] if len(parts) > 3 else "synthetic"
+    form = parts[4] if len(parts) > 4 else "canonical"
+    if cfg != config or n not in (None, proofs) or (air, form) != (WORKLOAD["air"], WORKLOAD["input_form"]):
         return None
     try:
         want = open(os.path.join(ROOT, "profiles", tag, "LIB_SHA256")).read().split()[0]
@@ -144,6 +165,34 @@ def pmc_valu_per_step(config: int, proofs: int):
         return (tot / steps, tag) if steps else (None, None)
     except (OSError, KeyError):
         return None, None
+
+
+def pmc_mp_valu_per_launch(config: int, proofs: int):
+    """Wave-level VALU instructions of the Merkle level hash launches (k_mp_hash*, the roofline's
+    kernel) per step, from the latest committed PMC pass; None when absent."""
+    import csv
+    tag = latest_profile(config, proofs)
+    if tag is None:
+        return None, None
+    try:
+        tot, steps = 0.0, 0
+        for r in csv.DictReader(open(os.path.join(ROOT, "profiles", tag, "pmc_valu_counter_collection.csv"))):
+            k = r["Kernel_Name"]
+            if r["Counter_Name"] != "SQ_INSTS_VALU":
+                continue
+            if "k_mp_hash" in k or "k_mp_climb" in k:
+                tot += float(r["Counter_Value"])
+            steps += "k_hash_rows" in k
+        return (tot / steps, tag) if steps else (None, None)
+    except (OSError, KeyError):
+        return None, None
+
+
+def under_profiler() -> bool:
+    """rocprofv3 runs this process with its tool library preloaded (it initialises the GPU before
+    bench.py starts): no child process may then be started from here."""
+    pre = os.environ.get("LD_PRELOAD", "") + os.environ.get("HSA_TOOLS_LIB", "")
+    return "rocprof" in pre or any(k.startswith("ROCPROF") for k in os.environ)
 
 
 def pmc_bytes_per_step(config: int, proofs: int):
@@ -388,8 +437,9 @@ def config1_latency(ctx, gair, stark, air_words, cpu_seconds: float, reps: int =
     import neptune_hip.stark as NS
     import stark_ref as S
     claim, proof = config1_case(air_words)
-    ncl = NS.Claim(*claim)
-    b = NS.Batch(ctx, gair, stark, [ncl], [proof])
+    dcl, dpr = device_form([claim], [proof], stark.input_form == 1)
+    ncl, dproof = NS.Claim(*dcl[0]), dpr[0]
+    b = NS.Batch(ctx, gair, stark, [ncl], [dproof])
     for _ in range(5):
         v, _ = b.run()
     res_ms = []
@@ -402,7 +452,7 @@ def config1_latency(ctx, gair, stark, air_words, cpu_seconds: float, reps: int =
     host_ms = []
     for _ in range(max(5, reps // 5)):
         t = time.perf_counter()
-        ok = NS.verify_batch(ctx, gair, stark, [(ncl, proof)]) == [True] and ok
+        ok = NS.verify_batch(ctx, gair, stark, [(ncl, dproof)]) == [True] and ok
         host_ms.append((time.perf_counter() - t) * 1e3)
     args = C.stark_batch_args(air_words, S.StarkParams(), [claim], [proof])
     ok = bool(C.stark_verify_args(args, 1)[0]) and ok  # warm, and the oracle's verdict
@@ -522,6 +572,63 @@ def pcie_stream(ctx, gair, stark, claims, proofs, expect, batches: int):
             "measured": f"{batches} batches from pinned host memory, 2 alternating (refill overlaps the other's run)"}
 
 
+def device_form(claims, proofs, mont: bool):
+    """(claims, proofs) in the input form the library is given: unchanged, or as twenty-first's
+    Montgomery words (each distinct proof array converted once: config 4 reuses 256 pool proofs)."""
+    if not mont:
+        return claims, proofs
+    from neptune_hip.stark import to_montgomery
+    seen = {}
+
+    def conv(p):
+        k = id(p)
+        if k not in seen:
+            seen[k] = (p, to_montgomery(p))
+        return seen[k][1]
+
+    def words(v):
+        return [int(x) for x in to_montgomery(list(v))] if len(v) else []
+
+    return [(words(c[0]), c[1], words(c[2]), words(c[3])) for c in claims], [conv(p) for p in proofs]
+
+
+def group_stream(devices, air_words, stark, claims, proofs, expect, batches: int):
+    """The in-process multi-GPU form neptune-core runs: ONE process driving every GPU through
+    nhip_group_stream (GpuNode::verify_stream in the Rust crate).  The job's whole batch is submitted
+    `batches` times from pinned host memory; each member's share of batch k is staged and uploaded
+    while its share of batch k - 1 runs, the members in parallel.  Two warm submissions first (each
+    member's two device batches are allocated on first use)."""
+    import neptune_hip.stark as NS
+    pinned = NS.PinnedProofs(proofs)
+    ncl = [NS.Claim(*c) for c in claims]
+    m = NS.marshal(ncl, pinned.views)
+    gair = NS.Air([int(w) for w in air_words])
+    want = [bool(x) for x in expect]
+    ok = True
+    with NS.Group(list(devices)) as g, NS.GroupStream(g, gair, stark) as st:
+        for _ in range(2):
+            st.submit_marshalled(m)
+        ok = st.finish()[0] == want
+        st0 = st.stats()
+        t = time.perf_counter()
+        for _ in range(batches):
+            r = st.submit_marshalled(m)
+            ok = ok and (r is None or r[0] == want)
+        ok = ok and st.finish()[0] == want
+        dt = time.perf_counter() - t
+        st1 = st.stats()
+    pinned.close()
+    nbytes = sum(len(p) for p in proofs) * 8
+    d = {k: (st1[k] - st0[k]) / batches for k in ("ms_stage", "ms_upload", "ms_device")}
+    return {"value": len(proofs) * batches / dt, "unit": "proofs/s", "gpus": len(devices), "batches": batches,
+            "proofs_per_batch": len(proofs), "h2d_GBps": nbytes * batches / dt / 1e9,
+            "per_batch_ms": {"wall": dt / batches * 1e3, "stage_sum_members": d["ms_stage"],
+                             "upload_wait_sum_members": d["ms_upload"], "device_sum_members": d["ms_device"]},
+            "verdicts_correct": ok,
+            "measured": f"{batches} submissions of the whole batch from pinned host memory through "
+                        f"nhip_group_stream over devices {list(devices)} (one process)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -539,18 +646,23 @@ def main():
     ap.add_argument("--corrupt-frac", type=float, default=0.05)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
-    ap.add_argument("--air", default="synthetic", choices=("synthetic", "triton-size"),
-                    help="AIR circuit: the pool's synthetic AIR (505 constraints, 3,151 nodes) or the same "
-                         "constraints bloated to triton-air's size class (~21.7k nodes, stark_ref.bloat_air; "
-                         "identically-zero extra terms, so the same proofs verify)")
+    ap.add_argument("--air", default="triton-size", choices=("synthetic", "triton-size"),
+                    help="AIR circuit: the same constraints bloated to triton-air's size class (default; ~21.7k "
+                         "nodes, stark_ref.bloat_air: identically-zero extra terms, so the same proofs verify) or the "
+                         "pool's synthetic AIR (505 constraints, 3,151 nodes)")
+    ap.add_argument("--input-form", default="montgomery", choices=("montgomery", "canonical"),
+                    help="how the proof / claim words reach the library: twenty-first's in-memory Montgomery "
+                         "words (default: what the Rust drop-in hands over, Proof.0 as it lies) or canonical values")
+    ap.add_argument("--group-batches", type=int, default=6,
+                    help="group_stream leg: submissions of the job's batch through nhip_group_stream over every GPU "
+                         "of the job from rank 0 (0 = skip)")
     ap.add_argument("--iso-steps", type=int, default=ISO_STEPS,
                     help="steps run one at a time after the timed region for roofline_isolated (0 = none: a "
                          "profiled run's kernel statistics then hold only in-flight steps)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--hwq4-steps", type=int, default=100,
-                    help="N = 1: also run the workload in a child process at HIP's default 4 hardware queues "
-                         "(GPU_MAX_HW_QUEUES=4, what a process gets that does not provision queues) and report it "
-                         "as hw_queues_4 (0 = skip)")
+    ap.add_argument("--hwq4-steps", type=int, default=0,
+                    help="N = 1, opt-in: also run the workload in a child process at HIP's default 4 hardware "
+                         "queues (GPU_MAX_HW_QUEUES=4) and report it as hw_queues_4; never under a profiler")
     ap.add_argument("--config1-seconds", type=float, default=8.0,
                     help="config-1 single-proof latency leg: CPU-restatement time budget (0 = skip the leg)")
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
@@ -569,12 +681,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
+    WORKLOAD.update(air=args.air, input_form=args.input_form)
+    if under_profiler():
+        args.hwq4_steps = 0  # no child process from a process the profiler has attached to the GPU
     air_words, pool = load_pool()
-    if args.air == "triton-size":
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import stark_ref as S  # AIR descriptor construction only (test-data generator)
-        air_words = np.asarray(S.bloat_air(S.AirCircuit.from_words([int(w) for w in air_words]), 24000).to_words(),
-                               dtype=np.uint64)
     sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
     shards = expect_all = None  # configs 4 / 5: per-proof verdicts are all-gathered every step
     if args.config == 3:
@@ -585,8 +695,7 @@ def main():
         t = time.time()
         pool4 = load_pool4()
         log(f"[rank {rank}] config-4 pool: {len(pool4['proofs'])} distinct proofs ({time.time() - t:.1f}s)")
-        if args.air == "synthetic":
-            air_words = pool4["air"]
+        air_words = pool4["air"]
         claims, proofs, expect, _, shards, expect_all = make_config4(pool4, total, 0.01, world, rank)
         if args.shuffle and world == 1:
             order = np.random.default_rng(0x5F).permutation(len(proofs))
@@ -596,6 +705,11 @@ def main():
     else:
         total = args.proofs or 64
         claims, proofs, expect, shards, expect_all = make_config5(air_words, total, args.log2_height, world, rank)
+    if args.air == "triton-size":
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import stark_ref as S  # AIR descriptor construction only (test-data generator)
+        air_words = np.asarray(S.bloat_air(S.AirCircuit.from_words([int(w) for w in air_words]), 24000).to_words(),
+                               dtype=np.uint64)
     n = len(proofs)
     R = args.inflight or default_inflight(n)
     # before anything initialises HIP (nothing above has)
@@ -611,7 +725,8 @@ def main():
         import subprocess
         cmd = [sys.executable, os.path.abspath(__file__), "--config", str(args.config), "--steps", str(args.hwq4_steps),
                "--warmup", str(min(args.warmup, 10)), "--no-cpu", "--paths-log2", "0", "--stream-batches", "0",
-               "--config1-seconds", "0", "--iso-steps", "0", "--hwq4-steps", "0", "--air", args.air]
+               "--config1-seconds", "0", "--iso-steps", "0", "--hwq4-steps", "0", "--air", args.air,
+               "--input-form", args.input_form, "--group-batches", "0"]
         if args.proofs:
             cmd += ["--proofs", str(args.proofs)]
         if args.inflight:
@@ -646,13 +761,17 @@ def main():
     import neptune_hip.stark as NS
     from neptune_hip import shard
 
+    mont = args.input_form == "montgomery"
+    # the words as the library gets them: a node holds its proofs as Vec<BFieldElement>, i.e. in
+    # Montgomery form already, so the conversion of these canonical test proofs is data preparation
+    dev_claims, dev_proofs = device_form(claims, proofs, mont)
     ctx = nh.Context(dev_index)
     t0 = time.time()
     gair = NS.Air([int(w) for w in air_words])
-    stark = NS.Stark.default()
-    ncl = [NS.Claim(*c) for c in claims]
+    stark = NS.Stark.default().montgomery() if mont else NS.Stark.default()
+    ncl = [NS.Claim(*c) for c in dev_claims]
     # R resident copies of the raw proof words (each step decodes them on the device again)
-    ring = [NS.Batch(ctx, gair, stark, ncl, proofs) for _ in range(R)]
+    ring = [NS.Batch(ctx, gair, stark, ncl, dev_proofs) for _ in range(R)]
     prep_s = time.time() - t0
     st0 = ring[0].stats()
     log(f"[rank {rank}] batch ready: {n} proofs x {R} resident copies, {st0['proof_words']} words, "
@@ -759,17 +878,19 @@ def main():
     perms = avg["tip5_perms_static"] + avg["tip5_perms_merkle"]
     step_ms = elapsed / K * 1e3
 
-    # roofline of the dominant kernel, the Merkle hash launches (k_mp_hash, + k_mp_hash_wide on the
-    # smallest levels): permutations per launch x the analytic VALU lane-ops per permutation / the
-    # average launch duration.  Each launch is timed by the HIP start / stop events of
-    # hipExtLaunchKernel on its stream (the dispatch's own begin / end timestamps, what the
-    # rocprofv3 kernel trace reports per dispatch).  `roofline`: over the timed region, where R
-    # steps are in flight and a launch shares the CUs with the other steps' kernels (so launches of
-    # different steps overlap: launches x average <= R x step time); `roofline_isolated`: the same
-    # launches in ISO_STEPS steps run one at a time after the timed region (launches x average <=
-    # the step time).  kernel_avg_ms_events: the HIP-event span of one step's back-to-back hash
-    # launches / launches (adds the dispatch gaps between levels).
-    traffic, traffic_tag = pmc_traffic("k_mp_hash", args.config, len(proofs)) if args.air == "synthetic" else (None, None)
+    # roofline of the dominant kernel, the Merkle hash launches (k_mp_hash, + k_mp_hash_wide /
+    # k_mp_hash_tail on the smallest levels): permutations per launch x the analytic VALU lane-ops per
+    # permutation / the average launch duration.  Each launch is timed by the HIP start / stop events
+    # of hipExtLaunchKernel on its stream (the dispatch's own begin / end timestamps, what the
+    # rocprofv3 kernel trace reports per dispatch).  `roofline`: the launches of ISO_STEPS steps run
+    # one at a time right after the timed region (the kernel's own rate; launches x average <= that
+    # step time <= ms_per_step, asserted).  `roofline.inflight`: the same launches inside the timed
+    # region, where R steps are in flight, so launches of different steps overlap each other and the
+    # other kernels (launches x average <= R x step time only): how the level launches share the
+    # machine, not the kernel's rate.  kernel_avg_ms_events: the HIP-event span of one step's
+    # back-to-back hash launches / launches (adds the dispatch gaps between levels).
+    traffic, traffic_tag = pmc_traffic("k_mp_hash", args.config, len(proofs))
+    mp_valu, mp_valu_tag = pmc_mp_valu_per_launch(args.config, len(proofs))
 
     def roofline(a, steps, step_ms_, overlap, measured):
         a = {k: v / steps for k, v in a.items()}
@@ -779,18 +900,32 @@ def main():
         perms_per_launch = a["mp_hash_kernel_perms"] / launches
         achieved = perms_per_launch * TIP5_VALU_OPS_PER_PERM / kern_avg_s if kern_avg_s > 0 else 0.0
         assert launches * kern_avg_s * 1e3 <= overlap * step_ms_ * 1.0001, (launches, kern_avg_s, step_ms_, overlap)
-        return {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
-                "unit": "T VALU lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS, "traffic": traffic,
-                "traffic_unit": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, KiB -> B; MI355X_MICROARCH.md HBM corrections)",
-                "traffic_profile": traffic_tag, "kernel": "k_mp_hash (+ k_mp_hash_wide on the smallest levels)",
-                "kernel_avg_ms": kern_avg_s * 1e3, "kernel_avg_ms_events": kern_avg_ev_s * 1e3,
-                "launches_per_step": launches, "perms_per_launch": perms_per_launch,
-                "valu_ops_per_perm": TIP5_VALU_OPS_PER_PERM, "step_ms": step_ms_,
-                # beside the spec peak: the measured integer issue ceiling (1 wave64 instruction
-                # per 4 clocks per SIMD = 64 lane-ops per instruction), DESIGN.md §3
-                "measured_ceiling": VALU_ISSUE_CEILING * 64 / 1e12,
-                "frac_of_measured_ceiling": achieved / (VALU_ISSUE_CEILING * 64),
-                "measured": measured}
+        r = {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
+             "unit": "T VALU lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS, "traffic": traffic,
+             "traffic_unit": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, KiB -> B; MI355X_MICROARCH.md HBM corrections)",
+             "traffic_profile": traffic_tag,
+             "kernel": "k_mp_hash (+ k_mp_hash_wide / k_mp_hash_tail on the smallest levels)",
+             "kernel_avg_ms": kern_avg_s * 1e3, "kernel_avg_ms_events": kern_avg_ev_s * 1e3,
+             "launches_per_step": launches, "launches_x_avg_ms": launches * kern_avg_s * 1e3,
+             "perms_per_launch": perms_per_launch, "valu_ops_per_perm": TIP5_VALU_OPS_PER_PERM,
+             "step_ms": step_ms_,
+             # the same launches counted with the ~6,070 VALU a pair hash needs (the kernel skips
+             # hash_pair's constant capacity and dead last-round outputs)
+             "pair_hash_valu_ops_per_perm": PAIR_HASH_VALU_OPS,
+             "frac_pair_hash_ops": achieved * PAIR_HASH_VALU_OPS / TIP5_VALU_OPS_PER_PERM / VALU_PEAK_LANE_OPS,
+             # beside the spec peak: the measured integer issue ceiling (1 wave64 instruction
+             # per 4 clocks per SIMD = 64 lane-ops per instruction), DESIGN.md §3
+             "measured_ceiling": VALU_ISSUE_CEILING * 64 / 1e12,
+             "frac_of_measured_ceiling": achieved / (VALU_ISSUE_CEILING * 64),
+             "measured": measured}
+        if mp_valu:
+            # executed lane-instructions per permutation (committed PMC pass of this library:
+            # SQ_INSTS_VALU of the step's hash launches x 64 / the step's Merkle permutations)
+            ex = mp_valu * 64 / max(a["mp_hash_kernel_perms"], 1.0)
+            r.update({"valu_ops_per_perm_executed": ex, "executed_profile": mp_valu_tag,
+                      "frac_executed": perms_per_launch * ex / kern_avg_s / VALU_PEAK_LANE_OPS,
+                      "frac_pair_hash_need_of_executed": PAIR_HASH_VALU_OPS / ex})
+        return r
 
     if args.config == 3:
         workload = (f"BASELINE config 3: {args.collections} ProofCollections x 8 proofs (log2 padded heights "
@@ -823,7 +958,7 @@ def main():
                  "synthetic: constant-codeword proofs (oracle/stark_prover_const.py), synthetic AIR with triton-vm "
                  "column counts"),
         "config": {"workload": workload, "proofs_total": total, "proofs_rank0": n,
-                   "parallelism": f"proof-sharded x{world}", "air": args.air,
+                   "parallelism": f"proof-sharded x{world}", "air": args.air, "input_form": args.input_form,
                    # value's input: the raw proof words already in HBM when the timed region starts;
                    # the host-memory (PCIe-inclusive) rate is pcie_inclusive, never value
                    "input": "HBM-resident raw proof words (uploaded before the timed region; decoded on the "
@@ -849,14 +984,19 @@ def main():
         "host_prepare_ms": {"stage": st0["ms_decode"], "upload_wait": st0["ms_upload"], "total": prep_s * 1e3},
         "inflight": R,
         "iso_steps": iso_steps if acc_iso else 0,
-        "roofline": roofline(acc, K, step_ms, R, f"timed region, {R} step(s) in flight; per-launch HIP events "
-                                                 f"(hipExtLaunchKernel start/stop)"),
     }
+    inflight = roofline(acc, K, step_ms, R, f"timed region, {R} step(s) in flight (launches of different steps "
+                                            f"overlap); per-launch HIP events (hipExtLaunchKernel start/stop)")
     if acc_iso:
-        res["roofline_isolated"] = roofline(acc_iso, iso_steps, iso_ms, 1,
-                                            f"{iso_steps} steps one at a time after the timed region; per-launch HIP "
-                                            f"events (hipExtLaunchKernel start/stop)")
-    valu_step, valu_tag = pmc_valu_per_step(args.config, len(proofs)) if args.air == "synthetic" else (None, None)
+        res["roofline"] = roofline(acc_iso, iso_steps, iso_ms, 1,
+                                   f"the kernel's own rate: {iso_steps} steps one at a time right after the timed "
+                                   f"region; per-launch HIP events (hipExtLaunchKernel start/stop)")
+        assert res["roofline"]["launches_x_avg_ms"] <= step_ms, (res["roofline"], step_ms)
+        res["roofline"]["inflight"] = {k: inflight[k] for k in ("achieved", "frac", "kernel_avg_ms",
+                                                                 "launches_x_avg_ms", "step_ms", "measured")}
+    else:
+        res["roofline"] = inflight
+    valu_step, valu_tag = pmc_valu_per_step(args.config, len(proofs))
     if valu_step:
         # the whole pipeline against the measured VALU issue ceiling: committed PMC instruction
         # count of one step (per GPU) / this run's step time
@@ -874,7 +1014,7 @@ def main():
     step_s = elapsed / K
     res["hbm"] = {"proof_bytes_per_step": words_step * 8, "achieved_GBps": words_step * 8 / step_s / 1e9,
                   "peak_GBps": HBM_PEAK / 1e9, "frac": words_step * 8 / step_s / HBM_PEAK}
-    bytes_step, bytes_tag = pmc_bytes_per_step(args.config, len(proofs)) if args.air == "synthetic" else (None, None)
+    bytes_step, bytes_tag = pmc_bytes_per_step(args.config, len(proofs))
     if bytes_step:
         res["hbm"].update({"pmc_bytes_per_step": bytes_step, "pmc_GBps": bytes_step / step_s / 1e9,
                            "pmc_frac": bytes_step / step_s / HBM_PEAK, "pmc_profile": bytes_tag})
@@ -884,7 +1024,7 @@ def main():
     # the PCIe-inclusive leg and the config-2 microbench belong to the one-GPU report (N = 1): with
     # several ranks, rank 0 would run them alone while the others tear down
     if world == 1 and args.stream_batches > 0:
-        res["pcie_inclusive"] = pcie_stream(ctx, gair, stark, claims, proofs, expect, args.stream_batches)
+        res["pcie_inclusive"] = pcie_stream(ctx, gair, stark, dev_claims, dev_proofs, expect, args.stream_batches)
     if world == 1 and args.paths_log2 > 0:
         res["tip5_paths"] = tip5_paths(ctx, args.paths_log2, 5)
     if world == 1 and args.config1_seconds > 0 and not args.no_cpu:
@@ -895,6 +1035,27 @@ def main():
     if hwq4 is not None:
         res["hw_queues_4"] = hwq4
         correct = correct and hwq4["verdicts_correct"]
+    # the in-process multi-GPU form (one process, nhip_group_stream over every GPU of the job): rank
+    # 0 drives all of them while the other ranks wait at the barrier with their batches freed
+    if args.group_batches > 0 and args.config == 4 and not under_profiler():
+        if dist is not None:
+            dist.barrier()
+        if rank == 0:
+            try:
+                job_claims, job_proofs = claims, proofs
+                job_expect = expect
+                if world > 1:
+                    job_claims, job_proofs, job_expect, _, _, _ = make_config4(pool4, total, 0.01, 1, 0)
+                dcl, dpr = device_form(job_claims, job_proofs, mont)
+                t = time.time()
+                res["group_stream"] = group_stream(range(world), air_words, stark, dcl, dpr, job_expect,
+                                                   args.group_batches)
+                if "pcie_inclusive" in res:
+                    res["group_stream"]["vs_pcie_inclusive"] = res["group_stream"]["value"] / res["pcie_inclusive"]["value"]
+                correct = correct and res["group_stream"]["verdicts_correct"]
+                log(f"[group] {res['group_stream']['value']:.0f} proofs/s over {world} GPU(s) ({time.time() - t:.1f}s)")
+            except Exception as e:  # noqa: BLE001 -- a leg, never the headline
+                res["group_stream"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()

@@ -4,7 +4,9 @@
  *
  * Conventions (mirroring the reference's Rust types; see INTEGRATION.md for bindings):
  *   - Field elements are passed as canonical u64 (BFieldElement::value()).  Inputs >= p are
- *     reduced mod p, i.e. BFieldElement::new semantics.
+ *     reduced mod p, i.e. BFieldElement::new semantics.  The STARK entry points also take them as
+ *     they lie in a `Vec<BFieldElement>` (nhip_stark_params.input_form = NHIP_INPUT_MONTGOMERY:
+ *     twenty-first's raw word x * 2^64 mod p), so a `Proof` is handed over without a copy.
  *   - A Digest is 5 consecutive u64 (Digest::values()), 40 bytes.
  *   - The caller owns every buffer; buffers are borrowed for the duration of the call.
  *   - Return value: 0 (NHIP_OK) or an infrastructure error code (no device, HIP failure,
@@ -53,10 +55,13 @@ enum {
 };
 
 /* ---- context --------------------------------------------------------------------------- */
-/* Bind to the lowest HIP device whose bit is set in device_mask (0 = device 0).  If the environment
- * has no GPU_MAX_HW_QUEUES, sets it to 8 first (two batches in flight need more than HIP's default
- * of 4 hardware queues); HIP reads it once, so this counts only when the library is the process's
- * first HIP user, and an operator's value always stands. */
+/* Hardware queues per process the verifier's pipeline wants: two batches in flight, each with a
+ * hashing and a latency stream, plus the context stream (streams that share a queue serialize; HIP's
+ * default is 4).  HIP reads GPU_MAX_HW_QUEUES once, at its initialisation.  The library never
+ * changes the environment: the operator, or the host binary's main() before it starts any thread,
+ * sets GPU_MAX_HW_QUEUES (e.g. to this value) when it wants more than the default. */
+#define NHIP_HW_QUEUES_RECOMMENDED 8
+/* Bind to the lowest HIP device whose bit is set in device_mask (0 = device 0). */
 int nhip_init(uint32_t device_mask, nhip_ctx **out);
 void nhip_destroy(nhip_ctx *ctx);
 const char *nhip_strerror(int code);
@@ -109,6 +114,13 @@ int nhip_verdicts_all_dev(nhip_ctx *ctx, const uint8_t *d_verdicts, size_t n, ui
  * verification error, incl. empty / short / garbage proofs, as in the reference's reject tests).
  * The AIR is data (nhip_air_create; format in DESIGN.md §9): triton-air's generated constraints
  * are not vendored in the reference, so the AIR is supplied by the caller. */
+/* How the field elements of the claims and proofs handed to the STARK entry points are given: */
+enum {
+    NHIP_INPUT_CANONICAL = 0,  /* canonical values (BFieldElement::value()), any u64 read mod p */
+    NHIP_INPUT_MONTGOMERY = 1  /* twenty-first's in-memory words (x * 2^64 mod p, BFieldElement's
+                                  repr(transparent) u64): Proof.0.as_ptr(), Digest / input /
+                                  output slices as they lie, no conversion; any u64 read mod p */
+};
 typedef struct {
     uint32_t security_level;          /* Stark::default: 160 */
     uint32_t log2_fri_expansion;      /* 2 (expansion factor 4) */
@@ -116,9 +128,11 @@ typedef struct {
     uint32_t num_main;                /* main table columns (triton-vm: 379) */
     uint32_t num_aux;                 /* auxiliary table columns (triton-vm: 88) */
     uint32_t num_quotient_segments;   /* 4 */
+    uint32_t input_form;              /* NHIP_INPUT_CANONICAL (default) or NHIP_INPUT_MONTGOMERY */
 } nhip_stark_params;
 
-/* triton_vm::proof::Claim { program_digest, version, input, output } (canonical u64) */
+/* triton_vm::proof::Claim { program_digest, version, input, output } (field elements in the
+ * params' input_form; version is a plain integer) */
 typedef struct {
     uint64_t program_digest[5];
     uint32_t version;
@@ -193,6 +207,9 @@ int nhip_batch_run(nhip_ctx *ctx, nhip_batch *batch, uint8_t *verdicts, uint8_t 
 int nhip_batch_launch(nhip_ctx *ctx, nhip_batch *batch);
 int nhip_batch_wait(nhip_ctx *ctx, nhip_batch *batch, uint8_t *verdicts, uint8_t *all_ok);
 int nhip_batch_stats(const nhip_batch *batch, nhip_stats *stats);
+/* Fiat-Shamir replay form of later launches, process-wide (tests and A/B runs): -1 = chosen by the
+ * batch size (default), 0 = 16-lane row, 1 = two-row pair, 2 = quad.  NHIP_ERR_ARG otherwise. */
+int nhip_set_fs_form(int form);
 /* Samples squeezed for proof `proof` in squeeze order (challenges, quotient weights, z, linear-
  * combination weights, FRI folding challenges, last-round indeterminate) as canonical XFE
  * triples, the FRI indices, and the proof's failure bits (0 = accepted). */
@@ -214,6 +231,19 @@ int nhip_queue_verify(nhip_queue *queue, const nhip_claim *claims, const nhip_pr
                       uint8_t *verdicts);
 /* batches launched and proofs verified so far */
 int nhip_queue_stats(const nhip_queue *queue, uint64_t *batches, uint64_t *proofs);
+/* Where a queue's time goes, summed over its batches since creation (or the last reset). */
+typedef struct {
+    uint64_t batches, proofs;
+    uint64_t size_hist[8];   /* batches of 1, 2-3, 4-7, 8-15, 16-31, 32-63, 64-127, >= 128 proofs */
+    double ms_window;        /* oldest request's arrival -> its batch's staging starts (coalescing wait) */
+    double ms_stage;         /* host: layout + staging copy + DMA issue of the batch's proofs */
+    double ms_upload;        /* host: the wait for those uploads */
+    double ms_launch;        /* host: enqueueing the batch's device phases */
+    double ms_device;        /* device: first phase start -> verdicts (k_decode to the verdict copy) */
+    double ms_wait;          /* worker blocked in nhip_batch_wait on the batch (not overlapped) */
+    double ms_turnaround;    /* oldest request's arrival -> its verdicts delivered */
+} nhip_queue_profile;
+int nhip_queue_profile_read(const nhip_queue *queue, nhip_queue_profile *out, int reset);
 /* Drains the pending requests, then stops the worker. */
 void nhip_queue_destroy(nhip_queue *queue);
 
@@ -240,6 +270,28 @@ int nhip_group_shard(const nhip_proof *proofs, size_t n, size_t n_members, uint3
 int nhip_group_verify_batch(nhip_group *group, nhip_air *air, const nhip_stark_params *params,
                             const nhip_claim *claims, const nhip_proof *proofs, size_t n, uint8_t *verdicts,
                             uint8_t *all_ok);
+/* Streaming form for callers that verify batch after batch (bootstrap import state/mod.rs:2226-2272,
+ * block batches peer_loop.rs:315-323): every member keeps two device batches, so each member's share
+ * of the next batch is staged and uploaded while the member's share of the current one still runs.
+ * nhip_group_stream_submit shards the batch over the members (nhip_group_shard), refills each
+ * member's idle device batch with its share and launches it, then waits for the PREVIOUS submitted
+ * batch and writes its verdicts / AND into the buffers given with that batch.  When it returns, the
+ * claims / proofs of this batch may be reused (they are on the devices); its `verdicts` (n bytes)
+ * and `all_ok` (nullable) stay borrowed until the next submit or nhip_group_stream_finish writes
+ * them.  A non-zero return is an infrastructure fault: the batches in flight are drained and their
+ * verdicts are unknown (never "accept"); the stream stays usable. */
+typedef struct nhip_group_stream nhip_group_stream;
+int nhip_group_stream_create(nhip_group *group, nhip_air *air, const nhip_stark_params *params,
+                             nhip_group_stream **out);
+int nhip_group_stream_submit(nhip_group_stream *stream, const nhip_claim *claims, const nhip_proof *proofs,
+                             size_t n, uint8_t *verdicts, uint8_t *all_ok);
+/* Waits for the last submitted batch and writes its verdicts. */
+int nhip_group_stream_finish(nhip_group_stream *stream);
+/* Host / device milliseconds of the stream's batches so far (summed over members: stage = host
+ * staging copy + DMA issue, upload = the wait for it, device = the members' device time). */
+int nhip_group_stream_stats(const nhip_group_stream *stream, uint64_t *batches, uint64_t *proofs, double *ms_stage,
+                            double *ms_upload, double *ms_device);
+void nhip_group_stream_destroy(nhip_group_stream *stream);
 
 /* ---- ingestion formats -------------------------------------------
  * Proof files of neptune-core/src/protocol/proof_abstractions/tasm/program.rs:374-390: 8-byte

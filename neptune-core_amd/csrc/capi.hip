@@ -134,7 +134,10 @@ bool is_pow2(size_t n) { return n >= 2 && (n & (n - 1)) == 0; }
 
 extern "C" {
 
-int nhip_abi_version(void) { return 1001; }
+// 2000: nhip_stark_params.input_form (the struct grew), nhip_set_fs_form, the streaming group
+int nhip_abi_version(void) { return 2000; }
+
+int nhip_set_fs_form(int form) { return nhip::set_fs_form(form) == 0 ? NHIP_OK : NHIP_ERR_ARG; }
 
 const char* nhip_strerror(int code) {
     switch (code) {
@@ -148,17 +151,9 @@ const char* nhip_strerror(int code) {
     }
 }
 
-// Hardware queues the verifier's pipeline wants: two batches in flight, each with a hashing and a
-// latency stream, plus the context stream (HIP serializes streams that share a queue; its default
-// is 4).  HIP reads GPU_MAX_HW_QUEUES once, when it initialises: nhip_init sets it before its first
-// HIP call if the operator has not, which counts when the library is the process's first HIP user
-// (the neptune-core node) and changes nothing otherwise.
-static constexpr const char* NHIP_HW_QUEUES = "8";
-
 int nhip_init(uint32_t device_mask, nhip_ctx** out) {
     if (!out) return NHIP_ERR_ARG;
     *out = nullptr;
-    (void)setenv("GPU_MAX_HW_QUEUES", NHIP_HW_QUEUES, 0);  // 0: an operator's value stands
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return NHIP_ERR_NO_DEVICE;
     int dev = 0;

@@ -86,48 +86,6 @@ __host__ __device__ __forceinline__ uint64_t mont_mul_lat(uint64_t a, uint64_t b
     return (E + ~M) + (neg ? GL_P + 1 : 1ull);
 }
 
-// N independent Montgomery products, written stage by stage so that the carry-chain
-// instructions of different elements interleave (fills the VALU->VCC->VALU wait states that a
-// single chain would pad with s_nop).
-template <int N>
-__host__ __device__ __forceinline__ void mont_mul_n(const uint64_t* a, const uint64_t* b, uint64_t* out) {
-    uint64_t p00[N], t[N], u[N], xh[N];
-    uint32_t ah[N], e[N], bl[N], bh[N], rl[N], rh[N], c1[N], c[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) p00[i] = (uint64_t)(uint32_t)a[i] * (uint32_t)b[i];
-#pragma unroll
-    for (int i = 0; i < N; ++i) t[i] = (uint64_t)(uint32_t)a[i] * (uint32_t)(b[i] >> 32) + (p00[i] >> 32);
-#pragma unroll
-    for (int i = 0; i < N; ++i) u[i] = (uint64_t)(uint32_t)(a[i] >> 32) * (uint32_t)b[i] + (uint32_t)t[i];
-#pragma unroll
-    for (int i = 0; i < N; ++i) xh[i] = (uint64_t)(uint32_t)(a[i] >> 32) * (uint32_t)(b[i] >> 32) + (t[i] >> 32);
-#pragma unroll
-    for (int i = 0; i < N; ++i) xh[i] += (u[i] >> 32);
-#pragma unroll
-    for (int i = 0; i < N; ++i) ah[i] = __builtin_addc((uint32_t)u[i], (uint32_t)p00[i], 0u, &e[i]);
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        unsigned int br1;
-        bl[i] = __builtin_subc((uint32_t)p00[i], ah[i], e[i], &br1);
-        e[i] = br1;
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        unsigned int br2;
-        bh[i] = __builtin_subc(ah[i], 0u, e[i], &br2);
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) rl[i] = __builtin_subc((uint32_t)xh[i], bl[i], 0u, &c1[i]);
-#pragma unroll
-    for (int i = 0; i < N; ++i) rh[i] = __builtin_subc((uint32_t)(xh[i] >> 32), bh[i], c1[i], &c[i]);
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        unsigned int c2;
-        const uint32_t lo = __builtin_subc(rl[i], 0u - c[i], 0u, &c2);
-        out[i] = ((uint64_t)(rh[i] - c2) << 32) | lo;
-    }
-}
-
 // a + b mod p for a, b in [0, p)
 __host__ __device__ __forceinline__ uint64_t gl_add(uint64_t a, uint64_t b) {
     const uint64_t s = a + b;

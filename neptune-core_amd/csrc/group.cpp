@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
+#include <functional>
 #include <new>
 #include <numeric>
 #include <system_error>
@@ -164,6 +166,247 @@ int nhip_group_verify_batch(nhip_group* g, nhip_air* air, const nhip_stark_param
         return NHIP_ERR_OOM;
     }
     return NHIP_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------- streaming group
+// Per member two device batches (slot k % 2 holds batch k's share).  submit(k): every busy member,
+// on its own host thread, refills slot k % 2 (host staging + upload; the member's slot (k - 1) % 2
+// is still running batch k - 1 on its GPU), launches it, then waits for slot (k - 1) % 2 and
+// scatters batch k - 1's verdicts.  So the upload of batch k overlaps the device run of batch k - 1
+// on every member at once, as the one-context refill / launch / wait loop does (bench.py's
+// pcie_inclusive), and the members stream concurrently.
+namespace {
+
+struct StreamBatch {
+    uint8_t* verdicts = nullptr;
+    uint8_t* all_ok = nullptr;
+    size_t n = 0;
+    std::vector<std::vector<size_t>> idx;  // per member: the caller's positions of its share
+    bool live = false;                     // launched on some member, verdicts not yet written
+};
+
+struct MemberSlots {
+    nhip_batch* b[2] = {nullptr, nullptr};
+    bool in_flight[2] = {false, false};
+    std::vector<nhip_claim> claims;
+    std::vector<nhip_proof> proofs;
+    std::vector<uint8_t> v;
+};
+
+}  // namespace
+
+struct nhip_group_stream {
+    nhip_group* g = nullptr;
+    nhip_air* air = nullptr;
+    nhip_stark_params params{};
+    std::vector<MemberSlots> m;
+    StreamBatch sb[2];
+    uint64_t next = 0;  // batches submitted
+    uint64_t batches = 0, proofs = 0;
+
+    // Run f(member) for every member in `who` concurrently (member threads; the caller's thread
+    // takes the first, and any share whose thread cannot be started); returns the first error.
+    int on_members(const std::vector<size_t>& who, const std::function<int(size_t)>& f) {
+        std::vector<int> rcs(who.size(), NHIP_OK);
+        std::vector<std::thread> th;
+        std::vector<size_t> inline_k;
+        th.reserve(who.size());
+        inline_k.reserve(who.size());
+        for (size_t k = 1; k < who.size(); ++k) {
+            try {
+                th.emplace_back([&, k] { rcs[k] = f(who[k]); });
+            } catch (const std::system_error&) {
+                inline_k.push_back(k);
+            }
+        }
+        if (!who.empty()) rcs[0] = f(who[0]);
+        for (auto& t : th) t.join();
+        for (size_t k : inline_k) rcs[k] = f(who[k]);
+        for (int rc : rcs)
+            if (rc) return rc;
+        return NHIP_OK;
+    }
+
+    // member mm: wait for its share of batch sb[s] and scatter the verdicts
+    int complete_member(size_t mm, int s) {
+        MemberSlots& ms = m[mm];
+        if (!ms.in_flight[s]) return NHIP_OK;
+        ms.in_flight[s] = false;
+        StreamBatch& B = sb[s];
+        const size_t cnt = B.idx[mm].size();
+        const int rc = nhip_batch_wait(g->members[mm], ms.b[s], ms.v.data(), nullptr);
+        if (rc) return rc;
+        for (size_t q = 0; q < cnt; ++q) B.verdicts[B.idx[mm][q]] = ms.v[q];
+        nhip_stats st{};
+        nhip_batch_stats(ms.b[s], &st);
+        dev_ms[mm] += st.ms_device_total;
+        return NHIP_OK;
+    }
+
+    std::vector<double> stage_ms, upload_ms, dev_ms;  // per member, written by that member's thread only
+
+    void finish_batch(int s) {
+        StreamBatch& B = sb[s];
+        if (!B.live) return;
+        B.live = false;
+        if (B.all_ok) {
+            uint8_t ok = 1;
+            for (size_t i = 0; i < B.n; ++i) ok &= (uint8_t)(B.verdicts[i] != 0);
+            *B.all_ok = ok;
+        }
+    }
+
+    // after a fault: wait for whatever is still running so every slot is idle again
+    void drain() {
+        for (size_t mm = 0; mm < m.size(); ++mm)
+            for (int s = 0; s < 2; ++s)
+                if (m[mm].in_flight[s]) {
+                    (void)nhip_batch_wait(g->members[mm], m[mm].b[s], nullptr, nullptr);
+                    m[mm].in_flight[s] = false;
+                }
+        sb[0].live = sb[1].live = false;
+    }
+};
+
+extern "C" {
+
+int nhip_group_stream_create(nhip_group* g, nhip_air* air, const nhip_stark_params* params,
+                             nhip_group_stream** out) {
+    if (!g || g->members.empty() || !air || !params || !out) return NHIP_ERR_ARG;
+    *out = nullptr;
+    nhip_group_stream* st = new (std::nothrow) nhip_group_stream();
+    if (!st) return NHIP_ERR_OOM;
+    try {
+        st->g = g;
+        st->air = air;
+        st->params = *params;
+        st->m.resize(g->members.size());
+        st->stage_ms.assign(g->members.size(), 0.0);
+        st->upload_ms.assign(g->members.size(), 0.0);
+        st->dev_ms.assign(g->members.size(), 0.0);
+        for (auto& b : st->sb) b.idx.resize(g->members.size());
+    } catch (const std::bad_alloc&) {
+        delete st;
+        return NHIP_ERR_OOM;
+    }
+    *out = st;
+    return NHIP_OK;
+}
+
+int nhip_group_stream_submit(nhip_group_stream* st, const nhip_claim* claims, const nhip_proof* proofs, size_t n,
+                             uint8_t* verdicts, uint8_t* all_ok) {
+    if (!st) return NHIP_ERR_ARG;
+    if (n && (!claims || !proofs || !verdicts)) return NHIP_ERR_ARG;
+    const size_t M = st->m.size();
+    const int s = (int)(st->next & 1u), sp = s ^ 1;
+    try {
+        StreamBatch& B = st->sb[s];
+        B.verdicts = verdicts;
+        B.all_ok = all_ok;
+        B.n = n;
+        std::vector<uint32_t> member_of(n);
+        int rc = nhip_group_shard(proofs, n, M, member_of.data());
+        if (rc) return rc;
+        for (auto& v : B.idx) v.clear();
+        for (size_t i = 0; i < n; ++i) B.idx[member_of[i]].push_back(i);
+        std::vector<size_t> who;  // members with a share of this batch or a previous share to complete
+        for (size_t mm = 0; mm < M; ++mm) {
+            MemberSlots& ms = st->m[mm];
+            ms.claims.clear();
+            ms.proofs.clear();
+            for (size_t i : B.idx[mm]) {
+                ms.claims.push_back(claims[i]);
+                ms.proofs.push_back(proofs[i]);
+            }
+            ms.v.resize(std::max<size_t>(1, st->sb[sp].idx[mm].size()));  // the previous share's verdicts
+            if (!B.idx[mm].empty() || ms.in_flight[sp]) who.push_back(mm);
+        }
+        B.live = n > 0;
+        rc = st->on_members(who, [&](size_t mm) -> int {
+            MemberSlots& ms = st->m[mm];
+            nhip_ctx* c = st->g->members[mm];
+            const size_t cnt = B.idx[mm].size();
+            if (cnt) {
+                // slot s is idle: its batch (k - 2) was completed by the previous submit
+                int r = ms.b[s] ? nhip_batch_refill(c, ms.b[s], st->air, &st->params, ms.claims.data(),
+                                                    ms.proofs.data(), cnt)
+                                : nhip_batch_prepare(c, st->air, &st->params, ms.claims.data(), ms.proofs.data(),
+                                                     cnt, &ms.b[s]);
+                if (!r) {
+                    nhip_stats bs{};
+                    nhip_batch_stats(ms.b[s], &bs);
+                    st->stage_ms[mm] += bs.ms_decode;
+                    st->upload_ms[mm] += bs.ms_upload;
+                    r = nhip_batch_launch(c, ms.b[s]);
+                }
+                if (r) return r;
+                ms.in_flight[s] = true;
+            }
+            return st->complete_member(mm, sp);
+        });
+        if (rc) {
+            st->drain();
+            ++st->next;
+            return rc;
+        }
+        st->finish_batch(sp);
+        st->batches += n ? 1 : 0;
+        st->proofs += n;
+        ++st->next;
+    } catch (const std::bad_alloc&) {
+        st->drain();
+        ++st->next;
+        return NHIP_ERR_OOM;
+    }
+    return NHIP_OK;
+}
+
+int nhip_group_stream_finish(nhip_group_stream* st) {
+    if (!st) return NHIP_ERR_ARG;
+    const int sp = (int)((st->next & 1u) ^ 1u);  // the last submitted batch's slot
+    std::vector<size_t> who;
+    for (size_t mm = 0; mm < st->m.size(); ++mm)
+        if (st->m[mm].in_flight[sp]) who.push_back(mm);
+    int rc;
+    try {
+        rc = st->on_members(who, [&](size_t mm) { return st->complete_member(mm, sp); });
+    } catch (const std::bad_alloc&) {
+        rc = NHIP_ERR_OOM;
+    }
+    if (rc) {
+        st->drain();
+        return rc;
+    }
+    st->finish_batch(sp);
+    return NHIP_OK;
+}
+
+int nhip_group_stream_stats(const nhip_group_stream* st, uint64_t* batches, uint64_t* proofs, double* ms_stage,
+                            double* ms_upload, double* ms_device) {
+    if (!st) return NHIP_ERR_ARG;
+    double a = 0, b = 0, c = 0;
+    for (size_t mm = 0; mm < st->m.size(); ++mm) {
+        a += st->stage_ms[mm];
+        b += st->upload_ms[mm];
+        c += st->dev_ms[mm];
+    }
+    if (batches) *batches = st->batches;
+    if (proofs) *proofs = st->proofs;
+    if (ms_stage) *ms_stage = a;
+    if (ms_upload) *ms_upload = b;
+    if (ms_device) *ms_device = c;
+    return NHIP_OK;
+}
+
+void nhip_group_stream_destroy(nhip_group_stream* st) {
+    if (!st) return;
+    st->drain();
+    for (size_t mm = 0; mm < st->m.size(); ++mm)
+        for (nhip_batch* b : st->m[mm].b)
+            if (b) nhip_batch_destroy(b);
+    delete st;
 }
 
 }  // extern "C"

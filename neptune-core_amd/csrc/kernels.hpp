@@ -154,16 +154,15 @@ struct StarkPhaseTimer {
 // FRI -> DEEP), st the VALU-bound hashing (rows -> per-level Merkle hashes -> roots -> verdicts).
 hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream_t st_aux, StarkPhaseTimer* tm);
 hipError_t stark_set_kernel_attributes();
+// nhip_set_fs_form: -1 = by batch size (default), 0 row, 1 pair, 2 quad; -1 return = bad form
+int set_fs_form(int form);
 
-// DEEP row combination: S column chunks per revealed row (S * k threads, <= 256), LDS for the
-// weights (main: 3 words per column, aux: 9 per column) and the S x k chunk sums.
-inline uint32_t deep_chunks(const StarkDims& d) {
-    uint32_t S = 256 / d.num_checks;
-    return S < 1 ? 1 : (S > 8 ? 8 : S);
-}
-inline size_t deep_lds_bytes(const StarkDims& d) {
-    return (size_t)(3 * d.num_main + 9 * d.num_aux) * 8 + (size_t)deep_chunks(d) * d.num_checks * 24;
-}
+// k_deep_rows8's carry-free accumulation (stark_kernels.hip): a row has M + 3A < DEEP_ROW_WORDS_MAX
+// words (dims_from), a lane takes at most ceil(M / 8) + ceil(3A / 8) <= DEEP_LANE_TERMS_MAX of them,
+// each partial product is < 2^54, and a 64-bit accumulator must not reach 2^63
+static constexpr uint32_t DEEP_ROW_WORDS_MAX = 2048;
+static constexpr uint64_t DEEP_LANE_TERMS_MAX = (DEEP_ROW_WORDS_MAX - 1 + 14) / 8;
+static_assert(DEEP_LANE_TERMS_MAX * (1ull << 54) < (1ull << 63), "k_deep_rows8 accumulators stay below 2^63");
 // k_deep_rows8: the weights (one uint4 of limbs per coefficient), then one XFE per revealed row
 inline size_t deep_rows8_lds_bytes(const StarkDims& d) {
     return (size_t)(3 * d.num_main + 9 * d.num_aux) * 16 + (size_t)d.num_checks * 24;

@@ -15,9 +15,12 @@
 // decode or come in another order, is rejected: the same verdicts as decoding every item first
 // and then dequeuing (and no allocation driven by the untrusted item count).
 //
-// Words may be any u64: structural words (lengths, counts, discriminants, the padded height) are
-// read through canon() (BFieldElement::new reduces mod p); the arithmetic kernels reduce what they
-// load (to_mont / mod-p accumulation), so no separate reduction pass over the proof is needed.
+// Words may be any u64, in either input form (nhip_stark_params.input_form): canonical values
+// (MW = false, BFieldElement::new semantics) or twenty-first's in-memory Montgomery words (MW = true,
+// x * 2^64 mod p).  Structural words (lengths, counts, discriminants, the padded height) are read
+// through word_value<MW> (the element's canonical value); the arithmetic kernels load through
+// word_mont<MW> (the canonical raw Montgomery word) or reduce mod p as they accumulate, so no
+// separate conversion pass over the proof is needed in either form.
 #pragma once
 #include <stdint.h>
 
@@ -34,6 +37,7 @@ enum ItemKind : uint32_t {
 struct Dims {
     StarkDims d;
     uint32_t expansion;
+    uint32_t mont_words;  // input form: 0 canonical values, 1 Montgomery words (NHIP_INPUT_*)
 };
 
 // Proof geometry implied by the padded height (the first item).
@@ -51,6 +55,18 @@ struct ClaimLoc {
 static constexpr uint32_t SHAPE_NONE = 0xFFFFFFFFu;  // header malformed: the proof is rejected
 
 __host__ __device__ __forceinline__ uint64_t canon(uint64_t v) { return v >= GL_P ? v - GL_P : v; }
+// A batch word as the element's canonical value (structural words) ...
+template <bool MW>
+__host__ __device__ __forceinline__ uint64_t word_value(uint64_t w) {
+    if constexpr (MW) return from_mont(w);  // montyred(w, 0): any u64 -> w * 2^-64 mod p, in [0, p)
+    else return canon(w);
+}
+// ... and as the canonical raw Montgomery word the arithmetic works on (Tip5 reads its bytes)
+template <bool MW>
+__host__ __device__ __forceinline__ uint64_t word_mont(uint64_t w) {
+    if constexpr (MW) return canon(w);
+    else return to_mont(w);
+}
 __host__ __device__ __forceinline__ uint32_t log2_u64(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
 
 // Fri::num_rounds for a FRI domain of fri_len: rounds until the code dimension reaches
@@ -96,9 +112,12 @@ __host__ __device__ __forceinline__ uint32_t expected_kind(uint64_t t, uint32_t 
 
 // The padded height the proof declares, if its header is well formed: [len - 1, n_items,
 // 2, LOG2_PADDED_HEIGHT, log2_ph, ...].  Host sizing of a batch peeks at it; k_decode re-reads it.
+template <bool MW>
 __host__ __device__ __forceinline__ bool header_log2_ph(const uint64_t* w, uint64_t len, uint64_t& log2_ph) {
-    if (len < 5 || canon(w[0]) != len - 1 || canon(w[2]) != 2 || canon(w[3]) != LOG2_PADDED_HEIGHT) return false;
-    log2_ph = canon(w[4]);
+    if (len < 5 || word_value<MW>(w[0]) != len - 1 || word_value<MW>(w[2]) != 2 ||
+        word_value<MW>(w[3]) != LOG2_PADDED_HEIGHT)
+        return false;
+    log2_ph = word_value<MW>(w[4]);
     return log2_ph < (1ull << 32);
 }
 
@@ -111,10 +130,11 @@ struct Item {
 };
 
 // Decode one ProofItem occupying words[lo, hi).  false on any malformation.
+template <bool MW>
 __host__ __device__ inline bool decode_item(const uint64_t* w, uint64_t lo, uint64_t hi, const Dims& D, Item& it) {
     if (lo >= hi) return false;
     it = Item{};
-    const uint64_t disc = canon(w[lo]);
+    const uint64_t disc = word_value<MW>(w[lo]);
     it.kind = (uint32_t)(disc < N_KINDS ? disc : N_KINDS);
     it.lo = lo;
     it.hi = hi;
@@ -127,31 +147,31 @@ __host__ __device__ inline bool decode_item(const uint64_t* w, uint64_t lo, uint
         case OOD_QUOT_SEGMENTS: it.payload = lo + 1; return len == 1 + 3ull * d.num_quot_seg;
         case LOG2_PADDED_HEIGHT:
             if (len != 2) return false;
-            it.n = canon(w[lo + 1]);
+            it.n = word_value<MW>(w[lo + 1]);
             return it.n < (1ull << 32);
         case N_KINDS: return false;
         default: break;
     }
     // dynamically sized payload: [kind, blen, body(blen)]
     if (len < 2) return false;
-    const uint64_t blen = canon(w[lo + 1]);
+    const uint64_t blen = word_value<MW>(w[lo + 1]);
     if (blen != len - 2) return false;
     const uint64_t b0 = lo + 2;
     if (it.kind == FRI_RESPONSE) {
         // FriResponse { auth_structure, revealed_leaves } encoded fields-reversed:
         // [len(rl), n_leaves, leaves.., len(au), n_auth, digests..]
         if (blen < 1) return false;
-        const uint64_t lrl = canon(w[b0]);
+        const uint64_t lrl = word_value<MW>(w[b0]);
         if (lrl < 1 || lrl >= blen) return false;
-        const uint64_t nl = canon(w[b0 + 1]);
+        const uint64_t nl = word_value<MW>(w[b0 + 1]);
         if (nl > (lrl - 1) / 3 || 3 * nl != lrl - 1) return false;
         it.leaves_off = b0 + 2;
         it.leaves_n = nl;
         const uint64_t pa = b0 + 1 + lrl;
         if (pa >= b0 + blen) return false;
-        const uint64_t lau = canon(w[pa]);
+        const uint64_t lau = word_value<MW>(w[pa]);
         if (lau < 1 || 1 + lrl + 1 + lau != blen) return false;
-        const uint64_t na = canon(w[pa + 1]);
+        const uint64_t na = word_value<MW>(w[pa + 1]);
         if (na > (lau - 1) / 5 || 5 * na != lau - 1) return false;
         it.auth_off = pa + 2;
         it.auth_n = na;
@@ -168,7 +188,7 @@ __host__ __device__ inline bool decode_item(const uint64_t* w, uint64_t lo, uint
         default: return false;
     }
     if (blen < 1) return false;
-    const uint64_t n = canon(w[b0]);
+    const uint64_t n = word_value<MW>(w[b0]);
     if (width == 0 || n > (blen - 1) / width || n * width != blen - 1) return false;
     it.n = n;
     it.payload = b0 + 1;
@@ -197,14 +217,15 @@ __host__ __device__ __forceinline__ void claim_offsets(ProofDesc& pd, const Clai
     pd.claim_digest_off = cl.off + clen - 5;
 }
 
+template <bool MW>
 __host__ __device__ inline uint32_t decode_stream_walk(const uint64_t* w, uint64_t base, uint64_t len,
                                                        const ClaimLoc& cl, const Dims& D, ProofDesc& pd, FsOp* ops,
                                                        uint64_t& perms, uint64_t& perms_lcw) {
     const StarkDims& d = D.d;
     const uint64_t clen = (uint64_t)cl.out_n + cl.in_n + 10;
     const uint64_t end = base + len;
-    if (len < 2 || canon(w[base]) != len - 1) return FAIL_DECODE;
-    const uint64_t n_items = canon(w[base + 1]);
+    if (len < 2 || word_value<MW>(w[base]) != len - 1) return FAIL_DECODE;
+    const uint64_t n_items = word_value<MW>(w[base + 1]);
     uint64_t pos = base + 2;
     ProofShape sh{};
     uint64_t t = 0;
@@ -224,9 +245,9 @@ __host__ __device__ inline uint32_t decode_stream_walk(const uint64_t* w, uint64
     for (;; ++t) {
         if (t > 0 && t == expected_items(R)) break;
         if (t >= n_items || pos >= end) return FAIL_DECODE;
-        const uint64_t ln = canon(w[pos++]);
+        const uint64_t ln = word_value<MW>(w[pos++]);
         if (ln > end - pos) return FAIL_DECODE;
-        if (!decode_item(w, pos, pos + ln, D, it)) return FAIL_DECODE;
+        if (!decode_item<MW>(w, pos, pos + ln, D, it)) return FAIL_DECODE;
         pos += ln;
         if (it.kind != expected_kind(t, R)) return FAIL_DECODE;
         const uint32_t k = d.num_checks;
@@ -297,12 +318,13 @@ __host__ __device__ inline uint32_t decode_stream_walk(const uint64_t* w, uint64
     return 0;
 }
 
+template <bool MW>
 __host__ __device__ inline uint32_t decode_stream(const uint64_t* w, uint64_t base, uint64_t len, const ClaimLoc& cl,
                                                   const Dims& D, ProofDesc& pd, FsOp* ops, uint64_t& perms,
                                                   uint64_t& perms_lcw) {
     pd = ProofDesc{};
     perms = perms_lcw = 0;
-    const uint32_t f = decode_stream_walk(w, base, len, cl, D, pd, ops, perms, perms_lcw);
+    const uint32_t f = decode_stream_walk<MW>(w, base, len, cl, D, pd, ops, perms, perms_lcw);
     if (f) {
         pd = ProofDesc{};
         perms = perms_lcw = 0;

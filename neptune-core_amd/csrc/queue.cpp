@@ -70,6 +70,14 @@ struct nhip_queue {
     std::vector<nhip_proof> proofs;
     std::vector<uint8_t> verdicts;
     std::atomic<uint64_t> n_batches{0}, n_proofs{0};
+    // nhip_queue_profile: written by the worker under prof_mu, read by nhip_queue_profile_read
+    mutable std::mutex prof_mu;
+    nhip_queue_profile prof{};
+    Clock::time_point oldest[2];  // per slot: the earliest arrival among its requests
+
+    static double ms_since(Clock::time_point t0, Clock::time_point t1) {
+        return std::chrono::duration<double, std::milli>(t1 - t0).count();
+    }
 
     void deliver(std::vector<Req*>& reqs, int rc, const uint8_t* v) {
         std::lock_guard<std::mutex> g(mu);
@@ -95,22 +103,36 @@ struct nhip_queue {
         } catch (const std::bad_alloc&) {
             rc = NHIP_ERR_OOM;  // still wait: the slot must be idle before it is refilled
         }
+        const Clock::time_point t0 = Clock::now();
         const int wrc = nhip_batch_wait(ctx, slot[s], rc ? nullptr : verdicts.data(), nullptr);
+        const Clock::time_point t1 = Clock::now();
+        nhip_stats st{};
+        if (!wrc) nhip_batch_stats(slot[s], &st);
         deliver(in_slot[s], rc ? rc : wrc, rc ? nullptr : verdicts.data());
+        std::lock_guard<std::mutex> g(prof_mu);
+        prof.ms_wait += ms_since(t0, t1);
+        prof.ms_device += st.ms_device_total;
+        prof.ms_turnaround += ms_since(oldest[s], Clock::now());
     }
 
     // stage + launch the requests in in_slot[s]
     void launch(int s) {
         claims.clear();
         proofs.clear();
-        for (Req* r : in_slot[s])
+        oldest[s] = Clock::now();
+        for (Req* r : in_slot[s]) {
+            oldest[s] = std::min(oldest[s], r->arrived);
             for (size_t i = 0; i < r->n; ++i) {
                 claims.push_back(r->claims[i]);
                 proofs.push_back(r->proofs[i]);
             }
+        }
+        const Clock::time_point t0 = Clock::now();
         int rc = slot[s] ? nhip_batch_refill(ctx, slot[s], air, &params, claims.data(), proofs.data(), claims.size())
                          : nhip_batch_prepare(ctx, air, &params, claims.data(), proofs.data(), claims.size(), &slot[s]);
+        const Clock::time_point t1 = Clock::now();
         if (!rc) rc = nhip_batch_launch(ctx, slot[s]);
+        const Clock::time_point t2 = Clock::now();
         if (rc) {
             deliver(in_slot[s], rc, nullptr);
             return;
@@ -118,6 +140,17 @@ struct nhip_queue {
         in_flight[s] = true;
         ++n_batches;
         n_proofs += claims.size();
+        nhip_stats st{};
+        nhip_batch_stats(slot[s], &st);
+        std::lock_guard<std::mutex> g(prof_mu);
+        const size_t n = claims.size();
+        prof.batches += 1;
+        prof.proofs += n;
+        prof.size_hist[std::min<size_t>(7, n <= 1 ? 0 : (size_t)(63 - __builtin_clzll((unsigned long long)n)))] += 1;
+        prof.ms_window += ms_since(oldest[s], t0);
+        prof.ms_stage += st.ms_decode;
+        prof.ms_upload += st.ms_upload;
+        prof.ms_launch += ms_since(t1, t2);
     }
 
     void run() {
@@ -232,6 +265,14 @@ int nhip_queue_stats(const nhip_queue* q, uint64_t* batches, uint64_t* proofs) {
     if (!q) return NHIP_ERR_ARG;
     if (batches) *batches = q->n_batches.load();
     if (proofs) *proofs = q->n_proofs.load();
+    return NHIP_OK;
+}
+
+int nhip_queue_profile_read(const nhip_queue* q, nhip_queue_profile* out, int reset) {
+    if (!q || !out) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(q->prof_mu);
+    *out = q->prof;
+    if (reset) const_cast<nhip_queue*>(q)->prof = nhip_queue_profile{};
     return NHIP_OK;
 }
 

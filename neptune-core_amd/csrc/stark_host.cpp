@@ -32,7 +32,6 @@ using namespace nhip;
 
 namespace {
 
-constexpr uint64_t P = GL_P;
 constexpr size_t OUT_HDR = CNT_N * 8;  // pinned readback: [device counters | plan counters | verdicts]
 // hash levels launched before the OOD / FRI / DEEP chain is released (NHIP_AUX_AFTER_LEVEL
 // overrides); tuned on MI355X
@@ -54,16 +53,19 @@ struct HostBatch {
 uint64_t claim_words(const nhip_claim& c) { return (uint64_t)c.output_len + c.input_len + 10; }
 
 // The claim's BFieldCodec encoding (pinned layout, new_claim.rs:38-100):
-// [out_n + 1, out_n, out.., in_n + 1, in_n, in.., version, digest(5)]
-void encode_claim(const nhip_claim& claim, uint64_t* c) {
-    *c++ = claim.output_len + 1;
-    *c++ = claim.output_len;
-    for (size_t i = 0; i < claim.output_len; ++i) *c++ = claim.output[i] % P;
-    *c++ = claim.input_len + 1;
-    *c++ = claim.input_len;
-    for (size_t i = 0; i < claim.input_len; ++i) *c++ = claim.input[i] % P;
-    *c++ = claim.version;
-    for (int i = 0; i < 5; ++i) *c++ = claim.program_digest[i] % P;
+// [out_n + 1, out_n, out.., in_n + 1, in_n, in.., version, digest(5)], staged in the batch's input
+// form (the kernels read the claim and the proof words alike): the caller's field elements reduced
+// mod p in their own form, the lengths and the version (plain integers) converted into it.
+void encode_claim(const nhip_claim& claim, bool mont, uint64_t* c) {
+    auto len = [&](uint64_t v) { return mont ? to_mont(v) : v; };
+    *c++ = len(claim.output_len + 1);
+    *c++ = len(claim.output_len);
+    for (size_t i = 0; i < claim.output_len; ++i) *c++ = canon(claim.output[i]);
+    *c++ = len(claim.input_len + 1);
+    *c++ = len(claim.input_len);
+    for (size_t i = 0; i < claim.input_len; ++i) *c++ = canon(claim.input[i]);
+    *c++ = len(claim.version);
+    for (int i = 0; i < 5; ++i) *c++ = canon(claim.program_digest[i]);
 }
 
 // Host threads for staging copies (NHIP_HOST_THREADS overrides; at most 16, the GPU box's CPU
@@ -193,8 +195,9 @@ bool dims_from(const nhip_stark_params* sp, const nhip_air* air, Dims& D) {
     if (sp->log2_fri_expansion < 1 || sp->log2_fri_expansion > 8) return false;
     if (sp->num_main != air->dims_air.num_main || sp->num_aux != air->dims_air.num_aux) return false;
     if (sp->num_quotient_segments < 1 || sp->num_quotient_segments > 64) return false;
-    // DEEP kernel: < 2^11 limb products per accumulator (M + 3A terms), weights in LDS
-    if (sp->num_main + 3ull * sp->num_aux >= 2048) return false;
+    if (sp->input_form != NHIP_INPUT_CANONICAL && sp->input_form != NHIP_INPUT_MONTGOMERY) return false;
+    // DEEP kernel: carry-free accumulators (M + 3A row words, DEEP_ROW_WORDS_MAX), weights in LDS
+    if (sp->num_main + 3ull * sp->num_aux >= DEEP_ROW_WORDS_MAX) return false;
     StarkDims& d = D.d;
     d.num_main = sp->num_main;
     d.num_aux = sp->num_aux;
@@ -206,7 +209,8 @@ bool dims_from(const nhip_stark_params* sp, const nhip_air* air, Dims& D) {
     d.num_sampled = air->dims_air.num_sampled;
     d.num_constraints = air->dims_air.num_constraints;
     D.expansion = 1u << sp->log2_fri_expansion;
-    if (deep_lds_bytes(d) > 160 * 1024 - 8192 || deep_rows8_lds_bytes(d) > 160 * 1024 - 8192) return false;
+    D.mont_words = sp->input_form == NHIP_INPUT_MONTGOMERY ? 1u : 0u;
+    if (deep_rows8_lds_bytes(d) > 160 * 1024 - 8192) return false;
     // the last FRI codeword has at most 2^(floor(log2 k) + 1 + log2 expansion) XFEs; bound its
     // Merkle-tree scratch (n x max_len digests)
     if ((1ull << (log2_u64(d.num_checks) + 1 + d.log2_expansion)) > 4096) return false;
@@ -333,6 +337,7 @@ void nhip_stark_params_default(nhip_stark_params* out) {
     out->num_main = 379;
     out->num_aux = 88;
     out->num_quotient_segments = 4;
+    out->input_form = NHIP_INPUT_CANONICAL;
 }
 
 int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
@@ -445,7 +450,9 @@ int nhip_proof_decodes(const nhip_air* air, const nhip_stark_params* sp, const n
     FsOp ops[fs_ops_for(MAX_FRI_ROUNDS)];
     uint64_t perms, perms_lcw;
     const ClaimLoc cl{0, (uint32_t)claim->input_len, (uint32_t)claim->output_len};
-    return decode_stream(proof->words, 0, proof->len, cl, D, pd, ops, perms, perms_lcw) ? 0 : 1;
+    const uint32_t f = D.mont_words ? decode_stream<true>(proof->words, 0, proof->len, cl, D, pd, ops, perms, perms_lcw)
+                                    : decode_stream<false>(proof->words, 0, proof->len, cl, D, pd, ops, perms, perms_lcw);
+    return f ? 0 : 1;
 }
 
 namespace {
@@ -518,7 +525,9 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         for (size_t i = 0; i < n; ++i) {
             uint64_t lph = 0;
             ProofShape s{};
-            if (header_log2_ph(proofs[i].words, proofs[i].len, lph) && shape_of(D, lph, s)) {
+            const bool hdr = D.mont_words ? header_log2_ph<true>(proofs[i].words, proofs[i].len, lph)
+                                          : header_log2_ph<false>(proofs[i].words, proofs[i].len, lph);
+            if (hdr && shape_of(D, lph, s)) {
                 pin[i].sized_log2_ph = s.log2_ph;
                 shp[i] = s;
                 H.max_R = std::max(H.max_R, s.R);
@@ -580,7 +589,7 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
                 pageable.resize(H.words_total + 1);
                 stage = pageable.data();
             }
-            for (size_t i = 0; i < n; ++i) encode_claim(claims[i], stage + pin[i].claim_off);
+            for (size_t i = 0; i < n; ++i) encode_claim(claims[i], D.mont_words != 0, stage + pin[i].claim_off);
             std::vector<size_t> todo;  // staged proofs, in order
             uint64_t staged_bytes = 0;
             for (size_t i = 0; i < n; ++i)

@@ -1,11 +1,14 @@
 // Phase kernels of the batched STARK verifier (see stark.hpp for the phase list).
 //
-// Conventions: the batch word buffer holds the proof words as the caller gave them (raw u64, any
-// value: BFieldElement::new semantics) and the staged claims; every load of a field element from it
-// reduces (to_mont / canon, proof_codec.hpp), structural words are read mod p by the decoder.  Every
+// Conventions: the batch word buffer holds the proof words as the caller gave them (any u64, in the
+// batch's input form: canonical values or twenty-first's Montgomery words; every kernel that reads
+// it is instantiated for both, MW = Montgomery) and the staged claims in the same form; every load
+// of a field element from it goes through word_mont<MW> (proof_codec.hpp), structural words through
+// word_value<MW> in the decoder.  Every
 // scratch value written by these kernels (samples, row digests, OOD sums) is a raw Montgomery word.  Each failed check ORs a FailBits bit into fail[proof].
 #include <hip/hip_ext.h>
 
+#include <atomic>
 #include <cstdlib>
 
 #include "../../include/nhip_challenge_id.h"
@@ -35,8 +38,10 @@ __device__ __forceinline__ void latency_priority() {
 #endif
 
 
-__device__ __forceinline__ Xfe ld_xfe_canon(const uint64_t* __restrict__ w, uint64_t off) {
-    return {to_mont(w[off]), to_mont(w[off + 1]), to_mont(w[off + 2])};
+// an XFE of the batch word buffer as raw Montgomery coefficients (either input form)
+template <bool MW>
+__device__ __forceinline__ Xfe ld_xfe_w(const uint64_t* __restrict__ w, uint64_t off) {
+    return {word_mont<MW>(w[off]), word_mont<MW>(w[off + 1]), word_mont<MW>(w[off + 2])};
 }
 __device__ __forceinline__ Xfe ld_xfe_raw(const uint64_t* __restrict__ w, uint64_t off) {
     return {w[off], w[off + 1], w[off + 2]};
@@ -60,6 +65,7 @@ __device__ __forceinline__ uint64_t root_of_unity(uint32_t log2n) {
 // its degree (lane-parallel: a prover can pad it with zero coefficients) and copies the descriptor
 // out.  Every run of a batch decodes again from the raw words in HBM, so the device phases never
 // depend on host-side parsing.  fail[p] is (re)initialised here: FAIL_DECODE or 0.
+template <bool MW>
 __global__ void __launch_bounds__(64) k_decode(const uint64_t* __restrict__ words, const ProofIn* __restrict__ in,
                                                uint32_t n_proofs, Dims D, uint32_t fs_stride, uint32_t xs_stride,
                                                ProofDesc* __restrict__ desc, FsOp* __restrict__ ops,
@@ -74,7 +80,7 @@ __global__ void __launch_bounds__(64) k_decode(const uint64_t* __restrict__ word
     if (lane == 0) {
         uint64_t perms = 0, perms_lcw = 0;
         const ClaimLoc cl{pin.claim_off, pin.claim_in_n, pin.claim_out_n};
-        uint32_t f = decode_stream(words, pin.off, pin.len, cl, D, spd, ops + (uint64_t)p * fs_stride, perms, perms_lcw);
+        uint32_t f = decode_stream<MW>(words, pin.off, pin.len, cl, D, spd, ops + (uint64_t)p * fs_stride, perms, perms_lcw);
         if (!f && spd.log2_ph != pin.sized_log2_ph) {  // capacity guard: the batch was sized from the header
             f = FAIL_DECODE;
             spd = ProofDesc{};
@@ -128,7 +134,7 @@ __global__ void __launch_bounds__(64) k_decode(const uint64_t* __restrict__ word
 // instructions per permutation again, at ~1.5x the lane-instructions; used for batches small
 // enough that the sponge replay is on the critical path with most SIMDs idle).  Both rows of a
 // pair hold the same state; only row 0 writes.
-template <bool PAIR>
+template <bool PAIR, bool MW>
 __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restrict__ words,
                                                         const ProofDesc* __restrict__ desc,
                                                         const FsOp* __restrict__ ops, uint32_t n_proofs,
@@ -174,7 +180,7 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
                 w = (e < TIP5_RATE && ni < len) ? src[ni] : 0ull;
                 if (e < TIP5_RATE) {
                     const uint32_t rem = len - pos;  // >= 10 except in the last chunk
-                    s = e < rem ? to_mont(cur) : (e == rem ? MONT_ONE : 0ull);
+                    s = e < rem ? word_mont<MW>(cur) : (e == rem ? MONT_ONE : 0ull);
                 }
                 s = permute(s);
             }
@@ -212,6 +218,7 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
 #ifndef NHIP_QUAD_PRIO
 #define NHIP_QUAD_PRIO NHIP_LAT_PRIO
 #endif
+template <bool MW>
 __global__ void __launch_bounds__(1024) k_fs_replay_quad(const uint64_t* __restrict__ words,
                                                        const ProofDesc* __restrict__ desc,
                                                        const FsOp* __restrict__ ops, uint32_t n_proofs,
@@ -251,9 +258,9 @@ __global__ void __launch_bounds__(1024) k_fs_replay_quad(const uint64_t* __restr
                 w0 = nx + e < len ? src[nx + e] : 0ull;
                 w1 = nx + 4 + e < len ? src[nx + 4 + e] : 0ull;
                 w2 = (r2 && nx + 8 + e < len) ? src[nx + 8 + e] : 0ull;
-                s[0] = e < rem ? to_mont(c0) : (e == rem ? MONT_ONE : 0ull);
-                s[1] = 4 + e < rem ? to_mont(c1) : (4 + e == rem ? MONT_ONE : 0ull);
-                if (r2) s[2] = 8 + e < rem ? to_mont(c2) : (8 + e == rem ? MONT_ONE : 0ull);
+                s[0] = e < rem ? word_mont<MW>(c0) : (e == rem ? MONT_ONE : 0ull);
+                s[1] = 4 + e < rem ? word_mont<MW>(c1) : (4 + e == rem ? MONT_ONE : 0ull);
+                if (r2) s[2] = 8 + e < rem ? word_mont<MW>(c2) : (8 + e == rem ? MONT_ONE : 0ull);
                 tip5_permute_quad(s, cq, rck, e, lds.lut);
             }
         } else if (op.kind == FS_SQUEEZE_X) {
@@ -297,6 +304,7 @@ __global__ void __launch_bounds__(1024) k_fs_replay_quad(const uint64_t* __restr
 #ifndef NHIP_ROWS_WAVES
 #define NHIP_ROWS_WAVES 5
 #endif
+template <bool MW>
 __global__ void __launch_bounds__(256, NHIP_ROWS_WAVES) k_hash_rows(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                                    uint32_t n_proofs, uint32_t k, StarkDims dims,
                                                    uint64_t* __restrict__ dig, const uint32_t* __restrict__ fail) {
@@ -324,13 +332,13 @@ __global__ void __launch_bounds__(256, NHIP_ROWS_WAVES) k_hash_rows(const uint64
             const bool last = c + 1 == nchunks;
             if (!last) {
 #pragma unroll
-                for (int q = 0; q < TIP5_RATE; ++q) s[q] = to_mont(row[pos + q]);
+                for (int q = 0; q < TIP5_RATE; ++q) s[q] = word_mont<MW>(row[pos + q]);
             } else {
                 const uint32_t rem = width - pos;
 #pragma unroll
                 for (int q = 0; q < TIP5_RATE; ++q) {
                     const uint32_t qq = (uint32_t)q;
-                    s[q] = qq < rem ? to_mont(row[pos + qq]) : (qq == rem ? MONT_ONE : 0ull);
+                    s[q] = qq < rem ? word_mont<MW>(row[pos + qq]) : (qq == rem ? MONT_ONE : 0ull);
                 }
             }
             tip5_rounds_0_3(s, lds.lut);
@@ -375,6 +383,7 @@ enum : uint64_t { MPS_ARENA = 0, MPS_AUTH = 1, MPS_DIG = 2, MPS_XFE = 3 };
 static constexpr uint64_t MPS_MASK = (1ull << 62) - 1, MPS_NONE = ~0ull;
 __device__ __forceinline__ uint64_t mps(uint64_t type, uint64_t v) { return (type << 62) | v; }
 
+template <bool MW>
 __device__ __forceinline__ void mp_load(uint64_t code, const uint64_t* __restrict__ words,
                                         const uint64_t* __restrict__ dig, const uint64_t* __restrict__ arena,
                                         uint64_t o[5]) {
@@ -385,10 +394,10 @@ __device__ __forceinline__ void mp_load(uint64_t code, const uint64_t* __restric
         for (int q = 0; q < 5; ++q) o[q] = s[q];
     } else if (t == MPS_AUTH) {
 #pragma unroll
-        for (int q = 0; q < 5; ++q) o[q] = to_mont(words[v + q]);
+        for (int q = 0; q < 5; ++q) o[q] = word_mont<MW>(words[v + q]);
     } else {  // an XFE leaf of a FRI codeword: digest [c0, c1, c2, 0, 0]
 #pragma unroll
-        for (int q = 0; q < 3; ++q) o[q] = to_mont(words[v + q]);
+        for (int q = 0; q < 3; ++q) o[q] = word_mont<MW>(words[v + q]);
         o[3] = 0;
         o[4] = 0;
     }
@@ -626,13 +635,14 @@ struct LcwTree {
     uint32_t max_len;   // max last-codeword length over the batch (power of two)
 };
 
+template <bool MW>
 __device__ __forceinline__ void lcw_node(const uint64_t* __restrict__ words, const ProofDesc& d,
                                          const uint64_t* __restrict__ mine, uint32_t v, uint32_t L, uint64_t o[5]) {
     if (v >= L) {
         const uint64_t off = d.last_cw_off + 3ull * (v - L);
-        o[0] = to_mont(words[off]);
-        o[1] = to_mont(words[off + 1]);
-        o[2] = to_mont(words[off + 2]);
+        o[0] = word_mont<MW>(words[off]);
+        o[1] = word_mont<MW>(words[off + 1]);
+        o[2] = word_mont<MW>(words[off + 2]);
         o[3] = 0;
         o[4] = 0;
     } else {
@@ -652,7 +662,7 @@ __device__ __forceinline__ void lcw_node(const uint64_t* __restrict__ words, con
 #ifndef NHIP_MP_WAVES_SMALL
 #define NHIP_MP_WAVES_SMALL 7
 #endif
-template <int WAVES>
+template <int WAVES, bool MW>
 __global__ void __launch_bounds__(256, WAVES) k_mp_hash(const uint64_t* __restrict__ words, const uint64_t* __restrict__ dig,
                                                  MpPlan plan, uint32_t lvl, uint32_t mp_blocks,
                                                  const ProofDesc* __restrict__ desc, uint32_t n_proofs,
@@ -684,8 +694,8 @@ __global__ void __launch_bounds__(256, WAVES) k_mp_hash(const uint64_t* __restri
             if (i < (L >> (lvl + 1))) {
                 const uint32_t v = (L >> (lvl + 1)) + i;
                 uint64_t* mine = lcw.nodes + (uint64_t)p * lcw.max_len * 5;
-                lcw_node(words, d, mine, 2 * v, L, s);
-                lcw_node(words, d, mine, 2 * v + 1, L, s + 5);
+                lcw_node<MW>(words, d, mine, 2 * v, L, s);
+                lcw_node<MW>(words, d, mine, 2 * v + 1, L, s + 5);
                 o = mine + 5ull * v;
                 work = true;
             }
@@ -699,8 +709,8 @@ __global__ void __launch_bounds__(256, WAVES) k_mp_hash(const uint64_t* __restri
             if (g - s_base[sh] < s_cnt[sh]) {
                 const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
                 if (lc != MPS_NONE) {  // else: op of a tree that already failed
-                    mp_load(lc, words, dig, plan.arena, s);
-                    mp_load(rc, words, dig, plan.arena, s + 5);
+                    mp_load<MW>(lc, words, dig, plan.arena, s);
+                    mp_load<MW>(rc, words, dig, plan.arena, s + 5);
                     o = plan.arena + 5 * g;
                     work = true;
                 }
@@ -716,24 +726,27 @@ __global__ void __launch_bounds__(256, WAVES) k_mp_hash(const uint64_t* __restri
 // Small levels (the last levels of the tallest trees): a lane-per-op permutation is a ~20 us
 // dependent instruction chain however few ops there are, so these levels use the 16-lane row
 // Tip5 (one op per DPP row, ~8x shorter chain) instead.
+template <bool MW>
 __device__ __forceinline__ uint64_t mp_load_word(uint64_t code, uint32_t e, const uint64_t* __restrict__ words,
                                                  const uint64_t* __restrict__ dig, const uint64_t* __restrict__ arena) {
     const uint64_t t = code >> 62, v = code & MPS_MASK;
     if (t == MPS_ARENA) return arena[5 * v + e];
     if (t == MPS_DIG) return dig[5 * v + e];
-    if (t == MPS_AUTH) return to_mont(words[v + e]);
-    return e < 3 ? to_mont(words[v + e]) : 0ull;  // XFE leaf [c0, c1, c2, 0, 0]
+    if (t == MPS_AUTH) return word_mont<MW>(words[v + e]);
+    return e < 3 ? word_mont<MW>(words[v + e]) : 0ull;  // XFE leaf [c0, c1, c2, 0, 0]
 }
 
 // Word e of a last-codeword tree node v (lcw_node, one word per lane of the row).
+template <bool MW>
 __device__ __forceinline__ uint64_t lcw_node_word(const uint64_t* __restrict__ words, const ProofDesc& d,
                                                   const uint64_t* __restrict__ mine, uint32_t v, uint32_t L, uint32_t e) {
-    if (v >= L) return e < 3 ? to_mont(words[d.last_cw_off + 3ull * (v - L) + e]) : 0ull;
+    if (v >= L) return e < 3 ? word_mont<MW>(words[d.last_cw_off + 3ull * (v - L) + e]) : 0ull;
     return mine[5ull * v + e];
 }
 
 // Rows [0, mp_rows) take the multiproof ops of level `lvl`; rows past them the level-`lvl` parents of
 // every proof's last-codeword tree (the same mapping as k_mp_hash's lcw blocks, one parent per row).
+template <bool MW>
 __global__ void __launch_bounds__(256) k_mp_hash_wide(const uint64_t* __restrict__ words,
                                                       const uint64_t* __restrict__ dig, MpPlan plan, uint32_t lvl,
                                                       uint64_t mp_rows, const ProofDesc* __restrict__ desc,
@@ -763,8 +776,8 @@ __global__ void __launch_bounds__(256) k_mp_hash_wide(const uint64_t* __restrict
         if (g - s_base[sh] >= s_cnt[sh]) return;
         const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
         if (lc == MPS_NONE) return;  // op of a tree that already failed
-        if (e < 5) s = mp_load_word(lc, e, words, dig, plan.arena);
-        else if (e < 10) s = mp_load_word(rc, e - 5, words, dig, plan.arena);
+        if (e < 5) s = mp_load_word<MW>(lc, e, words, dig, plan.arena);
+        else if (e < 10) s = mp_load_word<MW>(rc, e - 5, words, dig, plan.arena);
         o = plan.arena + 5 * g;
     } else {
         const uint32_t per = lcw.max_len >> (lvl + 1);
@@ -776,8 +789,8 @@ __global__ void __launch_bounds__(256) k_mp_hash_wide(const uint64_t* __restrict
         if (i >= (L >> (lvl + 1))) return;
         const uint32_t v = (L >> (lvl + 1)) + i;
         uint64_t* mine = lcw.nodes + (uint64_t)p * lcw.max_len * 5;
-        if (e < 5) s = lcw_node_word(words, d, mine, 2 * v, L, e);
-        else if (e < 10) s = lcw_node_word(words, d, mine, 2 * v + 1, L, e - 5);
+        if (e < 5) s = lcw_node_word<MW>(words, d, mine, 2 * v, L, e);
+        else if (e < 10) s = lcw_node_word<MW>(words, d, mine, 2 * v + 1, L, e - 5);
         o = mine + 5ull * v;
     }
     uint64_t rcs[TIP5_ROUNDS];
@@ -798,6 +811,7 @@ struct TailCaps {
     uint32_t cap[MP_TAIL_LEVELS_MAX];
 };
 
+template <bool MW>
 __global__ void __launch_bounds__(MP_TAIL_THREADS) k_mp_hash_tail(const uint64_t* __restrict__ words,
                                                                  const uint64_t* __restrict__ dig, MpPlan plan,
                                                                  uint32_t lvl0, uint32_t lvl1, TailCaps caps,
@@ -841,8 +855,8 @@ __global__ void __launch_bounds__(MP_TAIL_THREADS) k_mp_hash_tail(const uint64_t
                 if (g - s_base[sh] >= s_cnt[sh]) continue;
                 const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
                 if (lc == MPS_NONE) continue;
-                if (e < 5) st = mp_load_word(lc, e, words, dig, plan.arena);
-                else if (e < 10) st = mp_load_word(rc, e - 5, words, dig, plan.arena);
+                if (e < 5) st = mp_load_word<MW>(lc, e, words, dig, plan.arena);
+                else if (e < 10) st = mp_load_word<MW>(rc, e - 5, words, dig, plan.arena);
                 o = plan.arena + 5 * g;
             } else {
                 const uint64_t q = row - mp_rows;
@@ -853,8 +867,8 @@ __global__ void __launch_bounds__(MP_TAIL_THREADS) k_mp_hash_tail(const uint64_t
                 if (i >= (L >> (lvl + 1))) continue;
                 const uint32_t v = (L >> (lvl + 1)) + i;
                 uint64_t* mine = lcw.nodes + (uint64_t)p * lcw.max_len * 5;
-                if (e < 5) st = lcw_node_word(words, d, mine, 2 * v, L, e);
-                else if (e < 10) st = lcw_node_word(words, d, mine, 2 * v + 1, L, e - 5);
+                if (e < 5) st = lcw_node_word<MW>(words, d, mine, 2 * v, L, e);
+                else if (e < 10) st = lcw_node_word<MW>(words, d, mine, 2 * v + 1, L, e - 5);
                 o = mine + 5ull * v;
             }
             st = tip5_permute_wide<true>(st, e, rcs, t5.lut);
@@ -871,6 +885,7 @@ __global__ void __launch_bounds__(MP_TAIL_THREADS) k_mp_hash_tail(const uint64_t
 // is most of a small batch's Merkle phase.  A tree's parents depend only on its own earlier
 // levels, its leaves (row digests, done before this launch) and proof words.
 static constexpr uint32_t MP_CLIMB_THREADS = 1024;
+template <bool MW>
 __global__ void __launch_bounds__(MP_CLIMB_THREADS) k_mp_climb(const uint64_t* __restrict__ words,
                                                                const uint64_t* __restrict__ dig, MpPlan plan,
                                                                uint32_t trees_per_proof,
@@ -895,8 +910,8 @@ __global__ void __launch_bounds__(MP_CLIMB_THREADS) k_mp_climb(const uint64_t* _
             for (uint32_t row = row0; row < cnt; row += ROWS) {  // uniform within the 16-lane row
                 const uint32_t v = cnt + row;
                 uint64_t st = MONT_ONE;
-                if (e < 5) st = lcw_node_word(words, d, mine, 2 * v, L, e);
-                else if (e < 10) st = lcw_node_word(words, d, mine, 2 * v + 1, L, e - 5);
+                if (e < 5) st = lcw_node_word<MW>(words, d, mine, 2 * v, L, e);
+                else if (e < 10) st = lcw_node_word<MW>(words, d, mine, 2 * v + 1, L, e - 5);
                 st = tip5_permute_wide<true>(st, e, rcs, t5.lut);
                 if (e < 5) mine[5ull * v + e] = st;
             }
@@ -915,8 +930,8 @@ __global__ void __launch_bounds__(MP_CLIMB_THREADS) k_mp_climb(const uint64_t* _
             const uint64_t lc = plan.ops[2 * g], rc = plan.ops[2 * g + 1];
             if (lc == MPS_NONE) continue;  // a tree that already failed
             uint64_t st = MONT_ONE;
-            if (e < 5) st = mp_load_word(lc, e, words, dig, plan.arena);
-            else if (e < 10) st = mp_load_word(rc, e - 5, words, dig, plan.arena);
+            if (e < 5) st = mp_load_word<MW>(lc, e, words, dig, plan.arena);
+            else if (e < 10) st = mp_load_word<MW>(rc, e - 5, words, dig, plan.arena);
             st = tip5_permute_wide<true>(st, e, rcs, t5.lut);
             if (e < 5) plan.arena[5 * g + e] = st;
         }
@@ -926,6 +941,7 @@ __global__ void __launch_bounds__(MP_CLIMB_THREADS) k_mp_climb(const uint64_t* _
 
 // One lane per (proof, tree): duplicate leaf indices carry equal digests, final node == root.
 // Lanes n_records.. check the last codeword's Merkle root, one per proof.
+template <bool MW>
 __global__ void k_mp_roots(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                            const uint64_t* __restrict__ dig, MpPlan plan, uint32_t n_records, uint32_t trees_per_proof,
                            uint32_t k, uint32_t* __restrict__ fail, uint32_t n_proofs, LcwTree lcw) {
@@ -935,10 +951,10 @@ __global__ void k_mp_roots(const uint64_t* __restrict__ words, const ProofDesc* 
         if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
         const ProofDesc& d = desc[p];
         uint64_t v[5];
-        lcw_node(words, d, lcw.nodes + (uint64_t)p * lcw.max_len * 5, 1, d.last_cw_n, v);
+        lcw_node<MW>(words, d, lcw.nodes + (uint64_t)p * lcw.max_len * 5, 1, d.last_cw_n, v);
         bool ok = true;
 #pragma unroll
-        for (int q = 0; q < 5; ++q) ok &= v[q] == to_mont(words[d.fri_root[d.R] + q]);
+        for (int q = 0; q < 5; ++q) ok &= v[q] == word_mont<MW>(words[d.fri_root[d.R] + q]);
         if (!ok) atomicOr(&fail[p], FAIL_FRI_LAST_ROOT);
         return;
     }
@@ -951,15 +967,15 @@ __global__ void k_mp_roots(const uint64_t* __restrict__ words, const ProofDesc* 
     bool ok = true;
     for (uint32_t j = 0; j < nd; ++j) {
         uint64_t a[5], b[5];
-        mp_load(mp_leaf_code(d, p, tree, k, plan.dups[(grp_id * k + j) * 2]), words, dig, nullptr, a);
-        mp_load(mp_leaf_code(d, p, tree, k, plan.dups[(grp_id * k + j) * 2 + 1]), words, dig, nullptr, b);
+        mp_load<MW>(mp_leaf_code(d, p, tree, k, plan.dups[(grp_id * k + j) * 2]), words, dig, nullptr, a);
+        mp_load<MW>(mp_leaf_code(d, p, tree, k, plan.dups[(grp_id * k + j) * 2 + 1]), words, dig, nullptr, b);
 #pragma unroll
         for (int q = 0; q < 5; ++q) ok &= a[q] == b[q];
     }
     uint64_t v[5];
-    mp_load(r.code, words, dig, plan.arena, v);
+    mp_load<MW>(r.code, words, dig, plan.arena, v);
 #pragma unroll
-    for (int q = 0; q < 5; ++q) ok &= v[q] == to_mont(words[r.root_off + q]);
+    for (int q = 0; q < 5; ++q) ok &= v[q] == word_mont<MW>(words[r.root_off + q]);
     if (!ok) atomicOr(&fail[p], r.fail_bit);
 }
 
@@ -1040,7 +1056,7 @@ __device__ Xfe eval_terminal_wave(uint32_t n, Xfe c, Sym sym) {
 #ifndef NHIP_OOD_WAVES
 #define NHIP_OOD_WAVES 1
 #endif
-template <uint32_t BLOCK>
+template <uint32_t BLOCK, bool MW>
 __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_ood_air(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                                  uint32_t n_proofs, StarkDims dims, const OodIns* __restrict__ prog,
                                                  const uint32_t* __restrict__ prog_off, uint32_t n_levels,
@@ -1093,15 +1109,15 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
         // folded from 1 with its named sampled indeterminate (wave 3, lane-parallel)
         auto chal = [&](uint32_t i) { return ld_xfe_raw(xs, xb + 3ull * (sl.chal + i)); };
         const Xfe ein = eval_terminal_wave(d.claim_in_n, chal(CH_STANDARD_INPUT),
-                                           [&](uint32_t i) { return to_mont(words[d.claim_in_off + i]); });
+                                           [&](uint32_t i) { return word_mont<MW>(words[d.claim_in_off + i]); });
         const Xfe eout = eval_terminal_wave(d.claim_out_n, chal(CH_STANDARD_OUTPUT),
-                                            [&](uint32_t i) { return to_mont(words[d.claim_out_off + i]); });
+                                            [&](uint32_t i) { return word_mont<MW>(words[d.claim_out_off + i]); });
         const Xfe lut = eval_terminal_wave(256u, chal(CH_LOOKUP_TABLE_PUBLIC), [&](uint32_t i) {
             const uint64_t y = i + 1;  // tip5::LOOKUP_TABLE[i] = (i + 1)^3 - 1 mod 257
             return to_mont((y * y % 257u * y % 257u + 256u) % 257u);
         });
         const Xfe comp = eval_terminal_wave(5u, chal(CH_COMPRESS_PROGRAM_DIGEST),
-                                            [&](uint32_t i) { return to_mont(words[d.claim_digest_off + i]); });
+                                            [&](uint32_t i) { return word_mont<MW>(words[d.claim_digest_off + i]); });
         if (tid == 192) {
             chal_derived[0] = ein;
             chal_derived[1] = eout;
@@ -1119,10 +1135,10 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
         if (t == 1) return consts[ref & 0x3FFFFFFFu];
         const uint32_t kind = (ref >> 27) & 7u, i = ref & 0x7FFFFFFu;
         switch (kind) {
-            case IN_MAIN_CURR: return ld_xfe_canon(words, d.ood_mc + 3ull * i);
-            case IN_AUX_CURR: return ld_xfe_canon(words, d.ood_ac + 3ull * i);
-            case IN_MAIN_NEXT: return ld_xfe_canon(words, d.ood_mn + 3ull * i);
-            case IN_AUX_NEXT: return ld_xfe_canon(words, d.ood_an + 3ull * i);
+            case IN_MAIN_CURR: return ld_xfe_w<MW>(words, d.ood_mc + 3ull * i);
+            case IN_AUX_CURR: return ld_xfe_w<MW>(words, d.ood_ac + 3ull * i);
+            case IN_MAIN_NEXT: return ld_xfe_w<MW>(words, d.ood_mn + 3ull * i);
+            case IN_AUX_NEXT: return ld_xfe_w<MW>(words, d.ood_an + 3ull * i);
             default:
                 return i < dims.num_sampled ? ld_xfe_raw(xs, xb + 3ull * (sl.chal + i)) : chal_derived[i - dims.num_sampled];
         }
@@ -1152,8 +1168,8 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
     Xfe lc = x_zero(), ln = x_zero();
     for (uint32_t c = tid; c < M + A; c += blockDim.x) {
         const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + c));
-        const Xfe vc = c < M ? ld_xfe_canon(words, d.ood_mc + 3ull * c) : ld_xfe_canon(words, d.ood_ac + 3ull * (c - M));
-        const Xfe vn = c < M ? ld_xfe_canon(words, d.ood_mn + 3ull * c) : ld_xfe_canon(words, d.ood_an + 3ull * (c - M));
+        const Xfe vc = c < M ? ld_xfe_w<MW>(words, d.ood_mc + 3ull * c) : ld_xfe_w<MW>(words, d.ood_ac + 3ull * (c - M));
+        const Xfe vn = c < M ? ld_xfe_w<MW>(words, d.ood_mn + 3ull * c) : ld_xfe_w<MW>(words, d.ood_an + 3ull * (c - M));
         lc = x_add(lc, x_mul(w, vc));
         ln = x_add(ln, x_mul(w, vn));
     }
@@ -1162,7 +1178,7 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
     if (tid == 0) {
         Xfe seg = x_zero(), zk = x_one(), qlin = x_zero();
         for (uint32_t q = 0; q < Q; ++q) {
-            const Xfe sq = ld_xfe_canon(words, d.ood_qs + 3ull * q);
+            const Xfe sq = ld_xfe_w<MW>(words, d.ood_qs + 3ull * q);
             seg = x_add(seg, x_mul(zk, sq));
             zk = x_mul(zk, z);
             qlin = x_add(qlin, x_mul(ld_xfe_raw(xs, xb + 3ull * (sl.lin_w + M + A + q)), sq));
@@ -1198,6 +1214,7 @@ __device__ __forceinline__ uint64_t lds_pow(const uint64_t* __restrict__ sq, uin
 #ifndef NHIP_FRI_WAVES
 #define NHIP_FRI_WAVES 1
 #endif
+template <bool MW>
 __global__ void __launch_bounds__(256, NHIP_FRI_WAVES) k_fri(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                              uint32_t n_proofs, StarkDims dims, const uint64_t* __restrict__ xs,
                                              const uint32_t* __restrict__ idx_all, uint64_t* __restrict__ xdom,
@@ -1227,20 +1244,20 @@ __global__ void __launch_bounds__(256, NHIP_FRI_WAVES) k_fri(const uint64_t* __r
     uint32_t f = 0;
     if (tid < k) {
         const uint32_t i0 = idx[tid];
-        Xfe a = ld_xfe_canon(words, d.fri[0].leaves_off + 3ull * tid);
+        Xfe a = ld_xfe_w<MW>(words, d.fri[0].leaves_off + 3ull * tid);
         uint64_t x = mont_mul(to_mont(7), lds_pow(gsq, i0));
         xdom[(uint64_t)p * k + tid] = x;
         uint64_t xinv = b_inv(x);
         const uint64_t neg_half = to_mont((GL_P - 1) / 2);  // -1/2
         for (uint32_t r = 0; r < d.R; ++r) {
-            const Xfe b = ld_xfe_canon(words, d.fri[1 + r].leaves_off + 3ull * tid);
+            const Xfe b = ld_xfe_w<MW>(words, d.fri[1 + r].leaves_off + 3ull * tid);
             const Xfe alpha = ld_xfe_raw(xs, xb + 3ull * (sl.alpha + r));
             const Xfe slope = x_scale(x_sub(b, a), mont_mul(neg_half, xinv));
             a = x_add(a, x_mul(slope, x_sub(alpha, x_lift(x))));
             x = mont_mul(x, x);
             xinv = mont_mul(xinv, xinv);
         }
-        const Xfe last = ld_xfe_canon(words, d.last_cw_off + 3ull * (i0 & (L - 1)));
+        const Xfe last = ld_xfe_w<MW>(words, d.last_cw_off + 3ull * (i0 & (L - 1)));
         if (!x_eq(last, a)) f |= FAIL_FRI_LAST_AGREE;
     }
     // barycentric evaluation of the last codeword at the indeterminate vs Horner of the polynomial
@@ -1254,7 +1271,7 @@ __global__ void __launch_bounds__(256, NHIP_FRI_WAVES) k_fri(const uint64_t* __r
         // form, so num / den are those of the reference's per-point inverses in every case
         auto term = [&](uint32_t i, uint64_t w, Xfe inv) {
             const Xfe q = x_scale(inv, w);
-            num = x_add(num, x_mul(q, ld_xfe_canon(words, d.last_cw_off + 3ull * i)));
+            num = x_add(num, x_mul(q, ld_xfe_w<MW>(words, d.last_cw_off + 3ull * i)));
             den = x_add(den, q);
         };
         uint32_t i = tid;
@@ -1296,7 +1313,7 @@ __global__ void __launch_bounds__(256, NHIP_FRI_WAVES) k_fri(const uint64_t* __r
         Xfe pw = x_one();
         for (uint32_t j = 0; (c >> j) != 0; ++j)
             if ((c >> j) & 1u) pw = x_mul(pw, tpow[j]);
-        hp = x_add(hp, x_mul(pw, ld_xfe_canon(words, d.last_poly_off + 3ull * c)));
+        hp = x_add(hp, x_mul(pw, ld_xfe_w<MW>(words, d.last_poly_off + 3ull * c)));
     }
     const Xfe h = block_sum_xfe(hp, red);
     if (tid == 0) {
@@ -1308,17 +1325,19 @@ __global__ void __launch_bounds__(256, NHIP_FRI_WAVES) k_fri(const uint64_t* __r
 }
 
 // ------------------------------------------------------------------ DEEP
-// One workgroup per proof, thread (s, j) = chunk s of the columns of revealed row j (S chunks per
-// row, S * k <= 256).  Row linear combinations sum_c w_c * row_c are accumulated lazily: the proof
-// words are canonical, the weights raw Montgomery (w R); each weight is split into 32-bit halves and
-// each word into 16-bit limbs, so every partial product is < 2^48 and a 64-bit accumulator per
-// (coefficient, weight half, limb) absorbs up to 2^16 of them without carries (one v_mad_u64_u32
-// per partial product).  The accumulators are folded and reduced once per thread; the result,
-// R * sum w x mod p, is already the raw Montgomery word of the sum.  An XFE product w * x is
-// sum_m x_m * (w X^m) with w X = (-w2, w0 + w2, w1) and w X^2 = (-w1, w1 - w2, w0 + w2) (X^3 = X - 1),
-// precomputed per aux column in LDS.  Then thread j takes row j's three DEEP terms (x - z,
-// x - z w_trace, x - z^Q; x from k_fri), inverts their product once (Montgomery's trick), and
-// compares the recombined value with the FRI round-0 leaf.
+// One workgroup per proof; lane (r, q) of the 256 threads takes words q, q + 8, q + 16, ... of
+// revealed row r of the current pass (32 rows per pass), so one load instruction of a wave reads
+// 8 rows x 64 contiguous bytes.  Row linear combinations sum_c w_c * row_c are accumulated lazily:
+// the weights are raw Montgomery (w R), split into 22 / 22 / 20-bit limbs; each proof word enters as
+// its two 32-bit halves, so every partial product is < 2^54 and one 64-bit accumulator per (limb,
+// half) takes a whole row share without carries (one v_mad_u64_u32 per partial product).  Each
+// lane reduces its accumulators once, the 8 lanes of a row add theirs (3 xor shuffles): with
+// canonical words the sum R * sum w x mod p is the raw Montgomery word of the combination; with
+// Montgomery words (x R) it is R^2 * sum w x, and one from_mont makes it the same word.  An XFE
+// product w * x is sum_m x_m * (w X^m) with w X = (-w2, w0 + w2, w1) and w X^2 = (-w1, w1 - w2,
+// w0 + w2) (X^3 = X - 1), precomputed per aux column in LDS.  Then thread j takes row j's three DEEP
+// terms (x - z, x - z w_trace, x - z^Q; x from k_fri), inverts their product once (Montgomery's
+// trick), and compares the recombined value with the FRI round-0 leaf.
 typedef unsigned __int128 u128_t;
 static constexpr uint32_t DEEP_UNROLL = 8;
 
@@ -1329,174 +1348,17 @@ __device__ __forceinline__ uint64_t reduce_u108(u128_t y) {
     return gl_sub(r, y1 >> 32);  // 2^96 == -1 (mod p)
 }
 
-// (sum_{h<2, q<4} a[h][q] * 2^(32h + 16q)) mod p, a < 2^59
-__device__ __forceinline__ uint64_t limb_reduce(const uint64_t (&a)[8]) {
-    const u128_t U = (u128_t)a[0] + ((u128_t)a[1] << 16) + ((u128_t)a[2] << 32) + ((u128_t)a[3] << 48);
-    const u128_t W = (u128_t)a[4] + ((u128_t)a[5] << 16) + ((u128_t)a[6] << 32) + ((u128_t)a[7] << 48);
-    const uint64_t ur = reduce_u108(U), wr = reduce_u108(W);
-    return gl_add(ur, reduce96(wr << 32, (uint32_t)(wr >> 32)));  // + wr * 2^32
-}
-
-__device__ __forceinline__ void limb_mac(uint64_t (&a)[8], uint64_t w, const uint32_t (&xq)[4]) {
-    const uint32_t w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        a[q] += (uint64_t)w0 * xq[q];
-        a[4 + q] += (uint64_t)w1 * xq[q];
-    }
-}
-
-__device__ __forceinline__ void limbs16(uint64_t x, uint32_t (&xq)[4]) {
-    xq[0] = (uint32_t)x & 0xFFFFu;
-    xq[1] = (uint32_t)x >> 16;
-    xq[2] = (uint32_t)(x >> 32) & 0xFFFFu;
-    xq[3] = (uint32_t)(x >> 48);
-}
-
-__global__ void __launch_bounds__(256) k_deep(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
-                                              uint32_t n_proofs, StarkDims dims, uint32_t S,
-                                              const uint64_t* __restrict__ xs, const uint64_t* __restrict__ xdom,
-                                              const uint64_t* __restrict__ ood, uint32_t* __restrict__ fail) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t M = dims.num_main, A = dims.num_aux, Q = dims.num_quot_seg, k = dims.num_checks;
-    uint64_t* wm = reinterpret_cast<uint64_t*>(smem);  // [M][3] main weights (raw)
-    uint64_t* wa = wm + 3 * M;                         // [A][3 m][3 coeff] aux weights w X^m (raw)
-    Xfe* part = reinterpret_cast<Xfe*>(wa + 9 * A);    // [S][k] chunk sums (raw)
-    __shared__ Xfe s_quot[MAX_CHECKS];
-    __shared__ Xfe s_at[3];
-    const uint32_t p = blockIdx.x, tid = threadIdx.x;
-    if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
-    const ProofDesc& d = desc[p];
-    const SampleLayout sl = SampleLayout::of(dims, d.R);
-    const uint64_t xb = d.xs_off * 3;
-    const uint64_t* __restrict__ lw = xs + xb + 3ull * sl.lin_w;
-    for (uint32_t i = tid; i < 3 * M; i += blockDim.x) wm[i] = lw[i];
-    for (uint32_t c = tid; c < A; c += blockDim.x) {
-        const uint64_t w0 = lw[3 * (M + c)], w1 = lw[3 * (M + c) + 1], w2 = lw[3 * (M + c) + 2];
-        uint64_t* o = wa + 9 * c;
-        o[0] = w0, o[1] = w1, o[2] = w2;
-        o[3] = gl_sub(0, w2), o[4] = gl_add(w0, w2), o[5] = w1;
-        o[6] = gl_sub(0, w1), o[7] = gl_sub(w1, w2), o[8] = gl_add(w0, w2);
-    }
-    if (tid == blockDim.x - 1) {
-        // evaluation points of the three DEEP terms: z, z * w_trace, z^Q
-        const Xfe z = ld_xfe_raw(xs, xb + 3ull * sl.z);
-        s_at[0] = z;
-        s_at[1] = x_scale(z, root_of_unity(d.log2_ph));
-        Xfe zq = x_one();
-        for (uint32_t q = 0; q < Q; ++q) zq = x_mul(zq, z);
-        s_at[2] = zq;
-    }
-    __syncthreads();
-    const uint32_t s = tid / k, j = tid - s * k;
-    if (s < S) {
-        uint64_t acc[3][8];
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-#pragma unroll
-            for (int q = 0; q < 8; ++q) acc[c][q] = 0;
-        // the row words are read DEEP_UNROLL at a time so that many loads are in flight per lane
-        // (the lanes of a wave read different rows: the kernel is load-latency-bound otherwise)
-        const uint64_t* __restrict__ mrow = words + d.main_rows_off + (uint64_t)j * M;
-        uint32_t c = s * M / S;
-        const uint32_t ce = (s + 1) * M / S;
-        for (; c + DEEP_UNROLL <= ce; c += DEEP_UNROLL) {
-            uint64_t xv[DEEP_UNROLL];
-#pragma unroll
-            for (uint32_t u = 0; u < DEEP_UNROLL; ++u) xv[u] = mrow[c + u];
-#pragma unroll
-            for (uint32_t u = 0; u < DEEP_UNROLL; ++u) {
-                uint32_t xq[4];
-                limbs16(xv[u], xq);
-                limb_mac(acc[0], wm[3 * (c + u)], xq);
-                limb_mac(acc[1], wm[3 * (c + u) + 1], xq);
-                limb_mac(acc[2], wm[3 * (c + u) + 2], xq);
-            }
-        }
-        for (; c < ce; ++c) {
-            uint32_t xq[4];
-            limbs16(mrow[c], xq);
-            limb_mac(acc[0], wm[3 * c], xq);
-            limb_mac(acc[1], wm[3 * c + 1], xq);
-            limb_mac(acc[2], wm[3 * c + 2], xq);
-        }
-        const uint64_t* __restrict__ arow = words + d.aux_rows_off + (uint64_t)j * 3 * A;
-        uint32_t ca = s * A / S;
-        const uint32_t cae = (s + 1) * A / S;
-        for (; ca < cae; ca += DEEP_UNROLL / 2) {
-            const uint32_t nc = cae - ca < DEEP_UNROLL / 2 ? cae - ca : DEEP_UNROLL / 2;
-            uint64_t xv[3 * (DEEP_UNROLL / 2)];
-#pragma unroll
-            for (uint32_t u = 0; u < 3 * (DEEP_UNROLL / 2); ++u) xv[u] = u < 3 * nc ? arow[3 * ca + u] : 0ull;
-#pragma unroll
-            for (uint32_t u = 0; u < DEEP_UNROLL / 2; ++u) {
-                if (u >= nc) break;
-                const uint64_t* ww = wa + 9 * (ca + u);
-#pragma unroll
-                for (int m = 0; m < 3; ++m) {
-                    uint32_t xq[4];
-                    limbs16(xv[3 * u + m], xq);
-                    limb_mac(acc[0], ww[3 * m], xq);
-                    limb_mac(acc[1], ww[3 * m + 1], xq);
-                    limb_mac(acc[2], ww[3 * m + 2], xq);
-                }
-            }
-        }
-        part[s * k + j] = {limb_reduce(acc[0]), limb_reduce(acc[1]), limb_reduce(acc[2])};
-        if (s == S - 1) {
-            // quotient segments: sum_q w_q * seg_q (canonical products of raw weights and words)
-            Xfe qv = x_zero();
-            for (uint32_t q = 0; q < Q; ++q)
-                qv = x_add(qv, x_mul(ld_xfe_raw(lw, 3ull * (M + A + q)),
-                                     ld_xfe_raw(words, d.quot_rows_off + (uint64_t)j * 3 * Q + 3ull * q)));
-            s_quot[j] = {to_mont(qv.c0), to_mont(qv.c1), to_mont(qv.c2)};
-        }
-    }
-    __syncthreads();
-    uint32_t f = 0;
-    for (uint32_t j2 = tid; j2 < k; j2 += blockDim.x) {
-        Xfe row = part[j2];
-        for (uint32_t q = 1; q < S; ++q) row = x_add(row, part[q * k + j2]);
-        const Xfe x = x_lift(xdom[(uint64_t)p * k + j2]);
-        const Xfe d0 = x_sub(x, s_at[0]), d1 = x_sub(x, s_at[1]), d2 = x_sub(x, s_at[2]);
-        const Xfe d01 = x_mul(d0, d1);
-        const Xfe prod = x_mul(d01, d2);
-        if (x_is_zero(prod)) {
-            f |= FAIL_ZERO_INVERSE;
-            continue;
-        }
-        const Xfe inv = x_inv(prod);
-        const Xfe inv2 = x_mul(inv, d01);   // 1 / d2
-        const Xfe inv01 = x_mul(inv, d2);   // 1 / (d0 d1)
-        const Xfe inv0 = x_mul(inv01, d1);  // 1 / d0
-        const Xfe inv1 = x_mul(inv01, d0);  // 1 / d1
-        const uint64_t* __restrict__ oo = ood + (uint64_t)p * 9;
-        const uint64_t* __restrict__ wd = lw + 3ull * (M + A + Q);
-        const Xfe t0 = x_mul(x_mul(x_sub(row, ld_xfe_raw(oo, 0)), inv0), ld_xfe_raw(wd, 0));
-        const Xfe t1 = x_mul(x_mul(x_sub(row, ld_xfe_raw(oo, 3)), inv1), ld_xfe_raw(wd, 3));
-        const Xfe t2 = x_mul(x_mul(x_sub(s_quot[j2], ld_xfe_raw(oo, 6)), inv2), ld_xfe_raw(wd, 6));
-        const Xfe deep = x_add(x_add(t0, t1), t2);
-        const Xfe fri_v = ld_xfe_canon(words, d.fri[0].leaves_off + 3ull * j2);
-        if (!x_eq(deep, fri_v)) f |= FAIL_DEEP;
-    }
-    if (f) atomicOr(&fail[p], f);
-}
-
-// DEEP with eight lanes per revealed row (the default; NHIP_DEEP_ROWS8=0 selects k_deep): lane (r, q) of a
-// 256-thread workgroup takes words q, q + 8, q + 16, ... of row r of the current pass (32 rows per
-// pass), so one load instruction of a wave reads 8 rows x 64 contiguous bytes instead of 64 rows x
-// 8 bytes.  The same lazy limb accumulation per lane; each lane reduces its three accumulators to
-// field elements, the 8 lanes of a row add them (3 xor shuffles), and the DEEP check is k_deep's.
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
     return (uint64_t)__shfl_xor((long long)v, m);
 }
 
 // k_deep_rows8's accumulation: each weight (raw Montgomery, < 2^64) split into limbs of 22, 22 and
 // 20 bits (held in LDS as one uint4 per XFE coefficient), each proof word into its two 32-bit halves
-// (no extraction instructions); every partial product is < 2^54, so a lane's 81 words per row
-// (379 / 8 main + 264 / 8 aux; at most 2048 / 8 + 2 under dims_from's M + 3A < 2048) fit a 64-bit
-// accumulator per (limb, half) without carries (< 2^62): 6
-// multiply-adds per (word, coefficient) instead of 8 with 16-bit word limbs.
+// (no extraction instructions); every partial product is < 2^54.  A lane takes ceil(M / 8) +
+// ceil(3A / 8) words of a row (81 for triton-vm's 379 / 88 columns; < DEEP_LANE_TERMS_MAX = 258 under
+// dims_from's M + 3A < DEEP_ROW_WORDS_MAX), so each 64-bit accumulator stays below 258 * 2^54 < 2^63
+// (static_assert in kernels.hpp), and wl_reduce's U, W below 2^63 * (1 + 2^22 + 2^44) < 2^108 (its
+// reduce_u108 needs the high word < 2^44).  6 multiply-adds per (word, coefficient).
 __device__ __forceinline__ uint4 w_limbs(uint64_t w) {
     return make_uint4((uint32_t)w & 0x3FFFFFu, (uint32_t)(w >> 22) & 0x3FFFFFu, (uint32_t)(w >> 44), 0u);
 }
@@ -1508,7 +1370,7 @@ __device__ __forceinline__ void wl_mac(uint64_t (&a)[6], uint4 wl, uint32_t x0, 
     a[4] += (uint64_t)wl.y * x1;
     a[5] += (uint64_t)wl.z * x1;
 }
-// (sum_{i<3, h<2} a[3h + i] * 2^(22 i + 32 h)) mod p, a < 2^62 (U, W < 2^107)
+// (sum_{i<3, h<2} a[3h + i] * 2^(22 i + 32 h)) mod p, a < 2^63 (U, W < 2^108)
 __device__ __forceinline__ uint64_t wl_reduce(const uint64_t (&a)[6]) {
     const u128_t U = (u128_t)a[0] + ((u128_t)a[1] << 22) + ((u128_t)a[2] << 44);
     const u128_t W = (u128_t)a[3] + ((u128_t)a[4] << 22) + ((u128_t)a[5] << 44);
@@ -1522,6 +1384,7 @@ __device__ __forceinline__ uint64_t wl_reduce(const uint64_t (&a)[6]) {
 #ifndef NHIP_DEEP_WAVES
 #define NHIP_DEEP_WAVES 6
 #endif
+template <bool MW>
 __global__ void __launch_bounds__(256, NHIP_DEEP_WAVES) k_deep_rows8(const uint64_t* __restrict__ words,
                                                     const ProofDesc* __restrict__ desc, uint32_t n_proofs,
                                                     StarkDims dims, const uint64_t* __restrict__ xs,
@@ -1623,14 +1486,20 @@ __global__ void __launch_bounds__(256, NHIP_DEEP_WAVES) k_deep_rows8(const uint6
             v1 = gl_add(v1, shfl_xor_u64(v1, m));
             v2 = gl_add(v2, shfl_xor_u64(v2, m));
         }
-        if (j < k && q8 == 0) rowsum[j] = {v0, v1, v2};
+        if (j < k && q8 == 0) {
+            // canonical words: R * sum w x, the raw word; Montgomery words: R^2 * sum w x, one reduction
+            if constexpr (MW) rowsum[j] = {from_mont(v0), from_mont(v1), from_mont(v2)};
+            else rowsum[j] = {v0, v1, v2};
+        }
         if (j < k && q8 == 1) {
-            // quotient segments: sum_q w_q * seg_q (canonical products of raw weights and words)
+            // quotient segments: sum_q w_q * seg_q; Montgomery products of the raw weights with canonical
+            // words are canonical values (to_mont makes them raw), with Montgomery words raw already
             Xfe qv = x_zero();
             for (uint32_t q = 0; q < Q; ++q)
                 qv = x_add(qv, x_mul(ld_xfe_raw(lw, 3ull * (M + A + q)),
                                      ld_xfe_raw(words, d.quot_rows_off + (uint64_t)j * 3 * Q + 3ull * q)));
-            s_quot[j] = {to_mont(qv.c0), to_mont(qv.c1), to_mont(qv.c2)};
+            if constexpr (MW) s_quot[j] = qv;
+            else s_quot[j] = {to_mont(qv.c0), to_mont(qv.c1), to_mont(qv.c2)};
         }
     }
     __syncthreads();
@@ -1656,7 +1525,7 @@ __global__ void __launch_bounds__(256, NHIP_DEEP_WAVES) k_deep_rows8(const uint6
         const Xfe t1 = x_mul(x_mul(x_sub(row, ld_xfe_raw(oo, 3)), inv1), ld_xfe_raw(wd, 3));
         const Xfe t2 = x_mul(x_mul(x_sub(s_quot[j2], ld_xfe_raw(oo, 6)), inv2), ld_xfe_raw(wd, 6));
         const Xfe deep = x_add(x_add(t0, t1), t2);
-        const Xfe fri_v = ld_xfe_canon(words, d.fri[0].leaves_off + 3ull * j2);
+        const Xfe fri_v = ld_xfe_w<MW>(words, d.fri[0].leaves_off + 3ull * j2);
         if (!x_eq(deep, fri_v)) f |= FAIL_DEEP;
     }
     if (f) atomicOr(&fail[p], f);
@@ -1678,20 +1547,9 @@ static bool ood_wide(uint32_t n) {
     return n <= lim;
 }
 
-// DEEP form: k_deep_rows8 (default; config 4 +0.3-1.0% at 512 / 1,024 / 4,096 proofs, 2 alternating
-// repetitions, profiles/r03c) or k_deep (NHIP_DEEP_ROWS8=0, A/B runs)
-static bool deep_rows8() {
-    static const bool on = [] {
-        const char* v = std::getenv("NHIP_DEEP_ROWS8");
-        return !(v && v[0] == '0');
-    }();
-    return on;
-}
-
 // Fiat-Shamir replay form for an n-proof batch (see k_fs_replay_wide / k_fs_replay_quad):
-// 0 = 16-lane row, 1 = two-row pair, 2 = quad.  NHIP_FS_FORM=row|pair|quad forces one (A/B runs;
-// the older NHIP_FS_PAIR=0/1 still selects row / pair).  Read at every launch (one getenv per step)
-// so a test process can run every form on the same proofs.
+// 0 = 16-lane row, 1 = two-row pair, 2 = quad.  A forced form (nhip_set_fs_form: tests and A/B
+// runs; NHIP_FS_FORM=row|pair|quad sets the initial value, read once) overrides the size rule.
 enum FsForm { FS_ROW = 0, FS_PAIR = 1, FS_QUAD = 2 };
 // k_fs_replay_quad workgroup size (NHIP_QUAD_WG = 64..1024 overrides, A/B runs)
 static uint32_t quad_wg() {
@@ -1702,26 +1560,35 @@ static uint32_t quad_wg() {
     }();
     return v;
 }
-static FsForm fs_form(uint32_t n) {
-    const int forced = [] {
+static std::atomic<int>& fs_form_forced() {
+    static std::atomic<int> f([] {
         if (const char* v = std::getenv("NHIP_FS_FORM")) {
             if (v[0] == 'q') return (int)FS_QUAD;
             if (v[0] == 'p') return (int)FS_PAIR;
             if (v[0] == 'r') return (int)FS_ROW;
         }
-        const char* v = std::getenv("NHIP_FS_PAIR");
-        return v ? (v[0] == '1' ? (int)FS_PAIR : (int)FS_ROW) : -1;
-    }();
+        return -1;
+    }());
+    return f;
+}
+int set_fs_form(int form) {
+    if (form < -1 || form > (int)FS_QUAD) return -1;
+    fs_form_forced().store(form, std::memory_order_relaxed);
+    return 0;
+}
+static FsForm fs_form(uint32_t n) {
     static const uint32_t quad_min = [] {
         const char* v = std::getenv("NHIP_FS_QUAD_MIN");
         return v ? (uint32_t)std::strtoul(v, nullptr, 10) : FS_QUAD_MIN_PROOFS;
     }();
+    const int forced = fs_form_forced().load(std::memory_order_relaxed);
     if (forced >= 0) return (FsForm)forced;
     if (n < FS_PAIR_MAX_PROOFS) return FS_PAIR;
     return n >= quad_min ? FS_QUAD : FS_ROW;
 }
 
-hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream_t sa, StarkPhaseTimer* tm) {
+template <bool MW>
+static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStream_t sa, StarkPhaseTimer* tm) {
     const uint32_t n = b.n_proofs;
     if (n == 0) return hipSuccess;
     const uint32_t k = b.dims.num_checks;
@@ -1740,7 +1607,7 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     // the moment decode ends, before the row hashing (main stream, waiting on the same event) can
     // fill the CUs.  Decoding on the main stream instead let k_hash_rows take every wave slot first
     // and stretched the latency-bound sponge replay 1.6 -> 5.0 ms (config 4, one step in flight).
-    hipLaunchKernelGGL(k_decode, dim3(n), dim3(64), 0, sa, b.words, b.in, n, b.D, b.fs_stride, b.xs_stride, b.desc,
+    hipLaunchKernelGGL(k_decode<MW>, dim3(n), dim3(64), 0, sa, b.words, b.in, n, b.D, b.fs_stride, b.xs_stride, b.desc,
                        b.ops, b.fail, b.counters);
     mark(0, sa);
     (void)hipStreamWaitEvent(st, tm->ev[0], 0);
@@ -1751,13 +1618,13 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     // proof (quad form, fewer lane-instructions again).  NHIP_FS_FORM forces one.
     const FsForm ff = fs_form(n);
     if (ff == FS_PAIR)
-        hipLaunchKernelGGL(k_fs_replay_wide<true>, dim3((n * 32 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
+        hipLaunchKernelGGL((k_fs_replay_wide<true, MW>), dim3((n * 32 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
                            b.ops, n, b.xs, b.idx, b.fail);
     else if (ff == FS_QUAD)
-        hipLaunchKernelGGL(k_fs_replay_quad, dim3((n * 4 + quad_wg() - 1) / quad_wg()), dim3(quad_wg()), 0, sa, b.words, b.desc, b.ops, n,
+        hipLaunchKernelGGL(k_fs_replay_quad<MW>, dim3((n * 4 + quad_wg() - 1) / quad_wg()), dim3(quad_wg()), 0, sa, b.words, b.desc, b.ops, n,
                            b.xs, b.idx, b.fail);
     else
-        hipLaunchKernelGGL(k_fs_replay_wide<false>, dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
+        hipLaunchKernelGGL((k_fs_replay_wide<false, MW>), dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
                            b.ops, n, b.xs, b.idx, b.fail);
     mark(1, sa);
     if (k <= 128)
@@ -1772,13 +1639,13 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         const uint64_t rows = (uint64_t)n * k;
         unsigned gx = (unsigned)((rows + 255) / 256);
         if (gx > 16384) gx = 16384;
-        hipLaunchKernelGGL(k_hash_rows, dim3(gx, 3), dim3(256), 0, st, b.words, b.desc, n, k, b.dims, b.dig, b.fail);
+        hipLaunchKernelGGL(k_hash_rows<MW>, dim3(gx, 3), dim3(256), 0, st, b.words, b.desc, n, k, b.dims, b.dig, b.fail);
     }
     mark(2, st);
     if (small) {
         (void)hipStreamWaitEvent(st, tm->ev[1], 0);  // sponge replay done
         mark(13, st);
-        hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), 0, st, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
+        hipLaunchKernelGGL(k_fri<MW>, dim3(n), dim3(256), 0, st, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
         mark(7, st);
     }
     (void)hipStreamWaitEvent(st, tm->ev[3], 0);  // plan done
@@ -1790,28 +1657,22 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         if (!small) (void)hipStreamWaitEvent(sa, tm->ev[10], 0);  // small: OOD right after the plan
         mark(11, sa);
         if (ood_wide(n))
-            hipLaunchKernelGGL(k_ood_air<1024>, dim3(n), dim3(1024), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims,
+            hipLaunchKernelGGL((k_ood_air<1024, MW>), dim3(n), dim3(1024), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims,
                                b.air_prog, b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs, b.ood,
                                b.fail, b.air_lds_slots, b.air_gslots, b.air_gslot_n);
         else
-            hipLaunchKernelGGL(k_ood_air<256>, dim3(n), dim3(b.air_block), b.air_lds_bytes, sa, b.words, b.desc, n,
+            hipLaunchKernelGGL((k_ood_air<256, MW>), dim3(n), dim3(b.air_block), b.air_lds_bytes, sa, b.words, b.desc, n,
                                b.dims, b.air_prog, b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs,
                                b.ood, b.fail, b.air_lds_slots, b.air_gslots, b.air_gslot_n);
         mark(6, sa);
         if (small) {
             (void)hipStreamWaitEvent(sa, tm->ev[7], 0);  // FRI done (main stream)
         } else {
-            hipLaunchKernelGGL(k_fri, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
+            hipLaunchKernelGGL(k_fri<MW>, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
             mark(7, sa);
         }
-        if (deep_rows8()) {
-            hipLaunchKernelGGL(k_deep_rows8, dim3(n), dim3(256), deep_rows8_lds_bytes(b.dims), sa, b.words, b.desc, n,
-                               b.dims, b.xs, b.xdom, b.ood, b.fail);
-        } else {
-            const uint32_t S = deep_chunks(b.dims);
-            hipLaunchKernelGGL(k_deep, dim3(n), dim3(S * k), deep_lds_bytes(b.dims), sa, b.words, b.desc, n, b.dims, S,
-                               b.xs, b.xdom, b.ood, b.fail);
-        }
+        hipLaunchKernelGGL(k_deep_rows8<MW>, dim3(n), dim3(256), deep_rows8_lds_bytes(b.dims), sa, b.words, b.desc, n,
+                           b.dims, b.xs, b.xdom, b.ood, b.fail);
         mark(8, sa);
     };
     uint32_t launches = 0;
@@ -1820,7 +1681,7 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         launch_aux_chain();
         aux_started = true;
         const bool timed = tm->lev[0] != nullptr;
-        hipExtLaunchKernelGGL(k_mp_climb, dim3(n, tpp + 1), dim3(MP_CLIMB_THREADS), 0, st,
+        hipExtLaunchKernelGGL(k_mp_climb<MW>, dim3(n, tpp + 1), dim3(MP_CLIMB_THREADS), 0, st,
                               timed ? tm->lev[0] : nullptr, timed ? tm->lev[1] : nullptr, 0, b.words, b.dig, b.mp,
                               tpp, b.desc, n, (const uint32_t*)b.fail, LcwTree{b.lcw, b.max_lcw});
         launches = 1;
@@ -1851,7 +1712,7 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         if (l == tail0) {
             TailCaps caps{};
             for (uint32_t t = l; t < hash_levels; ++t) caps.cap[t - l] = t < b.mp.levels ? (uint32_t)b.mp_cap_host[t] : 0u;
-            hipExtLaunchKernelGGL(k_mp_hash_tail, dim3(1), dim3(MP_TAIL_THREADS), 0, st, e0, e1, 0, b.words, b.dig,
+            hipExtLaunchKernelGGL(k_mp_hash_tail<MW>, dim3(1), dim3(MP_TAIL_THREADS), 0, st, e0, e1, 0, b.words, b.dig,
                                   b.mp, l, hash_levels, caps, b.desc, n, (const uint32_t*)b.fail, lcw);
             ++launches;
             break;
@@ -1866,13 +1727,13 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
         // (what the rocprofv3 kernel trace reports): the launch's duration without the dispatch
         // gap before it, which a plain event pair around back-to-back launches would also hold
         if (wide)
-            hipExtLaunchKernelGGL(k_mp_hash_wide, dim3((unsigned)(((cap + per * n) * 16 + 255) / 256)), dim3(256), 0,
+            hipExtLaunchKernelGGL(k_mp_hash_wide<MW>, dim3((unsigned)(((cap + per * n) * 16 + 255) / 256)), dim3(256), 0,
                                   st, e0, e1, 0, b.words, b.dig, b.mp, l, cap, b.desc, n, (const uint32_t*)b.fail, lcw);
         else if (n < mp_small_max)
-            hipExtLaunchKernelGGL(k_mp_hash<NHIP_MP_WAVES_SMALL>, dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0,
+            hipExtLaunchKernelGGL((k_mp_hash<NHIP_MP_WAVES_SMALL, MW>), dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0,
                                   e1, 0, b.words, b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw);
         else
-            hipExtLaunchKernelGGL(k_mp_hash<NHIP_MP_WAVES>, dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0, e1, 0,
+            hipExtLaunchKernelGGL((k_mp_hash<NHIP_MP_WAVES, MW>), dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0, e1, 0,
                                   b.words, b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw);
         ++launches;
     }
@@ -1880,7 +1741,7 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     tm->mp_hash_launches = launches;
     mark(4, st);
     const uint32_t nrec = n * tpp;
-    hipLaunchKernelGGL(k_mp_roots, dim3((nrec + n + 255) / 256), dim3(256), 0, st, b.words, b.desc, b.dig, b.mp, nrec,
+    hipLaunchKernelGGL(k_mp_roots<MW>, dim3((nrec + n + 255) / 256), dim3(256), 0, st, b.words, b.desc, b.dig, b.mp, nrec,
                        tpp, k, b.fail, n, lcw);
     mark(5, st);
     (void)hipStreamWaitEvent(st, tm->ev[8], 0);  // join the aux chain
@@ -1889,16 +1750,24 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
     return hipGetLastError();
 }
 
+hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream_t sa, StarkPhaseTimer* tm) {
+    return b.D.mont_words ? launch_phases<true>(b, st, sa, tm) : launch_phases<false>(b, st, sa, tm);
+}
+
+template <bool MW>
+static hipError_t set_attributes() {
+    hipError_t e = hipFuncSetAttribute((const void*)k_ood_air<256, MW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       AIR_LDS_BUDGET);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void*)k_ood_air<1024, MW>, hipFuncAttributeMaxDynamicSharedMemorySize, AIR_LDS_BUDGET);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)k_deep_rows8<MW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024 - 8192);
+}
+
 hipError_t stark_set_kernel_attributes() {
-    hipError_t e = hipFuncSetAttribute((const void*)k_ood_air<256>, hipFuncAttributeMaxDynamicSharedMemorySize, AIR_LDS_BUDGET);
-    if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void*)k_ood_air<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, AIR_LDS_BUDGET);
-    if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void*)k_deep, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
-    if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void*)k_deep_rows8, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192);
-    if (e != hipSuccess) return e;
-    return e;
+    const hipError_t e = set_attributes<false>();
+    return e != hipSuccess ? e : set_attributes<true>();
 }
 
 }  // namespace nhip

@@ -63,9 +63,8 @@ struct Tip5Lds {
 };
 
 // L(x) = (x + 1)^3 - 1 mod 257: twenty-first's tip5::LOOKUP_TABLE, equal to the table TIP5_LUT for
-// every x (checked at compile time below).  NHIP_LUT_COMPUTE builds have each thread compute its
-// entries instead of loading them (a workgroup's first barrier then waits on ALU work, not on a
-// memory round trip); measured within noise, so the table load stays the default.
+// every x (checked at compile time below).  Computing the entries per thread instead of loading
+// them measured within noise in round 3 (-0.9% at 4,096 proofs, +1% at 512): the table load stays.
 __host__ __device__ constexpr uint32_t tip5_lut_entry(uint32_t x) {
     return ((((x + 1u) * (x + 1u)) % 257u * (x + 1u)) % 257u + 256u) % 257u;
 }
@@ -77,29 +76,12 @@ constexpr bool tip5_lut_formula_matches_table() {
 static_assert(tip5_lut_formula_matches_table(), "L(x) = (x+1)^3 - 1 mod 257 is the Tip5 lookup table");
 
 __device__ __forceinline__ void tip5_lds_init(Tip5Lds& lds) {
-#ifdef NHIP_LUT_COMPUTE  // A/B builds: every entry computed (round 3: within noise, -0.9% at 4,096 proofs, +1% at 512)
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) lds.lut[i] = (uint8_t)tip5_lut_entry((uint32_t)i);
-#else
     for (int i = threadIdx.x; i < 256; i += blockDim.x) lds.lut[i] = TIP5_LUT[i];
-#endif
     __syncthreads();
 }
 
-// NHIP_LUT_PERM_PACK builds pack the four looked-up bytes (each zero-extended in its own register)
-// with two v_perm_b32 (bytes 0-1 and 2-3, the selector zero-filling the other half) and one v_or_b32:
-// 2 regular + 1 cheap VALU per dword instead of the shift / or chain's 4 regular ones (a row-hashing
-// round 1,301 -> 1,285 regular instructions), yet config 4 ran 1.4% slower with it (418.5-420.5k vs
-// 424.9-426.2k proofs/s, 512-proof shares equal; 3 repetitions, profiles/r03i): not the default.
-#ifdef NHIP_LUT_PERM_PACK
-__device__ __forceinline__ uint32_t lookup4(const uint8_t* __restrict__ lut, uint32_t w) {
-    const uint32_t b0 = lut[w & 0xFFu];
-    const uint32_t b1 = lut[(w >> 8) & 0xFFu];
-    const uint32_t b2 = lut[(w >> 16) & 0xFFu];
-    const uint32_t b3 = lut[w >> 24];
-    // v_perm_b32(s0, s1, sel): byte i of the result = byte sel_i of {s0 : s1} (0-3 s1, 4-7 s0), 0x0C = 0
-    return __builtin_amdgcn_perm(b1, b0, 0x0C0C0400u) | __builtin_amdgcn_perm(b3, b2, 0x04000C0Cu);
-}
-#else  // the shift / or form (default)
+// The four looked-up bytes packed by a shift / or chain.  Packing them with two v_perm_b32 and one
+// v_or_b32 instead (16 fewer regular VALU per round) ran config 4 1.4% slower (profiles/r03i).
 __device__ __forceinline__ uint32_t lookup4(const uint8_t* __restrict__ lut, uint32_t w) {
     const uint32_t b0 = lut[w & 0xFFu];
     const uint32_t b1 = lut[(w >> 8) & 0xFFu];
@@ -107,7 +89,6 @@ __device__ __forceinline__ uint32_t lookup4(const uint8_t* __restrict__ lut, uin
     const uint32_t b3 = lut[w >> 24];
     return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
 }
-#endif
 
 __device__ __forceinline__ uint64_t split_and_lookup(const uint8_t* __restrict__ lut, uint64_t r) {
     const uint32_t lo = lookup4(lut, (uint32_t)r);
@@ -170,7 +151,7 @@ __device__ __forceinline__ void mont_mul_n_dev(const uint64_t* a, const uint64_t
 #pragma unroll
     for (int i = 0; i < N; ++i)
         xh[i] = (uint64_t)a1[i] * (uint32_t)(b[i] >> 32) + (((uint64_t)c[i] << 32) | (uint32_t)(u[i] >> 32));
-    // montyred, as mont_mul_n
+    // montyred, as mont_mul (stage by stage across the N products)
 #pragma unroll
     for (int i = 0; i < N; ++i) ah[i] = __builtin_addc((uint32_t)u[i], (uint32_t)p00[i], 0u, &e[i]);
 #pragma unroll
@@ -198,11 +179,7 @@ __device__ __forceinline__ void mont_mul_n_dev(const uint64_t* a, const uint64_t
 
 template <int G>
 __device__ __forceinline__ void pow7_mul(const uint64_t* a, const uint64_t* b, uint64_t* out) {
-#ifdef NHIP_POW7_PLAIN
-    mont_mul_n<G>(a, b, out);
-#else
     mont_mul_n_dev<G>(a, b, out);
-#endif
 }
 
 __device__ __forceinline__ void pow7_12(uint64_t* x) {
@@ -220,65 +197,9 @@ __device__ __forceinline__ void pow7_12(uint64_t* x) {
 
 // MDS + ARK.  Circulant 16x16 with small (< 2^16) coefficients applied to the raw words: each
 // word is split into 32-bit halves and the two half-products are accumulated exactly in 64 bits
-// (< 2^53) by v_mad_u64_u32.  Recombination and the round-constant add follow twenty-first
-// step by step (s = acc_lo + acc_hi * 2^32; res = s_lo + s_hi * (2^32 - 1) with the +EPS fix on
-// overflow; x = res - (p - rc), + p on borrow), so every intermediate word is bit-identical to the
-// reference's, written as explicit 32-bit carry chains interleaved across the 16 outputs.
-__device__ __forceinline__ void mds_ark_carry(uint64_t s[16], const uint64_t* __restrict__ rc) {
-    uint32_t lo[16], hi[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        lo[j] = (uint32_t)s[j];
-        hi[j] = (uint32_t)(s[j] >> 32);
-    }
-    uint64_t al[16], ah[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        al[i] = 0;
-        ah[i] = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const uint64_t c = TIP5_MDS[(i - j) & 15];
-            al[i] += c * lo[j];
-            ah[i] += c * hi[j];
-        }
-    }
-    uint32_t m1[16], sh[16], rl[16], rh[16];
-    unsigned int k[16], b[16], over[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) m1[i] = __builtin_addc((uint32_t)(al[i] >> 32), (uint32_t)ah[i], 0u, &k[i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sh[i] = (uint32_t)(ah[i] >> 32) + k[i];
-    // t = sh * (2^32 - 1) = {0 - sh, sh - (sh != 0)}
-    uint32_t tl[16], th[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) tl[i] = __builtin_subc(0u, sh[i], 0u, &b[i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        unsigned int dummy;
-        th[i] = __builtin_subc(sh[i], 0u, b[i], &dummy);
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) rl[i] = __builtin_addc((uint32_t)al[i], tl[i], 0u, &k[i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) rh[i] = __builtin_addc(m1[i], th[i], k[i], &over[i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) rl[i] = __builtin_addc(rl[i], 0u - over[i], 0u, &k[i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) rh[i] = rh[i] + k[i];
-    // ARK: x1 = res - (p - rc); borrow => x1 + p  (== x1 - (2^32 - 1) mod 2^64)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const uint64_t q = GL_P - rc[i];
-        rl[i] = __builtin_subc(rl[i], (uint32_t)q, 0u, &b[i]);
-        rh[i] = __builtin_subc(rh[i], (uint32_t)(q >> 32), b[i], &over[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) rl[i] = __builtin_subc(rl[i], 0u - over[i], 0u, &b[i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) s[i] = ((uint64_t)(rh[i] - b[i]) << 32) | rl[i];
-}
-
+// (< 2^53) by v_mad_u64_u32; the round constant and the reduction are folded (below).  The
+// step-by-step form twenty-first writes (reduce, then add the constant) is kept as the reference
+// of tests/native/mds_fold_check.cpp and as the latency forms' mds_reduce_ark_lat.
 // Four words of mds_ark's folded reduction: w = sh * (2^32 - 1) + s_lo with the multiply-add's
 // carry-out G (bit 64 of the sum), and e = G ? 0 : 2^32 - 1.  Written as assembly because the
 // compiler cannot keep v_mad_u64_u32's carry-out as a lane mask; each v_cndmask reads its mask
@@ -388,13 +309,8 @@ __device__ __forceinline__ void mds_ark_fold(uint64_t s[16], const uint64_t* __r
 template <int G = NHIP_SPONGE_MDS_GROUP>
 __device__ __forceinline__ void mds_ark(uint64_t s[16], const uint64_t* __restrict__ rc,
                                         const uint64_t* __restrict__ rck) {
-#ifdef NHIP_MDS_CARRY
-    (void)rck;
-    mds_ark_carry(s, rc);
-#else
     (void)rc;
     mds_ark_fold<16, 0, 16, G>(s, rck);
-#endif
 }
 
 // One permutation on a raw Montgomery state.
@@ -515,25 +431,6 @@ __device__ __forceinline__ uint64_t mds_reduce_ark_lat(uint64_t al, uint64_t ah,
     const uint64_t y = res + (res < slo ? GL_EPS : 0ull);
     const uint64_t x1 = y + nq;
     return x1 + (x1 > y ? GL_P : 0ull);
-}
-
-// The original carry-chain form of the same word (fewer instructions; the issue-bound callers).
-__device__ __forceinline__ uint64_t mds_reduce_ark_carry(uint64_t al, uint64_t ah, uint64_t rc) {
-    unsigned int k1, b1, over, c2, bb, ov2;
-    const uint32_t m1 = __builtin_addc((uint32_t)(al >> 32), (uint32_t)ah, 0u, &k1);
-    const uint32_t sh = (uint32_t)(ah >> 32) + k1;
-    const uint32_t tl = __builtin_subc(0u, sh, 0u, &b1);
-    unsigned int dummy;
-    const uint32_t th = __builtin_subc(sh, 0u, b1, &dummy);
-    uint32_t rl = __builtin_addc((uint32_t)al, tl, 0u, &k1);
-    uint32_t rh = __builtin_addc(m1, th, k1, &over);
-    rl = __builtin_addc(rl, 0u - over, 0u, &c2);
-    rh = rh + c2;
-    const uint64_t q = GL_P - rc;
-    rl = __builtin_subc(rl, (uint32_t)q, 0u, &bb);
-    rh = __builtin_subc(rh, (uint32_t)(q >> 32), bb, &ov2);
-    rl = __builtin_subc(rl, 0u - ov2, 0u, &bb);
-    return ((uint64_t)(rh - bb) << 32) | rl;
 }
 
 // mds_ark's folded reduction for one word (the row forms): al started at K = rc + 2^32 - 1.  One chain per lane, so the mask read waits out the two wait states itself.

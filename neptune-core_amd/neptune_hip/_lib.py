@@ -28,7 +28,11 @@ _sz = ctypes.c_size_t
 class StarkParams(ctypes.Structure):
     _fields_ = [("security_level", ctypes.c_uint32), ("log2_fri_expansion", ctypes.c_uint32),
                 ("num_collinearity_checks", ctypes.c_uint32), ("num_main", ctypes.c_uint32),
-                ("num_aux", ctypes.c_uint32), ("num_quotient_segments", ctypes.c_uint32)]
+                ("num_aux", ctypes.c_uint32), ("num_quotient_segments", ctypes.c_uint32),
+                ("input_form", ctypes.c_uint32)]
+
+
+NHIP_INPUT_CANONICAL, NHIP_INPUT_MONTGOMERY = 0, 1
 
 
 class Claim(ctypes.Structure):
@@ -55,6 +59,18 @@ class Stats(ctypes.Structure):
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class QueueProfile(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_uint64), ("proofs", ctypes.c_uint64), ("size_hist", ctypes.c_uint64 * 8),
+                ("ms_window", ctypes.c_double), ("ms_stage", ctypes.c_double), ("ms_upload", ctypes.c_double),
+                ("ms_launch", ctypes.c_double), ("ms_device", ctypes.c_double), ("ms_wait", ctypes.c_double),
+                ("ms_turnaround", ctypes.c_double)]
+
+    def as_dict(self):
+        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d["size_hist"] = list(self.size_hist)
+        return d
 
 
 class BlkBlock(ctypes.Structure):
@@ -111,6 +127,7 @@ SIGNATURES = {
                            ctypes.POINTER(_vp)], ctypes.c_int),
     "nhip_queue_verify": ([_vp, _vp, _vp, _sz, _vp], ctypes.c_int),
     "nhip_queue_stats": ([_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+    "nhip_queue_profile_read": ([_vp, ctypes.POINTER(QueueProfile), ctypes.c_int], ctypes.c_int),
     "nhip_queue_destroy": ([_vp], None),
     "nhip_host_alloc": ([_sz, ctypes.POINTER(_vp)], ctypes.c_int),
     "nhip_host_free": ([_vp], ctypes.c_int),
@@ -144,6 +161,13 @@ SIGNATURES = {
     "nhip_group_shard": ([ctypes.POINTER(Proof), _sz, _sz, ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
     "nhip_group_verify_batch": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof),
                                  _sz, _u8p, ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
+    "nhip_group_stream_create": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(_vp)], ctypes.c_int),
+    "nhip_group_stream_submit": ([_vp, ctypes.POINTER(Claim), ctypes.POINTER(Proof), _sz, _vp, _vp], ctypes.c_int),
+    "nhip_group_stream_finish": ([_vp], ctypes.c_int),
+    "nhip_group_stream_stats": ([_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                 ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+    "nhip_group_stream_destroy": ([_vp], None),
     "nhip_batch_prepare": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim), ctypes.POINTER(Proof),
                             _sz, _pp], ctypes.c_int),
     "nhip_batch_refill": ([_vp, _vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(Claim),
@@ -152,6 +176,7 @@ SIGNATURES = {
     "nhip_batch_launch": ([_vp, _vp], ctypes.c_int),
     "nhip_batch_wait": ([_vp, _vp, _u8p, ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
     "nhip_batch_stats": ([_vp, ctypes.POINTER(Stats)], ctypes.c_int),
+    "nhip_set_fs_form": ([ctypes.c_int], ctypes.c_int),
     "nhip_batch_transcript": ([_vp, _vp, _sz, _u64p, _sz, ctypes.POINTER(ctypes.c_uint32), _sz,
                                ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "nhip_batch_destroy": ([_vp], None),

@@ -10,6 +10,7 @@ triton-vm Claim fields, a proof is the flat `Proof(Vec<BFieldElement>)` word vec
 from __future__ import annotations
 
 import ctypes
+import dataclasses
 from dataclasses import dataclass, field
 from typing import List, Sequence, Tuple
 
@@ -27,10 +28,13 @@ class Stark:
     num_main: int = 379
     num_aux: int = 88
     num_quotient_segments: int = 4
+    # how the claims' and proofs' field elements are given (nhip_stark_params.input_form): canonical
+    # values, or twenty-first's in-memory Montgomery words (the drop-in hands `Proof.0` over as is)
+    input_form: int = _lib.NHIP_INPUT_CANONICAL
 
     def c(self) -> _lib.StarkParams:
         return _lib.StarkParams(self.security_level, self.log2_fri_expansion, self.num_collinearity_checks,
-                                self.num_main, self.num_aux, self.num_quotient_segments)
+                                self.num_main, self.num_aux, self.num_quotient_segments, self.input_form)
 
     @classmethod
     def default(cls) -> "Stark":
@@ -38,7 +42,53 @@ class Stark:
         p = _lib.StarkParams()
         lib.nhip_stark_params_default(ctypes.byref(p))
         return cls(p.security_level, p.log2_fri_expansion, p.num_collinearity_checks, p.num_main, p.num_aux,
-                   p.num_quotient_segments)
+                   p.num_quotient_segments, p.input_form)
+
+    def montgomery(self) -> "Stark":
+        """The same parameters taking Montgomery-word input (NHIP_INPUT_MONTGOMERY)."""
+        return dataclasses.replace(self, input_form=_lib.NHIP_INPUT_MONTGOMERY)
+
+
+_P = (1 << 64) - (1 << 32) + 1
+
+
+def to_montgomery(words) -> np.ndarray:
+    """Canonical values (any u64, read mod p) -> twenty-first's in-memory BFieldElement words
+    x * 2^64 mod p (goldilocks.hpp to_mont's closed form: with x = h 2^32 + l, x 2^64 == l 2^32 - h - l).
+    Host-side test-data preparation: a node's proofs are in this form already."""
+    x = np.asarray(words, dtype=np.uint64)
+    lo = x & np.uint64(0xFFFFFFFF)
+    hi = x >> np.uint64(32)
+    s = hi + lo
+    t = lo << np.uint64(32)
+    v = t - s
+    return np.where(t < s, v + np.uint64(_P), v).astype(np.uint64)
+
+
+def from_montgomery(words) -> np.ndarray:
+    """Inverse of to_montgomery: the canonical values of Montgomery words (any u64 read mod p),
+    x * 2^-64 = -(x * 2^32) mod p with x = h 2^32 + l: x 2^32 == (h + l) 2^32 - h."""
+    x = np.asarray(words, dtype=np.uint64)
+    p = np.uint64(_P)
+    h = x >> np.uint64(32)
+    s = h + (x & np.uint64(0xFFFFFFFF))
+    t1 = ((s & np.uint64(0xFFFFFFFF)) << np.uint64(32)) + (s >> np.uint64(32)) * np.uint64(0xFFFFFFFF)
+    t1 = np.where(t1 >= p, t1 - p, t1)
+    t = np.where(t1 >= h, t1 - h, t1 + (p - h))
+    return np.where(t == 0, t, p - t).astype(np.uint64)
+
+
+def montgomery_claim(c: "Claim") -> "Claim":
+    """A claim's field elements (digest, input, output) as Montgomery words; version unchanged."""
+    return Claim([int(v) for v in to_montgomery(list(c.program_digest))], c.version,
+                 [int(v) for v in to_montgomery(list(c.input))] if len(c.input) else [],
+                 [int(v) for v in to_montgomery(list(c.output))] if len(c.output) else [])
+
+
+def set_fs_form(form: int) -> None:
+    """Fiat-Shamir replay form of later launches (nhip_set_fs_form): -1 by batch size, 0 row, 1 pair,
+    2 quad (tests / A/B runs)."""
+    check(_lib.load().nhip_set_fs_form(int(form)), "nhip_set_fs_form")
 
 
 @dataclass
@@ -220,6 +270,13 @@ class Queue:
         check(self.ctx.lib.nhip_queue_stats(self.handle, ctypes.byref(b), ctypes.byref(p)), "nhip_queue_stats")
         return {"batches": b.value, "proofs": p.value}
 
+    def profile(self, reset: bool = False) -> dict:
+        """Where the queue's time went (nhip_queue_profile_read): per-batch window / stage / upload /
+        launch / device / wait / turnaround milliseconds summed, and the batch-size histogram."""
+        pr = _lib.QueueProfile()
+        check(self.ctx.lib.nhip_queue_profile_read(self.handle, ctypes.byref(pr), int(reset)), "nhip_queue_profile_read")
+        return pr.as_dict()
+
     def close(self):
         if self.handle:
             self.ctx.lib.nhip_queue_destroy(self.handle)
@@ -314,6 +371,57 @@ def verify_batch_group(group: Group, air: Air, stark: Stark,
     check(group.lib.nhip_group_verify_batch(group.handle, air.handle, ctypes.byref(params), m.claims, m.proofs, m.n,
                                             v, ctypes.byref(ok)), "nhip_group_verify_batch")
     return [bool(x) for x in v[:m.n]], bool(ok.value)
+
+
+class GroupStream:
+    """Batch after batch over every member of a group (nhip_group_stream_*): each member's share of
+    batch k is staged and uploaded while its share of batch k - 1 still runs.  ``submit(pairs)``
+    returns the verdicts of the PREVIOUS batch (None for the first), ``finish()`` the last one's."""
+
+    def __init__(self, group: Group, air: Air, stark: Stark):
+        self.group, self.air, self.stark = group, air, stark
+        self.lib = group.lib
+        h = ctypes.c_void_p()
+        params = stark.c()
+        check(self.lib.nhip_group_stream_create(group.handle, air.handle, ctypes.byref(params), ctypes.byref(h)),
+              "nhip_group_stream_create")
+        self.handle = h.value
+        self._prev = None  # (verdict array, all_ok byte) of the batch in flight
+
+    def submit_marshalled(self, m: "_Marshal"):
+        v = np.zeros(max(m.n, 1), dtype=np.uint8)
+        ok = (ctypes.c_uint8 * 1)()
+        check(self.lib.nhip_group_stream_submit(self.handle, m.claims, m.proofs, m.n, v.ctypes.data,
+                                                ctypes.addressof(ok)), "nhip_group_stream_submit")
+        prev, self._prev = self._prev, (v[:m.n], ok, m.n)
+        return None if prev is None else ([bool(x) for x in prev[0]], bool(prev[1][0]))
+
+    def submit(self, pairs: Sequence[Tuple[Claim, Sequence[int]]]):
+        return self.submit_marshalled(_Marshal([c for c, _ in pairs], [p for _, p in pairs]))
+
+    def finish(self):
+        check(self.lib.nhip_group_stream_finish(self.handle), "nhip_group_stream_finish")
+        prev, self._prev = self._prev, None
+        return None if prev is None else ([bool(x) for x in prev[0]], bool(prev[1][0]))
+
+    def stats(self) -> dict:
+        b, p = ctypes.c_uint64(), ctypes.c_uint64()
+        st, up, dv = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        check(self.lib.nhip_group_stream_stats(self.handle, ctypes.byref(b), ctypes.byref(p), ctypes.byref(st),
+                                               ctypes.byref(up), ctypes.byref(dv)), "nhip_group_stream_stats")
+        return {"batches": b.value, "proofs": p.value, "ms_stage": st.value, "ms_upload": up.value,
+                "ms_device": dv.value}
+
+    def close(self):
+        if self.handle:
+            self.lib.nhip_group_stream_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def proof_decodes(air: Air, stark: Stark, claim: Claim, proof: Sequence[int]) -> bool:

@@ -1,9 +1,11 @@
 //! Raw FFI of `libneptune_hip.so`, the MI355X (gfx950) batched STARK verifier for neptune-core's
 //! proof-validation path.  One declaration per entry point of `include/neptune_hip.h` (the C ABI
 //! is the contract; `tests/test_rust_crates.py` checks that this file declares every symbol the
-//! header does).  Conventions: field elements as canonical u64 (`BFieldElement::value()`),
-//! caller-owned buffers borrowed for the call, return 0 = ok, otherwise an infrastructure fault
-//! (never "accept").  Not compiled in the build container (no Rust toolchain there).
+//! header does).  Conventions: field elements as canonical u64 (`BFieldElement::value()`), or for
+//! the STARK entry points with `input_form = NHIP_INPUT_MONTGOMERY` as twenty-first's in-memory
+//! words (a `Vec<BFieldElement>` passed by pointer), caller-owned buffers borrowed for the call,
+//! return 0 = ok, otherwise an infrastructure fault (never "accept").  Not compiled in the build
+//! container (no Rust toolchain there).
 #![allow(non_camel_case_types)]
 #![no_std]
 
@@ -21,11 +23,14 @@ pub const NHIP_BLOCK_PROOF_INVALID: u32 = 1;
 pub const NHIP_BLOCK_PROOF_SINGLE: u32 = 2;
 pub const NHIP_TX_PROOF_COLLECTION: u32 = 0;
 pub const NHIP_TX_SINGLE_PROOF: u32 = 1;
+pub const NHIP_INPUT_CANONICAL: u32 = 0;
+pub const NHIP_INPUT_MONTGOMERY: u32 = 1;
+pub const NHIP_HW_QUEUES_RECOMMENDED: u32 = 8;
 
 macro_rules! opaque {
     ($($name:ident),*) => { $( #[repr(C)] pub struct $name { _p: [u8; 0] } )* };
 }
-opaque!(nhip_ctx, nhip_air, nhip_batch, nhip_group, nhip_queue, nhip_pow_buffer);
+opaque!(nhip_ctx, nhip_air, nhip_batch, nhip_group, nhip_group_stream, nhip_queue, nhip_pow_buffer);
 
 /// `Stark::default()` plus the table dimensions (`nhip_stark_params_default`).
 #[repr(C)]
@@ -37,9 +42,12 @@ pub struct nhip_stark_params {
     pub num_main: u32,
     pub num_aux: u32,
     pub num_quotient_segments: u32,
+    /// `NHIP_INPUT_CANONICAL` or `NHIP_INPUT_MONTGOMERY` (claims' and proofs' field elements)
+    pub input_form: u32,
 }
 
-/// `triton_vm::proof::Claim { program_digest, version, input, output }`, canonical words.
+/// `triton_vm::proof::Claim { program_digest, version, input, output }`, words in the params'
+/// `input_form`.
 #[repr(C)]
 #[derive(Clone, Copy, Debug)]
 pub struct nhip_claim {
@@ -51,7 +59,7 @@ pub struct nhip_claim {
     pub output_len: usize,
 }
 
-/// `triton_vm::proof::Proof(Vec<BFieldElement>)`, canonical words.
+/// `triton_vm::proof::Proof(Vec<BFieldElement>)`, words in the params' `input_form`.
 #[repr(C)]
 #[derive(Clone, Copy, Debug)]
 pub struct nhip_proof {
@@ -82,6 +90,21 @@ pub struct nhip_stats {
     pub mp_hash_kernel_perms: u64,
     pub ms_device_decode: f64,
     pub ms_mp_hash_exec: f64,
+}
+
+#[repr(C)]
+#[derive(Default, Clone, Copy, Debug)]
+pub struct nhip_queue_profile {
+    pub batches: u64,
+    pub proofs: u64,
+    pub size_hist: [u64; 8],
+    pub ms_window: f64,
+    pub ms_stage: f64,
+    pub ms_upload: f64,
+    pub ms_launch: f64,
+    pub ms_device: f64,
+    pub ms_wait: f64,
+    pub ms_turnaround: f64,
 }
 
 #[repr(C)]
@@ -183,11 +206,13 @@ extern "C" {
                                  xfe_out: *mut u64, xfe_cap: usize, idx_out: *mut u32, idx_cap: usize,
                                  fail_bits: *mut u32, n_xfe: *mut usize) -> c_int;
     pub fn nhip_batch_destroy(batch: *mut nhip_batch);
+    pub fn nhip_set_fs_form(form: c_int) -> c_int;
     pub fn nhip_queue_create(ctx: *mut nhip_ctx, air: *mut nhip_air, params: *const nhip_stark_params,
                              max_batch: u32, max_wait_us: u32, out: *mut *mut nhip_queue) -> c_int;
     pub fn nhip_queue_verify(queue: *mut nhip_queue, claims: *const nhip_claim, proofs: *const nhip_proof,
                              n: usize, verdicts: *mut u8) -> c_int;
     pub fn nhip_queue_stats(queue: *const nhip_queue, batches: *mut u64, proofs: *mut u64) -> c_int;
+    pub fn nhip_queue_profile_read(queue: *const nhip_queue, out: *mut nhip_queue_profile, reset: c_int) -> c_int;
     pub fn nhip_queue_destroy(queue: *mut nhip_queue);
     pub fn nhip_group_create(devices: *const c_int, n_devices: usize, out: *mut *mut nhip_group) -> c_int;
     pub fn nhip_group_init(device_mask: u32, out: *mut *mut nhip_group) -> c_int;
@@ -198,6 +223,14 @@ extern "C" {
     pub fn nhip_group_verify_batch(group: *mut nhip_group, air: *mut nhip_air,
                                    params: *const nhip_stark_params, claims: *const nhip_claim,
                                    proofs: *const nhip_proof, n: usize, verdicts: *mut u8, all_ok: *mut u8) -> c_int;
+    pub fn nhip_group_stream_create(group: *mut nhip_group, air: *mut nhip_air, params: *const nhip_stark_params,
+                                    out: *mut *mut nhip_group_stream) -> c_int;
+    pub fn nhip_group_stream_submit(stream: *mut nhip_group_stream, claims: *const nhip_claim,
+                                    proofs: *const nhip_proof, n: usize, verdicts: *mut u8, all_ok: *mut u8) -> c_int;
+    pub fn nhip_group_stream_finish(stream: *mut nhip_group_stream) -> c_int;
+    pub fn nhip_group_stream_stats(stream: *const nhip_group_stream, batches: *mut u64, proofs: *mut u64,
+                                   ms_stage: *mut f64, ms_upload: *mut f64, ms_device: *mut f64) -> c_int;
+    pub fn nhip_group_stream_destroy(stream: *mut nhip_group_stream);
     pub fn nhip_proof_from_be_bytes(bytes: *const u8, n_bytes: usize, words: *mut u64, cap: usize,
                                     n_words: *mut usize) -> c_int;
     pub fn nhip_proof_to_be_bytes(words: *const u64, n: usize, out: *mut u8) -> c_int;

@@ -17,7 +17,11 @@
 //!   built once at startup ([`Air::triton`]).
 //! * Process-wide use: [`gpu_verifier`] / [`gpu_node`] create the verifier once, on first use,
 //!   from the environment (`NEPTUNE_HIP_DEVICE`, `NEPTUNE_HIP_DEVICES`); `None` means "no GPU"
-//!   and the callers take the CPU path.
+//!   and the callers take the CPU path; why is logged once (`tracing::warn!`) and kept by
+//!   [`gpu_verifier_status`] / [`gpu_node_status`].  The library never touches the environment:
+//!   call [`provision_hw_queues`] from `main()` before the runtime starts its threads.
+//! * Zero copy: proofs and claims are handed to the library as their `BFieldElement` words lie in
+//!   memory (Montgomery form, `NHIP_INPUT_MONTGOMERY`); no per-word conversion, no buffer copy.
 //!
 //! Not compiled in the build container (no Rust toolchain there); the C ABI underneath is
 //! exercised by the repository's Python and C99 tests.
@@ -45,19 +49,29 @@ fn ok(rc: i32) -> Result<(), GpuFault> {
     if rc == sys::NHIP_OK { Ok(()) } else { Err(GpuFault(rc)) }
 }
 
-fn canon(d: &Digest) -> [u64; 5] {
-    d.values().map(|b| b.value())
+// twenty-first 1.0.0 holds a BFieldElement as its Montgomery word in a `#[repr(transparent)]`
+// u64 newtype, so a `[BFieldElement]` is a `[u64]` of those words: the library reads them as they
+// lie (NHIP_INPUT_MONTGOMERY), with no conversion and no copy.
+const _: () = assert!(
+    std::mem::size_of::<BFieldElement>() == 8 && std::mem::align_of::<BFieldElement>() == std::mem::align_of::<u64>()
+);
+
+fn raw_words(v: &[BFieldElement]) -> *const u64 {
+    debug_assert!(v.first().map_or(true, |b| unsafe { *(v.as_ptr() as *const u64) } == b.raw_u64()));
+    v.as_ptr() as *const u64
 }
 
-fn words(v: &[BFieldElement]) -> Vec<u64> {
-    v.iter().map(|b| b.value()).collect()
+fn raw_digest(d: &Digest) -> [u64; 5] {
+    d.values().map(|b| b.raw_u64())
 }
 
 /// `Stark::default()` as the library's parameters (security 160, FRI expansion 4, 80
 /// collinearity checks, triton-vm's 379 main / 88 auxiliary columns, 4 quotient segments).
+/// Claims and proofs are passed as twenty-first's in-memory words (`input_form` Montgomery).
 pub fn default_params() -> sys::nhip_stark_params {
     let mut p = sys::nhip_stark_params::default();
     unsafe { sys::nhip_stark_params_default(&mut p) };
+    p.input_form = sys::NHIP_INPUT_MONTGOMERY;
     p
 }
 
@@ -86,36 +100,29 @@ impl Drop for Air {
     }
 }
 
-/// Canonical-word views of a batch, kept alive while the C structs point into them.
-struct Marshal {
+/// The C structs of a batch, pointing straight into the callers' `Claim` / `Proof` memory (no
+/// word is converted or copied; the digest's five words are copied into the struct).
+struct Marshal<'a> {
     claims: Vec<sys::nhip_claim>,
     proofs: Vec<sys::nhip_proof>,
-    _bufs: Vec<Vec<u64>>,
+    _borrow: std::marker::PhantomData<&'a ()>,
 }
 
-fn marshal(items: &[(&Claim, &Proof)]) -> Marshal {
-    let mut bufs: Vec<Vec<u64>> = Vec::with_capacity(3 * items.len());
+fn marshal<'a>(items: impl ExactSizeIterator<Item = (&'a Claim, &'a Proof)>) -> Marshal<'a> {
+    let mut claims = Vec::with_capacity(items.len());
+    let mut proofs = Vec::with_capacity(items.len());
     for (c, p) in items {
-        bufs.push(words(&c.input));
-        bufs.push(words(&c.output));
-        bufs.push(words(&p.0));
-    }
-    let claims = items
-        .iter()
-        .enumerate()
-        .map(|(i, (c, _))| sys::nhip_claim {
-            program_digest: canon(&c.program_digest),
+        claims.push(sys::nhip_claim {
+            program_digest: raw_digest(&c.program_digest),
             version: c.version,
-            input: bufs[3 * i].as_ptr(),
-            input_len: bufs[3 * i].len(),
-            output: bufs[3 * i + 1].as_ptr(),
-            output_len: bufs[3 * i + 1].len(),
-        })
-        .collect();
-    let proofs = (0..items.len())
-        .map(|i| sys::nhip_proof { words: bufs[3 * i + 2].as_ptr(), len: bufs[3 * i + 2].len() })
-        .collect();
-    Marshal { claims, proofs, _bufs: bufs }
+            input: raw_words(&c.input),
+            input_len: c.input.len(),
+            output: raw_words(&c.output),
+            output_len: c.output.len(),
+        });
+        proofs.push(sys::nhip_proof { words: raw_words(&p.0), len: p.0.len() });
+    }
+    Marshal { claims, proofs, _borrow: std::marker::PhantomData }
 }
 
 /// One GPU: a context, the AIR, and a coalescing queue for single-proof calls.
@@ -151,7 +158,7 @@ impl Verifier {
     /// proofs of concurrent callers (e.g. one tokio blocking task per peer transaction,
     /// `peer_loop.rs:1342`).
     pub fn verify(&self, claim: &Claim, proof: &Proof) -> Result<bool, GpuFault> {
-        let m = marshal(&[(claim, proof)]);
+        let m = marshal(std::iter::once((claim, proof)));
         let mut v = [0u8; 1];
         ok(unsafe { sys::nhip_queue_verify(self.queue, m.claims.as_ptr(), m.proofs.as_ptr(), 1, v.as_mut_ptr()) })?;
         Ok(v[0] == 1)
@@ -159,8 +166,7 @@ impl Verifier {
 
     /// `verify_batch(&[(Claim, Proof)]) -> Vec<bool>`: one device batch.
     pub fn verify_batch(&self, items: &[(Claim, Proof)]) -> Result<Vec<bool>, GpuFault> {
-        let refs: Vec<(&Claim, &Proof)> = items.iter().map(|(c, p)| (c, p)).collect();
-        let m = marshal(&refs);
+        let m = marshal(items.iter().map(|(c, p)| (c, p)));
         let mut v = vec![0u8; items.len()];
         let _g = self.batch_lock.lock().unwrap_or_else(|e| e.into_inner());
         ok(unsafe {
@@ -206,8 +212,7 @@ impl GpuNode {
     /// (verdicts, AND of the verdicts): the block / ProofCollection verdict is the AND
     /// (`proof_collection.rs:388`).
     pub fn verify_batch(&self, items: &[(Claim, Proof)]) -> Result<(Vec<bool>, bool), GpuFault> {
-        let refs: Vec<(&Claim, &Proof)> = items.iter().map(|(c, p)| (c, p)).collect();
-        let m = marshal(&refs);
+        let m = marshal(items.iter().map(|(c, p)| (c, p)));
         let mut v = vec![0u8; items.len()];
         let mut all = 0u8;
         ok(unsafe {
@@ -215,6 +220,48 @@ impl GpuNode {
                                          items.len(), v.as_mut_ptr(), &mut all)
         })?;
         Ok((v.into_iter().map(|b| b == 1).collect(), all == 1))
+    }
+
+    /// Batch after batch (bootstrap import, `state/mod.rs:2226-2272`; block batches,
+    /// `peer_loop.rs:315-323`): each GPU's share of the next batch is staged and uploaded while its
+    /// share of the current one runs (`nhip_group_stream`).  `on_verdicts(i, verdicts, all_ok)` is
+    /// called for batch i once it is verified, in order; the batches are borrowed only until the
+    /// next one is submitted.  A fault stops the stream: the batches not yet reported are unknown.
+    pub fn verify_stream<'a, I, F>(&self, batches: I, mut on_verdicts: F) -> Result<(), GpuFault>
+    where
+        I: IntoIterator<Item = &'a [(Claim, Proof)]>,
+        F: FnMut(usize, Vec<bool>, bool),
+    {
+        let mut st = ptr::null_mut();
+        ok(unsafe { sys::nhip_group_stream_create(self.group, self.air.0, &self.params, &mut st) })?;
+        struct Stream(*mut sys::nhip_group_stream);
+        impl Drop for Stream {
+            fn drop(&mut self) {
+                unsafe { sys::nhip_group_stream_destroy(self.0) }
+            }
+        }
+        let st = Stream(st);
+        // verdict buffers of the batch in flight and of the one before it (written one submit later)
+        let mut bufs: [(Vec<u8>, u8); 2] = [(Vec::new(), 0), (Vec::new(), 0)];
+        let mut k = 0usize;
+        for items in batches {
+            let m = marshal(items.iter().map(|(c, p)| (c, p)));
+            let slot = k & 1;
+            bufs[slot].0 = vec![0u8; items.len()];
+            let (vp, ap) = (bufs[slot].0.as_mut_ptr(), &mut bufs[slot].1 as *mut u8);
+            ok(unsafe { sys::nhip_group_stream_submit(st.0, m.claims.as_ptr(), m.proofs.as_ptr(), items.len(), vp, ap) })?;
+            if k > 0 {
+                let (v, all) = &bufs[slot ^ 1];
+                on_verdicts(k - 1, v.iter().map(|&b| b == 1).collect(), *all == 1);
+            }
+            k += 1;
+        }
+        ok(unsafe { sys::nhip_group_stream_finish(st.0) })?;
+        if k > 0 {
+            let (v, all) = &bufs[(k - 1) & 1];
+            on_verdicts(k - 1, v.iter().map(|&b| b == 1).collect(), *all == 1);
+        }
+        Ok(())
     }
 }
 
@@ -224,46 +271,87 @@ impl Drop for GpuNode {
     }
 }
 
-/// Hardware queues the verifier's pipeline uses when it is the first HIP user of the process: two
-/// batches in flight, each with a hashing and a latency stream, plus the context stream and one
-/// spare (HIP serializes streams that share a queue; its default is 4).  Set only if the operator
-/// has not set `GPU_MAX_HW_QUEUES`, and only before the first HIP call (later it has no effect).
-pub const HW_QUEUES: u32 = 8;
+/// Hardware queues the verifier's pipeline uses: two batches in flight, each with a hashing and a
+/// latency stream, plus the context stream and one spare (HIP serializes streams that share a
+/// queue; its default is 4).
+pub const HW_QUEUES: u32 = sys::NHIP_HW_QUEUES_RECOMMENDED;
 
-fn provision_hw_queues() {
+/// Sets `GPU_MAX_HW_QUEUES` to [`HW_QUEUES`] unless the operator has set it.  HIP reads it once, at
+/// its initialisation, and changing the environment races with every thread that reads it: call
+/// this from `main()` before the tokio runtime (or anything else) starts a thread.  The library
+/// itself never changes the environment.
+pub fn provision_hw_queues() {
     if std::env::var_os("GPU_MAX_HW_QUEUES").is_none() {
         std::env::set_var("GPU_MAX_HW_QUEUES", HW_QUEUES.to_string());
     }
 }
 
-static GPU_VERIFIER: OnceLock<Option<Verifier>> = OnceLock::new();
-static GPU_NODE: OnceLock<Option<GpuNode>> = OnceLock::new();
-
-/// The process's single-GPU verifier (created on first use): device `NEPTUNE_HIP_DEVICE`
-/// (default 0), triton-air's AIR, a 200 us coalescing window.  `None` when there is no usable GPU.
-/// This is the `GPU_VERIFIER.get()` of INTEGRATION.md.
-pub fn gpu_verifier() -> Option<&'static Verifier> {
-    GPU_VERIFIER
-        .get_or_init(|| {
-            provision_hw_queues();
-            let dev = std::env::var("NEPTUNE_HIP_DEVICE").ok().and_then(|v| v.parse().ok()).unwrap_or(0);
-            Air::triton().and_then(|air| Verifier::new(dev, air, 200)).ok()
-        })
-        .as_ref()
+/// Why the GPU path is not available (kept by the process-wide constructors).
+#[derive(Debug, Clone)]
+pub enum InitError {
+    /// `Air::triton()`: the exporter could not build triton-air's descriptor.
+    AirExport(String),
+    /// `nhip_*` returned this fault (no device, HIP error, out of memory, bad argument).
+    Gpu(GpuFault),
 }
 
-/// Every GPU of the node (created on first use): the device mask `NEPTUNE_HIP_DEVICES` (hex or
-/// decimal, default 0 = every visible GPU).  `None` when there is no usable GPU.
+impl std::fmt::Display for InitError {
+    fn fmt(&self, f: &mut std::fmt::Formatter<'_>) -> std::fmt::Result {
+        match self {
+            InitError::AirExport(e) => write!(f, "neptune-hip: triton-air export failed: {e}"),
+            InitError::Gpu(g) => g.fmt(f),
+        }
+    }
+}
+impl std::error::Error for InitError {}
+
+fn triton_air() -> Result<Air, InitError> {
+    let words = air_export::triton_air_descriptor().map_err(|e| InitError::AirExport(format!("{e:?}")))?;
+    Air::from_descriptor(&words).map_err(InitError::Gpu)
+}
+
+static GPU_VERIFIER: OnceLock<Result<Verifier, InitError>> = OnceLock::new();
+static GPU_NODE: OnceLock<Result<GpuNode, InitError>> = OnceLock::new();
+
+fn logged<T>(what: &str, r: &Result<T, InitError>) {
+    if let Err(e) = r {
+        tracing::warn!("{what}: GPU verification unavailable, using the CPU verifier: {e}");
+    }
+}
+
+/// The process's single-GPU verifier, or why there is none (created on first use): device
+/// `NEPTUNE_HIP_DEVICE` (default 0), triton-air's AIR, a 200 us coalescing window.
+pub fn gpu_verifier_status() -> &'static Result<Verifier, InitError> {
+    GPU_VERIFIER.get_or_init(|| {
+        let dev = std::env::var("NEPTUNE_HIP_DEVICE").ok().and_then(|v| v.parse().ok()).unwrap_or(0);
+        let r = triton_air().and_then(|air| Verifier::new(dev, air, 200).map_err(InitError::Gpu));
+        logged("gpu_verifier", &r);
+        r
+    })
+}
+
+/// [`gpu_verifier_status`] as an `Option` (`None`: no usable GPU, the reason was logged).  This is
+/// the `GPU_VERIFIER.get()` of INTEGRATION.md.
+pub fn gpu_verifier() -> Option<&'static Verifier> {
+    gpu_verifier_status().as_ref().ok()
+}
+
+/// Every GPU of the node, or why there is none (created on first use): the device mask
+/// `NEPTUNE_HIP_DEVICES` (hex or decimal, default 0 = every visible GPU).
+pub fn gpu_node_status() -> &'static Result<GpuNode, InitError> {
+    GPU_NODE.get_or_init(|| {
+        let mask = std::env::var("NEPTUNE_HIP_DEVICES").ok().and_then(|v| {
+            v.strip_prefix("0x").map_or_else(|| v.parse().ok(), |h| u32::from_str_radix(h, 16).ok())
+        });
+        let r = triton_air().and_then(|air| GpuNode::init(mask.unwrap_or(0), air).map_err(InitError::Gpu));
+        logged("gpu_node", &r);
+        r
+    })
+}
+
+/// [`gpu_node_status`] as an `Option` (`None`: no usable GPU, the reason was logged).
 pub fn gpu_node() -> Option<&'static GpuNode> {
-    GPU_NODE
-        .get_or_init(|| {
-            provision_hw_queues();
-            let mask = std::env::var("NEPTUNE_HIP_DEVICES").ok().and_then(|v| {
-                v.strip_prefix("0x").map_or_else(|| v.parse().ok(), |h| u32::from_str_radix(h, 16).ok())
-            });
-            Air::triton().and_then(|air| GpuNode::init(mask.unwrap_or(0), air)).ok()
-        })
-        .as_ref()
+    gpu_node_status().as_ref().ok()
 }
 
 /// The drop-in for `verifier.rs:60-63`: the GPU verdict, or on a GPU fault (or without a GPU)

@@ -34,7 +34,7 @@ def pytest_collection_modifyitems(session, config, items):
     """The config-4 GPU tests draw from oracle/pool4.py's 256 distinct proofs, built once per machine
     in a child process: build it here, after collection and before any test creates a GPU context,
     so the child is never forked from a process that has initialised HIP."""
-    if any(it.get_closest_marker("gpu") and ("test_gpu_config4" in it.nodeid or "test_gpu_fs_forms" in it.nodeid)
-           for it in items):
+    users = ("test_gpu_config4", "test_gpu_fs_forms", "test_gpu_input_forms", "test_gpu_group_stream")
+    if any(it.get_closest_marker("gpu") and any(u in it.nodeid for u in users) for it in items):
         import pool4  # oracle/: test-data generator
         pool4.load()

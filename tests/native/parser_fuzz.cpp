@@ -57,24 +57,31 @@ Dims dims_of(uint32_t checks, uint32_t main, uint32_t aux) {
 
 uint64_t g_ok = 0, g_runs = 0;
 
-// the walk reads exactly words[0, n): parse from a heap copy of that size so ASan sees any overrun
-void run_proof(const std::vector<uint8_t>& bytes, const Dims& D) {
-    const size_t n = bytes.size() / 8;
-    std::vector<uint64_t> w(n);
-    if (n) std::memcpy(w.data(), bytes.data(), n * 8);
+// the walk reads exactly words[0, n): parse from a heap copy of that size so ASan sees any overrun.
+// Both input forms (canonical values, Montgomery words): the same bytes, different structural values.
+template <bool MW>
+void run_proof_form(const uint64_t* words, size_t n, const Dims& D) {
     ProofDesc pd;
     FsOp ops[fs_ops_for(MAX_FRI_ROUNDS)];
     uint64_t perms, plcw;
     const ClaimLoc cl{0, 3, 1};
-    const uint64_t* words = n ? w.data() : nullptr;
-    const uint32_t f = decode_stream(words, 0, n, cl, D, pd, ops, perms, plcw);
+    const uint32_t f = decode_stream<MW>(words, 0, n, cl, D, pd, ops, perms, plcw);
     if (!f) {
         const int64_t deg = last_poly_degree_host(words, pd);
         last_poly_finish(pd, deg, D);
         ++g_ok;
     }
     uint64_t lph;
-    (void)header_log2_ph(words, n, lph);
+    (void)header_log2_ph<MW>(words, n, lph);
+}
+
+void run_proof(const std::vector<uint8_t>& bytes, const Dims& D) {
+    const size_t n = bytes.size() / 8;
+    std::vector<uint64_t> w(n);
+    if (n) std::memcpy(w.data(), bytes.data(), n * 8);
+    const uint64_t* words = n ? w.data() : nullptr;
+    run_proof_form<false>(words, n, D);
+    run_proof_form<true>(words, n, D);
     ++g_runs;
 }
 

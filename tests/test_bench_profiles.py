@@ -5,6 +5,8 @@ the default bench line with its roofline and cpu_baseline objects)."""
 import json
 import os
 
+import pytest
+
 import bench
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -13,6 +15,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _latest():
     parts = open(os.path.join(ROOT, "profiles", "LATEST")).read().split()
     return parts[0], int(parts[1]), int(parts[2])
+
+
+def _workload():
+    """(AIR, input form) of the LATEST profile (a 3-field line: synthetic AIR, canonical words)."""
+    parts = open(os.path.join(ROOT, "profiles", "LATEST")).read().split()
+    return (parts[3] if len(parts) > 3 else "synthetic"), (parts[4] if len(parts) > 4 else "canonical")
+
+
+@pytest.fixture(autouse=True)
+def _latest_workload(monkeypatch):
+    air, form = _workload()
+    monkeypatch.setitem(bench.WORKLOAD, "air", air)
+    monkeypatch.setitem(bench.WORKLOAD, "input_form", form)
 
 
 def _profiled_lib(tag):
@@ -30,6 +45,14 @@ def test_latest_profile_is_keyed_by_workload_and_library(monkeypatch):
     assert bench.latest_profile(cfg, n) == tag
     assert bench.latest_profile(cfg, n // 8) is None  # another per-GPU batch size
     assert bench.latest_profile(3 if cfg != 3 else 4, n) is None
+    # another AIR or input form: another workload
+    air, form = _workload()
+    monkeypatch.setitem(bench.WORKLOAD, "air", "synthetic" if air != "synthetic" else "triton-size")
+    assert bench.latest_profile(cfg, n) is None
+    monkeypatch.setitem(bench.WORKLOAD, "air", air)
+    monkeypatch.setitem(bench.WORKLOAD, "input_form", "canonical" if form != "canonical" else "montgomery")
+    assert bench.latest_profile(cfg, n) is None
+    monkeypatch.setitem(bench.WORKLOAD, "input_form", form)
     # counters of another binary are never attached
     monkeypatch.setattr(bench, "lib_sha256", lambda path=None: "0" * 64)
     assert bench.latest_profile(cfg, n) is None

@@ -1,8 +1,8 @@
 """The three device forms of the Fiat-Shamir sponge replay (k_fs_replay_wide's 16-lane row and
 two-row pair, k_fs_replay_quad's four lanes per proof) on the same proofs: the 256 distinct config-4
 pool proofs (oracle/pool4.py, each with its oracle transcript) plus mutants whose absorbed items
-change (an OOD row word, an authentication word, the last polynomial).  NHIP_FS_FORM forces the form
-for the run (the library reads it at every launch); every verdict, every squeezed sample and every
+change (an OOD row word, an authentication word, the last polynomial).  nhip_set_fs_form forces the
+form for the run; every verdict, every squeezed sample and every
 sampled index must equal the oracle's whatever the form and the batch size (reference: the sponge
 of triton-vm's ProofStream; the forms are bit-identical restatements of one
 Tip5 permutation, tip5_device.hpp)."""
@@ -19,9 +19,19 @@ def pool():
     return bench.load_pool4()
 
 
-def _run(ctx, pool, sel, mutate, monkeypatch, form):
+FORMS = {"row": 0, "pair": 1, "quad": 2}
+
+
+@pytest.fixture
+def forced_form():
     import neptune_hip.stark as NS
-    monkeypatch.setenv("NHIP_FS_FORM", form)
+    yield NS.set_fs_form
+    NS.set_fs_form(-1)  # back to the batch-size rule
+
+
+def _run(ctx, pool, sel, mutate, set_form, form):
+    import neptune_hip.stark as NS
+    set_form(FORMS[form])
     gair = NS.Air([int(w) for w in pool["air"]])
     proofs = [np.array(pool["proofs"][j], dtype=np.uint64) for j in sel]
     for i, (pos, delta) in mutate.items():
@@ -36,7 +46,7 @@ def _run(ctx, pool, sel, mutate, monkeypatch, form):
 
 @pytest.mark.parametrize("form", ["quad", "row", "pair"])
 @pytest.mark.parametrize("n", [256, 1024])
-def test_fs_form_transcripts(ctx, pool, monkeypatch, form, n):
+def test_fs_form_transcripts(ctx, pool, forced_form, form, n):
     sel = [j % 256 for j in range(n)]
     # mutants: a word inside the proof body (absorbed by the sponge, so every later sample moves)
     rng = np.random.default_rng(0xF5 + n)
@@ -44,7 +54,7 @@ def test_fs_form_transcripts(ctx, pool, monkeypatch, form, n):
     for i in rng.choice(n, size=8, replace=False).tolist():
         L = len(pool["proofs"][sel[i]])
         mutate[int(i)] = (int(rng.integers(L // 4, L - 8)), 1)
-    v, tr = _run(ctx, pool, sel, mutate, monkeypatch, form)
+    v, tr = _run(ctx, pool, sel, mutate, forced_form, form)
     for i in range(n):
         want_xs, want_idx = pool["transcripts"][sel[i]]
         xs, idx, fail = tr[i]
@@ -52,7 +62,7 @@ def test_fs_form_transcripts(ctx, pool, monkeypatch, form, n):
             assert v[i] and fail == 0 and xs == want_xs and idx == want_idx, (form, n, i)
 
 
-def test_fs_forms_agree_on_mutants(ctx, pool, monkeypatch):
+def test_fs_forms_agree_on_mutants(ctx, pool, forced_form):
     """Rejected proofs still replay their whole sponge: the samples of mutated proofs are equal
     across the forms (the oracle transcript of a mutant is not stored, so the forms are held to each
     other, and the row form to the oracle on every accepting proof above)."""
@@ -63,7 +73,7 @@ def test_fs_forms_agree_on_mutants(ctx, pool, monkeypatch):
     for i in rng.choice(n, size=32, replace=False).tolist():
         L = len(pool["proofs"][sel[i]])
         mutate[int(i)] = (int(rng.integers(16, L - 8)), int(rng.integers(1, 1 << 63)))
-    runs = {f: _run(ctx, pool, sel, mutate, monkeypatch, f) for f in ("row", "pair", "quad")}
+    runs = {f: _run(ctx, pool, sel, mutate, forced_form, f) for f in ("row", "pair", "quad")}
     for f in ("pair", "quad"):
         assert runs[f][0] == runs["row"][0], f
         for i in range(n):

@@ -74,10 +74,17 @@ def test_queue_verdicts_and_coalescing_rate(ctx, pool_batch):
             th.join()
         rate_q = threads_n * rounds / (time.perf_counter() - t)
         st = q.stats()
+        prof = q.profile()
     assert not errors
     assert all(v == bool(expect[i]) for i, v in got)
     assert st["batches"] < st["proofs"] / 4, st  # calls were coalesced
     print(f"serialized {rate_ser:.0f} proofs/s, queue (64 threads) {rate_q:.0f} proofs/s, {st}")
+    nb = max(prof["batches"], 1)
+    print("queue per batch (ms): " + ", ".join(f"{k[3:]} {prof[k] / nb:.3f}" for k in prof if k.startswith("ms_")) +
+          f"; sizes {prof['size_hist']}")
+    # the profile counts the warm-up call's batch too
+    assert prof["batches"] == st["batches"] and sum(prof["size_hist"]) == prof["batches"]
+    assert prof["proofs"] == st["proofs"] and prof["ms_device"] > 0 and prof["ms_turnaround"] >= prof["ms_window"]
     # 13-16x on most boxes (7.6-9.7k vs 0.5-0.6k proofs/s); one box gave 9.3x (5.5k): the coalesced
     # rate leans on the host's copy threads, so the bound is the coalescing itself, not one box's rate
     assert rate_q >= 6 * rate_ser, (rate_q, rate_ser)

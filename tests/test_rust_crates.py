@@ -51,8 +51,8 @@ def _rust_struct_fields(name):
 
 
 def test_sys_structs_mirror_the_header():
-    for s in ("nhip_stark_params", "nhip_claim", "nhip_proof", "nhip_stats", "nhip_blk_block", "nhip_tx",
-              "nhip_pow_mast_paths"):
+    for s in ("nhip_stark_params", "nhip_claim", "nhip_proof", "nhip_stats", "nhip_queue_profile", "nhip_blk_block",
+              "nhip_tx", "nhip_pow_mast_paths"):
         assert _rust_struct_fields(s) == _c_struct_fields(s), s
 
 

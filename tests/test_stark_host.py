@@ -120,3 +120,55 @@ def test_air_descriptor_validation():
 
 def oracle_constraints(g, params):
     return _air_obj(g, params).num_constraints
+
+
+def test_montgomery_word_helpers():
+    """neptune_hip.stark.to_montgomery is twenty-first's in-memory form x * 2^64 mod p (any u64 read
+    mod p) and from_montgomery its inverse."""
+    import neptune_hip.stark as NS
+    rng = np.random.default_rng(0x4D)
+    xs = [0, 1, 2, S.P - 1, S.P, S.P + 1, (1 << 64) - 1, 1 << 32, (1 << 32) - 1] + \
+        [int(v) for v in rng.integers(0, 1 << 63, size=200, dtype=np.uint64)] + \
+        [int(v) | (1 << 63) for v in rng.integers(0, 1 << 63, size=200, dtype=np.uint64)]
+    m = NS.to_montgomery(xs)
+    for x, w in zip(xs, m):
+        assert int(w) == (x % S.P) * (1 << 64) % S.P
+    assert [int(v) for v in NS.from_montgomery(m)] == [x % S.P for x in xs]
+
+
+def test_host_decoder_montgomery_form(tiny):
+    """nhip_proof_decodes with input_form = Montgomery: every golden proof and every structural /
+    payload mutant (given as the same field elements in Montgomery words) decodes exactly as in the
+    canonical form; raw Montgomery words >= p (w + p, the same element) decode too."""
+    import neptune_hip.stark as NS
+    g, params = tiny
+    air = NS.Air([int(w) for w in g["air"]])
+    can = NS.Stark(num_collinearity_checks=8, num_main=24, num_aux=9)
+    mont = can.montgomery()
+    n = 0
+    for case in g["cases"]:
+        c = case["claim"]
+        claim = NS.Claim(c["digest"], c["version"], c["input"], c["output"])
+        mclaim = NS.montgomery_claim(claim)
+        proof = [int(w) for w in case["proof"]]
+        mp = [int(w) for w in NS.to_montgomery(proof)]
+        assert NS.proof_decodes(air, mont, mclaim, mp) is True
+        # the canonical words read as Montgomery words are other elements: the structure breaks
+        assert NS.proof_decodes(air, mont, mclaim, proof) is False
+        hi = [w + S.P if w < (1 << 64) - S.P else w for w in mp]
+        assert NS.proof_decodes(air, mont, mclaim, hi) is True
+        for m in _mutations(proof):
+            mm = [int(w) for w in NS.to_montgomery(m)]
+            assert NS.proof_decodes(air, mont, mclaim, mm) == NS.proof_decodes(air, can, claim, m)
+            n += 1
+    assert n > 300
+    for proof in ([], [0] * 65, [0], [1]):
+        assert NS.proof_decodes(air, mont, NS.Claim([1, 2, 3, 4, 5]), proof) is False
+    bad = dataclasses_replace(can, input_form=2)
+    with pytest.raises(Exception):
+        NS.proof_decodes(air, bad, NS.Claim([1, 2, 3, 4, 5]), [])
+
+
+def dataclasses_replace(obj, **kw):
+    import dataclasses
+    return dataclasses.replace(obj, **kw)
