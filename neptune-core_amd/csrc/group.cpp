@@ -184,7 +184,7 @@ struct StreamBatch {
     uint8_t* all_ok = nullptr;
     size_t n = 0;
     std::vector<std::vector<size_t>> idx;  // per member: the caller's positions of its share
-    bool live = false;                     // launched on some member, verdicts not yet written
+    bool live = false;                     // submitted, verdicts / AND not yet written
 };
 
 struct MemberSlots {
@@ -323,7 +323,7 @@ int nhip_group_stream_submit(nhip_group_stream* st, const nhip_claim* claims, co
             ms.v.resize(std::max<size_t>(1, st->sb[sp].idx[mm].size()));  // the previous share's verdicts
             if (!B.idx[mm].empty() || ms.in_flight[sp]) who.push_back(mm);
         }
-        B.live = n > 0;
+        B.live = true;  // an empty batch too: its AND (1) is written with the others'
         rc = st->on_members(who, [&](size_t mm) -> int {
             MemberSlots& ms = st->m[mm];
             nhip_ctx* c = st->g->members[mm];

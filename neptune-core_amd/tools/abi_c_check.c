@@ -6,16 +6,25 @@
  *                            file bytes round trip, group shard; prints the nhip_init return code
  *   abi_c_check verify FILE  verify the batch in FILE on one context and on a group of every
  *                            visible GPU; prints "ctx <verdicts>" and "group <verdicts> <all_ok>"
+ *   abi_c_check marshal N W  host only: time handing N proofs of W words each to the library in
+ *                            both input forms, as the Rust drop-in would.  The proofs sit in memory
+ *                            as twenty-first keeps Vec<BFieldElement> (Montgomery words).
+ *                            canonical: a new buffer per proof, every word reduced (BFieldElement::
+ *                            value(), montyred) - round 3's marshal; montgomery: the nhip_proof
+ *                            array points at the words as they lie (NHIP_INPUT_MONTGOMERY).
+ *                            Prints "marshal canonical_ms montgomery_ms bytes checksum".
  *
  * FILE (little-endian u64 stream, written by tests/test_capi_c.py):
  *   n_air, air[n_air], security_level, log2_fri_expansion, num_collinearity_checks, num_main,
  *   num_aux, num_quotient_segments, n, then per proof: digest[5], version, in_len, in[],
  *   out_len, out[], proof_len, proof[]
  */
+#define _POSIX_C_SOURCE 199309L
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "neptune_hip.h"
 
@@ -36,7 +45,8 @@ static int host_checks(void) {
     int rc, i;
 
     nhip_stark_params_default(&sp);
-    if (sp.security_level != 160 || sp.log2_fri_expansion != 2 || sp.num_collinearity_checks != 80)
+    if (sp.security_level != 160 || sp.log2_fri_expansion != 2 || sp.num_collinearity_checks != 80 ||
+        sp.input_form != NHIP_INPUT_CANONICAL)
         return fail("nhip_stark_params_default", -1);
     /* program.rs:374-390 / 565-572: big-endian 8-byte chunks, BFieldElement::new on the way in */
     if ((rc = nhip_proof_to_be_bytes(words, 4, bytes)) != NHIP_OK) return fail("nhip_proof_to_be_bytes", rc);
@@ -57,6 +67,66 @@ static int host_checks(void) {
     printf("init %d\n", rc);
     if (rc == NHIP_OK) nhip_destroy(ctx);
     printf("host ok\n");
+    return 0;
+}
+
+static double now_ms(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec * 1e3 + (double)t.tv_nsec * 1e-6;
+}
+
+/* twenty-first's montyred(x, 0): a Montgomery word's canonical value (BFieldElement::value()) */
+static uint64_t value_of(uint64_t xl) {
+    const uint64_t P_EPS = 0xFFFFFFFFull;
+    uint64_t a = xl + (xl << 32);
+    uint64_t e = a < xl ? 1u : 0u;
+    uint64_t b = a - (a >> 32) - e;
+    uint64_t r = 0 - b;
+    return b > 0 ? r - P_EPS : r;
+}
+
+static int marshal_timing(size_t n, size_t w) {
+    uint64_t **mem = (uint64_t **)calloc(n, sizeof(uint64_t *));
+    uint64_t **canon = (uint64_t **)calloc(n, sizeof(uint64_t *));
+    nhip_proof *pc = (nhip_proof *)calloc(n, sizeof(nhip_proof));
+    nhip_proof *pm = (nhip_proof *)calloc(n, sizeof(nhip_proof));
+    uint64_t x = 0x9E3779B97F4A7C15ull, sum = 0;
+    double t0, t1, t2;
+    size_t i, k;
+    if (!mem || !canon || !pc || !pm) return fail("allocation", -1);
+    for (i = 0; i < n; ++i) {  /* the node's proofs: Montgomery words, one allocation per proof */
+        mem[i] = (uint64_t *)malloc(w * 8);
+        if (!mem[i]) return fail("allocation", -1);
+        for (k = 0; k < w; ++k) {
+            x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+            mem[i][k] = x % 0xFFFFFFFF00000001ull;
+        }
+    }
+    t0 = now_ms();
+    for (i = 0; i < n; ++i) {  /* canonical: words(&p.0) = a new Vec<u64> of value()s */
+        canon[i] = (uint64_t *)malloc(w * 8);
+        if (!canon[i]) return fail("allocation", -1);
+        for (k = 0; k < w; ++k) canon[i][k] = value_of(mem[i][k]);
+        pc[i].words = canon[i];
+        pc[i].len = w;
+    }
+    t1 = now_ms();
+    for (i = 0; i < n; ++i) {  /* montgomery: the words as they lie */
+        pm[i].words = mem[i];
+        pm[i].len = w;
+    }
+    t2 = now_ms();
+    for (i = 0; i < n; ++i) sum += pc[i].words[w - 1] ^ pm[i].words[0];
+    printf("marshal %.3f %.6f %llu %llu\n", t1 - t0, t2 - t1, (unsigned long long)(n * w * 8), (unsigned long long)sum);
+    for (i = 0; i < n; ++i) {
+        free(mem[i]);
+        free(canon[i]);
+    }
+    free(mem);
+    free(canon);
+    free(pc);
+    free(pm);
     return 0;
 }
 
@@ -100,6 +170,7 @@ static int verify_file(const char *path) {
         if ((rc = nhip_air_create(w + pos, (size_t)n_air, &air)) != NHIP_OK) return fail("nhip_air_create", rc);
         pos += (size_t)n_air;
     }
+    nhip_stark_params_default(&sp); /* input_form: canonical */
     {
         uint64_t t[6];
         for (i = 0; i < 6; ++i) TAKE(t[i]);
@@ -165,6 +236,8 @@ static int verify_file(const char *path) {
 int main(int argc, char **argv) {
     if (argc >= 2 && strcmp(argv[1], "host") == 0) return host_checks();
     if (argc >= 3 && strcmp(argv[1], "verify") == 0) return verify_file(argv[2]);
-    fprintf(stderr, "usage: %s host | verify FILE\n", argv[0]);
+    if (argc >= 4 && strcmp(argv[1], "marshal") == 0)
+        return marshal_timing((size_t)strtoull(argv[2], NULL, 10), (size_t)strtoull(argv[3], NULL, 10));
+    fprintf(stderr, "usage: %s host | verify FILE | marshal N_PROOFS WORDS\n", argv[0]);
     return 2;
 }

@@ -34,6 +34,17 @@ def test_c_consumer_builds_and_host_entry_points():
         assert "init 1" in out.stdout  # NHIP_ERR_NO_DEVICE
 
 
+def test_c_consumer_marshal_timing():
+    """The harness times handing proofs over in both input forms (round 3's per-word canonical
+    conversion + copy vs the Montgomery words as they lie); small here, 4,096 proofs on the GPU box."""
+    subprocess.check_call(["make", "-s", "-C", PKG, "build/abi_c_check"])
+    out = subprocess.run([EXE, "marshal", "64", "20000"], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stdout + out.stderr
+    tag, canon_ms, mont_ms, nbytes, _ = out.stdout.split()
+    assert tag == "marshal" and int(nbytes) == 64 * 20000 * 8
+    assert float(canon_ms) > float(mont_ms) >= 0
+
+
 def _batch_file(path, air, stark, cases):
     w = [len(air)] + list(air)
     w += [stark.security_level, stark.log2_fri_expansion, stark.num_collinearity_checks, stark.num_main,
