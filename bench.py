@@ -1048,14 +1048,19 @@ def main():
                     job_claims, job_proofs, job_expect, _, _, _ = make_config4(pool4, total, 0.01, 1, 0)
                 dcl, dpr = device_form(job_claims, job_proofs, mont)
                 t = time.time()
-                res["group_stream"] = group_stream(range(world), air_words, stark, dcl, dpr, job_expect,
-                                                   args.group_batches)
+                # every GPU the job's ranks use (a gloo rehearsal puts several ranks on one GPU)
+                devs = sorted({r if dist is None or os.environ.get("NHIP_DIST_BACKEND", "nccl") == "nccl"
+                               else r % max(1, __import__("torch").cuda.device_count()) for r in range(world)})
+                res["group_stream"] = group_stream(devs, air_words, stark, dcl, dpr, job_expect, args.group_batches)
                 if "pcie_inclusive" in res:
                     res["group_stream"]["vs_pcie_inclusive"] = res["group_stream"]["value"] / res["pcie_inclusive"]["value"]
                 correct = correct and res["group_stream"]["verdicts_correct"]
                 log(f"[group] {res['group_stream']['value']:.0f} proofs/s over {world} GPU(s) ({time.time() - t:.1f}s)")
             except Exception as e:  # noqa: BLE001 -- a leg, never the headline
                 res["group_stream"] = {"error": repr(e)}
+            if dist is not None:
+                import torch
+                torch.cuda.set_device(dev_index)  # the members' threads ran on the other devices
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()

@@ -164,7 +164,14 @@ int nhip_init(uint32_t device_mask, nhip_ctx** out) {
     nhip_ctx* c = new (std::nothrow) nhip_ctx();
     if (!c) return NHIP_ERR_OOM;
     c->device = dev;
-    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    // the caller's current device is left as it was (a host with its own HIP user, e.g. torch,
+    // must not find another device current after creating a context)
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    const bool ok = hipSetDevice(dev) == hipSuccess &&
+                    hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+    if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    if (!ok) {
         delete c;
         return NHIP_ERR_HIP;
     }

@@ -331,8 +331,14 @@ __global__ void __launch_bounds__(256, NHIP_ROWS_WAVES) k_hash_rows(const uint64
             const uint32_t pos = c * TIP5_RATE;
             const bool last = c + 1 == nchunks;
             if (!last) {
+                // five 16-byte loads per chunk (8-byte aligned: gfx950 global loads need dword alignment)
 #pragma unroll
-                for (int q = 0; q < TIP5_RATE; ++q) s[q] = word_mont<MW>(row[pos + q]);
+                for (int q = 0; q < TIP5_RATE; q += 2) {
+                    uint64_t pr[2];
+                    __builtin_memcpy(pr, row + pos + q, 16);
+                    s[q] = word_mont<MW>(pr[0]);
+                    s[q + 1] = word_mont<MW>(pr[1]);
+                }
             } else {
                 const uint32_t rem = width - pos;
 #pragma unroll

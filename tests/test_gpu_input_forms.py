@@ -67,7 +67,8 @@ def test_montgomery_mutants_and_noncanonical_words(ctx, c4):
         for _ in range(6):
             m = p.copy()
             pos = int(rng.integers(10, len(p)))
-            m[pos] = np.uint64((int(m[pos]) + int(rng.choice([1, S.P - 1, int(rng.integers(1, S.P))]))) % S.P)
+            delta = [1, S.P - 1, int(rng.integers(1, 1 << 63))][int(rng.integers(0, 3))]
+            m[pos] = np.uint64((int(m[pos]) + delta) % S.P)
             cl.append(claims[i])
             pr.append(m)
     got_can = NS.verify_batch(ctx, air, can, [(NS.Claim(*c), p) for c, p in zip(cl, pr)])
