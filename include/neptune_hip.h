@@ -223,7 +223,9 @@ void nhip_batch_destroy(nhip_batch *batch);
  * call: blocking, thread-safe, nhip_verify_batch semantics for its own proofs; a worker thread
  * gathers the proofs of every caller waiting at the time (up to max_batch proofs, at most
  * max_wait_us after the oldest arrival) into one device batch, with the next batch collected while
- * the current one runs.  max_batch 0 = 4096. */
+ * the current one runs.  Each caller copies its proofs into the queue's pinned arena itself (in
+ * parallel with the other callers), so the worker only DMAs them; a request the arena cannot hold
+ * at the time goes through the context's staging instead.  max_batch 0 = 4096. */
 typedef struct nhip_queue nhip_queue;
 int nhip_queue_create(nhip_ctx *ctx, nhip_air *air, const nhip_stark_params *params, uint32_t max_batch,
                       uint32_t max_wait_us, nhip_queue **out);
@@ -242,6 +244,8 @@ typedef struct {
     double ms_device;        /* device: first phase start -> verdicts (k_decode to the verdict copy) */
     double ms_wait;          /* worker blocked in nhip_batch_wait on the batch (not overlapped) */
     double ms_turnaround;    /* oldest request's arrival -> its verdicts delivered */
+    uint64_t pinned_proofs;  /* proofs their caller's thread copied into the queue's pinned arena (DMA'd
+                                from there without a staging copy on the worker) */
 } nhip_queue_profile;
 int nhip_queue_profile_read(const nhip_queue *queue, nhip_queue_profile *out, int reset);
 /* Drains the pending requests, then stops the worker. */

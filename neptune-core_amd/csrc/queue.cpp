@@ -21,6 +21,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <new>
 #include <system_error>
@@ -46,7 +47,43 @@ struct Req {
     Clock::time_point arrived;
     int rc = NHIP_OK;
     bool done = false;
+    uint64_t arena_at = ~0ull;  // its proofs' range in the pinned arena (~0: its own memory)
 };
+
+// Pinned receive arena of a queue: a ring of monotonically growing offsets.  A caller takes a
+// contiguous range for its proofs (under the queue lock), copies them in on its own thread (no
+// lock held), and the worker releases the range once the batch holding them has been uploaded
+// (nhip_batch_refill waits for its uploads).  Ranges are taken in arrival order but may be
+// released out of order (two slots); the ring's tail advances over released ranges only.
+struct PinnedRing {
+    uint8_t* base = nullptr;
+    uint64_t cap = 0, head = 0, tail = 0;
+    std::map<uint64_t, std::pair<uint64_t, bool>> live;  // start -> (bytes, released)
+
+    uint64_t take(uint64_t n) {
+        if (!base || n == 0 || n > cap) return ~0ull;
+        uint64_t at = head;
+        if (at % cap + n > cap) at += cap - at % cap;  // would wrap: start at the ring's beginning
+        if (at + n - tail > cap) return ~0ull;           // full
+        live.emplace(at, std::make_pair(n, false));
+        head = at + n;
+        return at;
+    }
+    void release(uint64_t at) {
+        auto it = live.find(at);
+        if (it == live.end()) return;
+        it->second.second = true;
+        while (!live.empty() && live.begin()->second.second) {
+            tail = live.begin()->first + live.begin()->second.first;
+            live.erase(live.begin());
+        }
+        if (live.empty()) tail = head;
+    }
+    uint8_t* ptr(uint64_t at) const { return base + at % cap; }
+};
+
+// arena size: about two full batches of config-4-sized proofs from concurrent callers
+constexpr uint64_t ARENA_BYTES = 256ull << 20;
 
 }  // namespace
 
@@ -70,6 +107,7 @@ struct nhip_queue {
     std::vector<nhip_proof> proofs;
     std::vector<uint8_t> verdicts;
     std::atomic<uint64_t> n_batches{0}, n_proofs{0};
+    PinnedRing ring;  // guarded by mu
     // nhip_queue_profile: written by the worker under prof_mu, read by nhip_queue_profile_read
     mutable std::mutex prof_mu;
     nhip_queue_profile prof{};
@@ -131,6 +169,11 @@ struct nhip_queue {
         int rc = slot[s] ? nhip_batch_refill(ctx, slot[s], air, &params, claims.data(), proofs.data(), claims.size())
                          : nhip_batch_prepare(ctx, air, &params, claims.data(), proofs.data(), claims.size(), &slot[s]);
         const Clock::time_point t1 = Clock::now();
+        {  // uploaded (or failed): the requests' arena ranges can take new proofs
+            std::lock_guard<std::mutex> g(mu);
+            for (Req* r : in_slot[s])
+                if (r->arena_at != ~0ull) ring.release(r->arena_at);
+        }
         if (!rc) rc = nhip_batch_launch(ctx, slot[s]);
         const Clock::time_point t2 = Clock::now();
         if (rc) {
@@ -148,6 +191,7 @@ struct nhip_queue {
         prof.proofs += n;
         prof.size_hist[std::min<size_t>(7, n <= 1 ? 0 : (size_t)(63 - __builtin_clzll((unsigned long long)n)))] += 1;
         prof.ms_window += ms_since(oldest[s], t0);
+        for (Req* r : in_slot[s]) prof.pinned_proofs += r->arena_at != ~0ull ? r->n : 0;
         prof.ms_stage += st.ms_decode;
         prof.ms_upload += st.ms_upload;
         prof.ms_launch += ms_since(t1, t2);
@@ -221,15 +265,24 @@ int nhip_queue_create(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* par
     q->params = *params;
     q->max_batch = max_batch ? max_batch : 4096;
     q->max_wait = std::chrono::microseconds(max_wait_us);
+    {
+        void* a = nullptr;
+        if (nhip_host_alloc(ARENA_BYTES, &a) == NHIP_OK) {  // without it every request is staged
+            q->ring.base = (uint8_t*)a;
+            q->ring.cap = ARENA_BYTES;
+        }
+    }
     try {
         // a slot holds at most max_batch requests (each of >= 1 proof): the worker's push_back
         // under its lock never allocates
         for (auto& v : q->in_slot) v.reserve(std::min<size_t>(q->max_batch, 1u << 16) + 1);
         q->worker = std::thread([q] { q->run(); });
     } catch (const std::system_error&) {
+        if (q->ring.base) nhip_host_free(q->ring.base);
         delete q;
         return NHIP_ERR_HIP;
     } catch (const std::bad_alloc&) {
+        if (q->ring.base) nhip_host_free(q->ring.base);
         delete q;
         return NHIP_ERR_OOM;
     }
@@ -247,12 +300,44 @@ int nhip_queue_verify(nhip_queue* q, const nhip_claim* claims, const nhip_proof*
             (claims[i].output_len && !claims[i].output) || claims[i].input_len > 0xFFFFFFFFull ||
             claims[i].output_len > 0xFFFFFFFFull)
             return NHIP_ERR_ARG;
-    Req r{claims, proofs, n, verdicts, Clock::now()};
+    // this caller's proofs into the pinned arena, copied on this thread while the other callers copy
+    // theirs: the worker then DMAs them without a staging copy (adjacent requests as one copy)
+    uint64_t bytes = 0;
+    for (size_t i = 0; i < n; ++i) bytes += proofs[i].len * 8;
+    std::vector<nhip_proof> mine;
+    uint64_t at = ~0ull;
+    {
+        std::lock_guard<std::mutex> g(q->mu);
+        if (q->stop) return NHIP_ERR_ARG;
+        at = q->ring.take(bytes);
+    }
+    if (at != ~0ull) {
+        try {
+            mine.resize(n);
+        } catch (const std::bad_alloc&) {
+            std::lock_guard<std::mutex> g(q->mu);
+            q->ring.release(at);
+            return NHIP_ERR_OOM;
+        }
+        uint8_t* dst = q->ring.ptr(at);
+        for (size_t i = 0; i < n; ++i) {
+            if (proofs[i].len) std::memcpy(dst, proofs[i].words, proofs[i].len * 8);
+            mine[i].words = proofs[i].len ? (const uint64_t*)dst : nullptr;
+            mine[i].len = proofs[i].len;
+            dst += proofs[i].len * 8;
+        }
+    }
+    Req r{claims, at != ~0ull ? mine.data() : proofs, n, verdicts, Clock::now()};
+    r.arena_at = at;
     std::unique_lock<std::mutex> lk(q->mu);
-    if (q->stop) return NHIP_ERR_ARG;
+    if (q->stop) {
+        if (at != ~0ull) q->ring.release(at);
+        return NHIP_ERR_ARG;
+    }
     try {
         q->pending.push_back(&r);
     } catch (const std::bad_alloc&) {
+        if (at != ~0ull) q->ring.release(at);
         return NHIP_ERR_OOM;
     }
     q->pending_proofs += n;
@@ -286,6 +371,7 @@ void nhip_queue_destroy(nhip_queue* q) {
     q->worker.join();
     for (nhip_batch* b : q->slot)
         if (b) nhip_batch_destroy(b);
+    if (q->ring.base) nhip_host_free(q->ring.base);
     delete q;
 }
 

@@ -65,7 +65,7 @@ class QueueProfile(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("proofs", ctypes.c_uint64), ("size_hist", ctypes.c_uint64 * 8),
                 ("ms_window", ctypes.c_double), ("ms_stage", ctypes.c_double), ("ms_upload", ctypes.c_double),
                 ("ms_launch", ctypes.c_double), ("ms_device", ctypes.c_double), ("ms_wait", ctypes.c_double),
-                ("ms_turnaround", ctypes.c_double)]
+                ("ms_turnaround", ctypes.c_double), ("pinned_proofs", ctypes.c_uint64)]
 
     def as_dict(self):
         d = {f: getattr(self, f) for f, _ in self._fields_}

@@ -105,6 +105,7 @@ pub struct nhip_queue_profile {
     pub ms_device: f64,
     pub ms_wait: f64,
     pub ms_turnaround: f64,
+    pub pinned_proofs: u64,
 }
 
 #[repr(C)]
