@@ -108,6 +108,9 @@ struct nhip_air {
     std::vector<uint32_t> prog_off;
     std::vector<Xfe> consts;
     uint32_t slots = 0;
+    // slots held in LDS (the rest in the per-proof global area): AIR_LDS_SLOTS_MAX, or less when
+    // NHIP_OOD_LDS_SLOTS asks for it at creation (tests of the global-slot path)
+    uint32_t lds_cap = AIR_LDS_SLOTS_MAX;
     // device copies, one per GPU that has used this AIR (read-only, so every context on that GPU
     // shares it; a group drives several contexts from one process, possibly concurrently);
     // created on first use, freed with the AIR
@@ -254,71 +257,161 @@ int air_upload(nhip_ctx* ctx, nhip_air* a, nhip_air::Dev* out) {
     return NHIP_OK;
 }
 
-// Compile the levelized circuit into the slot program of k_ood_air (OodIns, stark.hpp).
-void air_compile(nhip_air* a, const std::vector<uint32_t>& level, uint32_t max_level,
-                 const std::vector<uint32_t>& cons) {
+// Instructions per step of the compiled AIR program (NHIP_OOD_STEP_WIDTH overrides, A/B runs):
+// two per thread of k_ood_air's 256-thread workgroups.
+uint32_t ood_step_width() {
+    static const uint32_t w = [] {
+        const char* e = std::getenv("NHIP_OOD_STEP_WIDTH");
+        const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 10) : 512u;
+        return v >= 16 && v <= (1u << 16) ? v : 512u;
+    }();
+    return w;
+}
+
+// Compile the circuit into the slot program of k_ood_air (OodIns, stark.hpp): a sequence of
+// steps, each a set of independent instructions the workgroup runs between two barriers, every
+// value in a slot from the step that computes it to the step of its last use (a slot is reused
+// from the step after).  The steps come from list scheduling with a liveness priority instead of
+// the circuit's levels: a level-by-level program keeps every value of a wide level live at once
+// (triton-air-sized circuits: ~13k slots, half of them past the LDS budget in global memory), while
+// here each step takes up to `width` ready nodes, those that retire an operand (its last use) first,
+// then in the order of the first constraint that needs them, so constraints are finished one after
+// another and their values released (the same circuit: ~2.3k slots, all in LDS, 3x the steps).
+// A step never takes a node past the LDS slot budget unless it retires a value or the step would be
+// empty.  Constraint accumulations (OOD_ACC) run in the step after their value.  Within a step the
+// instructions are grouped by kind (loads, products, sums, accumulations): a wave then runs one kind
+// of XFE operation instead of the divergent union of several.
+void air_compile(nhip_air* a, const std::vector<uint32_t>& cons, uint32_t width) {
     const size_t NN = a->nodes.size();
-    const uint32_t n_lv = max_level + 2;  // + one level for the accumulation of top-level constraints
-    std::vector<int64_t> last(NN, -1);
-    for (size_t i = 0; i < NN; ++i) {
-        const AirNode& nd = a->nodes[i];
-        if (nd.op == AIR_ADD || nd.op == AIR_SUB || nd.op == AIR_MUL) {
-            last[nd.a] = std::max<int64_t>(last[nd.a], level[i]);
-            last[nd.b] = std::max<int64_t>(last[nd.b], level[i]);
-        }
-    }
-    for (uint32_t c : cons) last[c] = std::max<int64_t>(last[c], (int64_t)level[c] + 1);
-    std::vector<std::vector<uint32_t>> by_level(n_lv), release(n_lv + 1);
-    for (size_t i = 0; i < NN; ++i) by_level[level[i]].push_back((uint32_t)i);
-    std::vector<uint32_t> ref(NN, 0), free_slots;
-    std::vector<std::vector<OodIns>> lv_prog(n_lv);
-    uint32_t next_slot = 0;
-    auto alloc = [&](uint32_t i) {
-        uint32_t sl;
-        if (!free_slots.empty()) {
-            sl = free_slots.back();
-            free_slots.pop_back();
-        } else {
-            sl = next_slot++;
-        }
-        ref[i] = OOD_REF_SLOT | sl;
-        release[last[i] + 1].push_back(sl);
-        return sl;
+    const auto is_op = [&](size_t i) {
+        const uint32_t op = a->nodes[i].op;
+        return op == AIR_ADD || op == AIR_SUB || op == AIR_MUL;
     };
-    for (uint32_t l = 0; l < n_lv; ++l) {
-        for (uint32_t sl : release[l]) free_slots.push_back(sl);
-        for (uint32_t i : by_level[l]) {
-            const AirNode& nd = a->nodes[i];
-            if (nd.op == AIR_CONST) {
-                ref[i] = OOD_REF_CONST | (uint32_t)a->consts.size();
-                a->consts.push_back(Xfe{nd.k0, nd.k1, nd.k2});
-            } else if (nd.op == AIR_INPUT) {
-                if (last[i] < 0) continue;
-                const uint32_t sl = alloc(i);
-                lv_prog[l].push_back(OodIns{OOD_LOAD, OOD_REF_INPUT | (nd.a << 27) | nd.b, 0, sl});
-            } else {
-                if (last[i] < 0) continue;  // dead node
-                const uint32_t ra = ref[nd.a], rb = ref[nd.b];
-                const uint32_t sl = alloc(i);
-                lv_prog[l].push_back(OodIns{nd.op, ra, rb, sl});
+    // nodes the constraints reach, each with the first constraint (descriptor order) that needs it
+    std::vector<uint32_t> corder(NN, UINT32_MAX);
+    {
+        std::vector<uint32_t> st;
+        for (size_t c = 0; c < cons.size(); ++c) {
+            st.push_back(cons[c]);
+            while (!st.empty()) {
+                const uint32_t i = st.back();
+                st.pop_back();
+                if (corder[i] != UINT32_MAX) continue;
+                corder[i] = (uint32_t)c;
+                if (is_op(i)) {
+                    st.push_back(a->nodes[i].a);
+                    st.push_back(a->nodes[i].b);
+                }
             }
         }
     }
-    for (size_t c = 0; c < cons.size(); ++c)
-        lv_prog[level[cons[c]] + 1].push_back(OodIns{OOD_ACC, ref[cons[c]], (uint32_t)c, 0});
-    // Within a level every instruction is independent (its operands come from earlier levels), so
-    // each level is grouped by kind: a wave then runs one kind of XFE operation instead of the
-    // divergent union of several (a product where any lane multiplies, an add where any lane adds).
-    auto kind_rank = [](uint32_t op) {
-        return op == OOD_LOAD ? 0 : (op == AIR_MUL ? 1 : (op == OOD_ACC ? 3 : 2));
+    // operand refs: constants in the table, inputs and results in slots
+    std::vector<uint32_t> ref(NN, 0);
+    std::vector<uint8_t> slotted(NN, 0);
+    for (size_t i = 0; i < NN; ++i) {
+        if (corder[i] == UINT32_MAX) continue;  // dead node
+        if (a->nodes[i].op == AIR_CONST) {
+            ref[i] = OOD_REF_CONST | (uint32_t)a->consts.size();
+            a->consts.push_back(Xfe{a->nodes[i].k0, a->nodes[i].k1, a->nodes[i].k2});
+        } else {
+            slotted[i] = 1;
+        }
+    }
+    // remaining uses of each slotted value (operand occurrences + accumulations), pending operands of
+    // each node, and the users of each value (CSR)
+    std::vector<uint32_t> remaining(NN, 0), deps(NN, 0), uoff(NN + 1, 0);
+    for (size_t i = 0; i < NN; ++i)
+        if (slotted[i] && is_op(i))
+            for (uint32_t o : {a->nodes[i].a, a->nodes[i].b})
+                if (slotted[o]) ++remaining[o], ++deps[i], ++uoff[o + 1];
+    for (uint32_t c : cons)
+        if (slotted[c]) ++remaining[c];
+    for (size_t i = 0; i < NN; ++i) uoff[i + 1] += uoff[i];
+    std::vector<uint32_t> users(uoff[NN]);
+    {
+        std::vector<uint32_t> fill(uoff.begin(), uoff.end() - 1);
+        for (size_t i = 0; i < NN; ++i)
+            if (slotted[i] && is_op(i))
+                for (uint32_t o : {a->nodes[i].a, a->nodes[i].b})
+                    if (slotted[o]) users[fill[o]++] = (uint32_t)i;
+    }
+    std::vector<std::vector<uint32_t>> acc_of(NN);  // constraint indices accumulating a slotted node
+    std::vector<OodIns> step0_acc;                  // constraints on constants: accumulated in step 0
+    for (size_t c = 0; c < cons.size(); ++c) {
+        if (slotted[cons[c]]) acc_of[cons[c]].push_back((uint32_t)c);
+        else step0_acc.push_back(OodIns{OOD_ACC, ref[cons[c]], (uint32_t)c, 0});
+    }
+    std::vector<uint32_t> ready;
+    for (size_t i = 0; i < NN; ++i)
+        if (slotted[i] && deps[i] == 0) ready.push_back((uint32_t)i);
+    const uint32_t budget = AIR_LDS_SLOTS_MAX;
+    std::vector<uint32_t> free_slots, to_free;
+    uint32_t next_slot = 0, live = 0;
+    std::vector<OodIns> cur, acc_next = step0_acc;
+    std::vector<std::pair<int32_t, uint64_t>> key(NN);
+    auto retires = [&](uint32_t i) {  // operands whose last use this node is
+        if (!is_op(i)) return 0;
+        const uint32_t x = a->nodes[i].a, y = a->nodes[i].b;
+        int r = 0;
+        if (slotted[x] && remaining[x] == (x == y ? 2u : 1u)) ++r;
+        if (slotted[y] && y != x && remaining[y] == 1u) ++r;
+        return r;
     };
-    for (auto& lp : lv_prog)
-        std::stable_sort(lp.begin(), lp.end(),
-                         [&](const OodIns& x, const OodIns& y) { return kind_rank(x.op) < kind_rank(y.op); });
+    auto use = [&](uint32_t o) {  // a read of o in this step (its slot index is ref[o])
+        if (slotted[o] && --remaining[o] == 0) to_free.push_back(ref[o]);
+    };
     a->prog_off.assign(1, 0);
-    for (uint32_t l = 0; l < n_lv; ++l) {
-        a->prog.insert(a->prog.end(), lv_prog[l].begin(), lv_prog[l].end());
+    while (!ready.empty() || !acc_next.empty()) {
+        cur.swap(acc_next);  // the accumulations of the values of the step before
+        acc_next.clear();
+        for (const OodIns& ins : cur)
+            if (slotted[cons[ins.b]]) use(cons[ins.b]);
+        for (uint32_t i : ready) key[i] = {-retires(i), ((uint64_t)corder[i] << 32) | i};
+        std::sort(ready.begin(), ready.end(), [&](uint32_t x, uint32_t y) { return key[x] < key[y]; });
+        std::vector<uint32_t> chosen, rest;
+        for (uint32_t i : ready) {
+            if (chosen.size() < width && (live < budget || key[i].first < 0 || chosen.empty())) {
+                chosen.push_back(i);
+                ++live;
+            } else {
+                rest.push_back(i);
+            }
+        }
+        ready.swap(rest);
+        for (uint32_t i : chosen) {
+            uint32_t sl;
+            if (!free_slots.empty()) {
+                sl = free_slots.back();
+                free_slots.pop_back();
+            } else {
+                sl = next_slot++;
+            }
+                const AirNode& nd = a->nodes[i];
+            if (nd.op == AIR_INPUT) {
+                cur.push_back(OodIns{OOD_LOAD, OOD_REF_INPUT | (nd.a << 27) | nd.b, 0, sl});
+            } else {
+                cur.push_back(OodIns{nd.op, ref[nd.a], ref[nd.b], sl});
+                use(nd.a);
+                use(nd.b);
+            }
+            ref[i] = OOD_REF_SLOT | sl;
+            for (uint32_t c : acc_of[i]) acc_next.push_back(OodIns{OOD_ACC, ref[i], c, 0});
+        }
+        for (uint32_t i : chosen)
+            for (uint32_t k = uoff[i]; k < uoff[i + 1]; ++k)
+                if (--deps[users[k]] == 0) ready.push_back(users[k]);
+        // values whose last use was in this step: their slots take new values from the next step on
+        live -= (uint32_t)to_free.size();
+        free_slots.insert(free_slots.end(), to_free.begin(), to_free.end());
+        to_free.clear();
+        auto kind_rank = [](uint32_t op) {
+            return op == OOD_LOAD ? 0 : (op == AIR_MUL ? 1 : (op == OOD_ACC ? 3 : 2));
+        };
+        std::stable_sort(cur.begin(), cur.end(),
+                         [&](const OodIns& x, const OodIns& y) { return kind_rank(x.op) < kind_rank(y.op); });
+        a->prog.insert(a->prog.end(), cur.begin(), cur.end());
         a->prog_off.push_back((uint32_t)a->prog.size());
+        cur.clear();
     }
     a->slots = next_slot;
 }
@@ -405,7 +498,9 @@ int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
         cons[i] = (uint32_t)cw[i];
     }
     a->cons_off = make_uint4((uint32_t)nc[0], (uint32_t)(nc[0] + nc[1]), (uint32_t)(nc[0] + nc[1] + nc[2]), (uint32_t)C);
-    air_compile(a, level, max_level, cons);
+    air_compile(a, cons, ood_step_width());
+    if (const char* e = std::getenv("NHIP_OOD_LDS_SLOTS"))
+        a->lds_cap = std::min<uint32_t>(AIR_LDS_SLOTS_MAX, (uint32_t)std::strtoul(e, nullptr, 10));
     *out = a;
     return NHIP_OK;
 }
@@ -432,7 +527,7 @@ int nhip_air_info(const nhip_air* a, uint32_t* num_nodes, uint32_t* num_levels, 
 // Slots of the compiled AIR program: held in LDS, and past the LDS budget (global memory).
 int nhip_air_slots(const nhip_air* a, uint32_t* lds_slots, uint32_t* global_slots) {
     if (!a) return NHIP_ERR_ARG;
-    const uint32_t l = std::min<uint32_t>(a->slots, AIR_LDS_SLOTS_MAX);
+    const uint32_t l = std::min<uint32_t>(a->slots, a->lds_cap);
     if (lds_slots) *lds_slots = l;
     if (global_slots) *global_slots = a->slots - l;
     return NHIP_OK;
@@ -718,7 +813,7 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
                              N1 * k * 8,
                              N1 * H.max_last_cw * 40,
                              // OOD slots past the LDS budget (an AIR larger than ~6K live XFEs)
-                             N1 * (size_t)(air->slots - std::min<uint32_t>(air->slots, AIR_LDS_SLOTS_MAX)) * 24 + 24,
+                             N1 * (size_t)(air->slots - std::min<uint32_t>(air->slots, air->lds_cap)) * 24 + 24,
                              // per (proof, tree group, level) op ranges of the plan (k_mp_climb)
                              N1 * (1 + H.max_R) * (size_t)(levels + 1) * 8,
                              N1 * (1 + H.max_R) * (size_t)(levels + 1) * 4,
@@ -804,7 +899,7 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         dv.air_n_levels = (uint32_t)air->prog_off.size() - 1;
         dv.air_consts = adev.d_consts;
         dv.air_cons_off = air->cons_off;
-        dv.air_lds_slots = std::min<uint32_t>(air->slots, AIR_LDS_SLOTS_MAX);
+        dv.air_lds_slots = std::min<uint32_t>(air->slots, air->lds_cap);
         dv.air_gslot_n = air->slots - dv.air_lds_slots;
         dv.air_gslots = (Xfe*)ptr[21];
         dv.mp.lvl_g0 = (uint64_t*)ptr[22];

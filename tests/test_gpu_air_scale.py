@@ -1,9 +1,11 @@
 """The OOD AIR evaluator at triton-air's size class (SURVEY §7 hard part 2; triton-air 1.0.0,
 Cargo.lock:4194, ~600 constraints, tens of thousands of circuit nodes after degree lowering):
 the synthetic AIR with 620 constraints, bloated to ~22k nodes by identically-zero terms
-(stark_ref.bloat_air: same constraint values, real evaluation work), needs more value slots than
-LDS holds, so k_ood_air runs with its global-memory slot overflow.  An accepting proof and
-mutated ones give the oracle's verdicts, and the Fiat-Shamir transcript is the oracle's."""
+(stark_ref.bloat_air: same constraint values, real evaluation work).  Its compiled program (the
+liveness-priority schedule of stark_host.cpp air_compile) keeps every value in LDS; the same circuit
+with the LDS part capped (NHIP_OOD_LDS_SLOTS at creation) runs k_ood_air's global-memory slot
+overflow.  An accepting proof and mutated ones give the oracle's verdicts either way, and the
+Fiat-Shamir transcript is the oracle's."""
 import numpy as np
 import pytest
 
@@ -14,7 +16,7 @@ import tip5_ref as T
 pytestmark = pytest.mark.gpu
 
 
-def test_triton_air_sized_circuit_uses_global_slots_and_matches_oracle(ctx):
+def test_triton_air_sized_circuit_matches_oracle_in_lds_and_with_global_slots(ctx, monkeypatch):
     import neptune_hip.stark as NS
     T.use_c_backend()
     params = S.StarkParams()
@@ -25,7 +27,12 @@ def test_triton_air_sized_circuit_uses_global_slots_and_matches_oracle(ctx):
     proof, _ = F.prove(params, big, recipe, claim, 10, seed=0xA1)
     gair = NS.Air(big.to_words())
     info = gair.info()
-    assert info["global_slots"] > 0, info  # the overflow path is exercised
+    assert info["global_slots"] == 0 and info["lds_slots"] < 4000, info  # the schedule fits LDS
+    monkeypatch.setenv("NHIP_OOD_LDS_SLOTS", "600")
+    gair_g = NS.Air(big.to_words())
+    monkeypatch.delenv("NHIP_OOD_LDS_SLOTS")
+    info_g = gair_g.info()
+    assert info_g["lds_slots"] == 600 and info_g["global_slots"] > 1000, info_g  # the overflow path
     items = S.decode_proof(proof, params)
     spans, pos = [], 2
     for _ in items:
@@ -44,6 +51,10 @@ def test_triton_air_sized_circuit_uses_global_slots_and_matches_oracle(ctx):
     b = NS.Batch(ctx, gair, NS.Stark.default(), [NS.Claim(*claim)] * len(cases), cases)
     v, _ = b.run()
     assert [bool(x) for x in v] == want
+    bg = NS.Batch(ctx, gair_g, NS.Stark.default(), [NS.Claim(*claim)] * len(cases), cases)
+    vg, _ = bg.run()
+    assert [bool(x) for x in vg] == want
+    bg.close()
     tr = {}
     S.verify(params, big, claim, proof, tr)
     samples = [tuple(x) for tag, vals in tr["sponge_samples"] if tag != "fri_indices" for x in vals]
