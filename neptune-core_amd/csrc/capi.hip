@@ -214,10 +214,13 @@ void* nhip_internal_verify_scratch(nhip_ctx* c, void* (*make)(), void (*freefn)(
 // Pinned staging of at least `bytes` (caller holds c->mu); nullptr if it cannot be pinned.
 void* nhip_internal_staging(nhip_ctx* c, size_t bytes) {
     if (bytes <= c->staging_bytes) return c->staging;
+    const size_t have = c->staging_bytes;
     if (c->staging) (void)hipHostFree(c->staging);
     c->staging = nullptr;
     c->staging_bytes = 0;
-    const size_t want = bytes + bytes / 4;  // headroom for slightly larger batches
+    // headroom, at least doubling: hipHostFree waits for the device, so a context whose batches
+    // vary in size should stop reallocating after a few calls
+    const size_t want = std::max(bytes + bytes / 4, 2 * have);
     if (hipHostMalloc(&c->staging, want, hipHostMallocDefault) != hipSuccess) {
         c->staging = nullptr;
         return nullptr;

@@ -418,6 +418,15 @@ void air_compile(nhip_air* a, const std::vector<uint32_t>& cons, uint32_t width)
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Size of a buffer that must grow from `have` to hold `need`: exact for a one-shot batch; for
+// buffers refilled again and again (streams, the queue's slots, the verify scratch) with headroom
+// and at least doubling, so that batches of varying size stop reallocating after a few calls (a
+// hipFree / hipHostFree waits for the device, which stalls the other batches in flight).
+inline size_t grown(size_t need, size_t have, bool refilled) {
+    if (!refilled) return need;
+    return std::max(need + need / 4, have ? 2 * have : 0);
+}
+
 }  // namespace
 
 extern "C" {
@@ -643,7 +652,7 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
                 if (*dw) (void)hipFree(*dw);
                 *dw = nullptr;
                 *dwb = 0;
-                const size_t want = (reuse || scr) ? wbytes + wbytes / 4 : wbytes;
+                const size_t want = grown(wbytes, *dwb, reuse || scr);
                 const hipError_t ea = hipMalloc(dw, want);
                 if (ea != hipSuccess) {
                     if (scr) b->dwords = nullptr;
@@ -824,19 +833,20 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         if (scr) {  // grow-only device scratch of the context
             if (scr->dmem_bytes < total) {
                 (void)hipStreamSynchronize(st);
+                const size_t want = grown(total, scr->dmem_bytes, true);
                 if (scr->dmem) (void)hipFree(scr->dmem);
                 scr->dmem = nullptr;
                 scr->dmem_bytes = 0;
-                e = hipMalloc(&scr->dmem, total + total / 4);
-                if (e == hipSuccess) scr->dmem_bytes = total + total / 4;
+                e = hipMalloc(&scr->dmem, want);
+                if (e == hipSuccess) scr->dmem_bytes = want;
             }
             b->dmem = scr->dmem;
         } else if (b->dmem_bytes < total) {  // new batch, or a refill that no longer fits
             (void)hipStreamSynchronize(st);
+            const size_t want = grown(total, b->dmem_bytes, reuse != nullptr);
             if (b->dmem) (void)hipFree(b->dmem);
             b->dmem = nullptr;
             b->dmem_bytes = 0;
-            const size_t want = reuse ? total + total / 4 : total;
             e = hipMalloc(&b->dmem, want);
             if (e == hipSuccess) b->dmem_bytes = want;
         }
@@ -994,11 +1004,12 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
     if (!b->scratch) {  // pinned readback, grown when a refill needs more
         const size_t out_bytes = OUT_HDR + (size_t)b->dev.mp.levels * MP_SHARDS * 4 + b->dev.n_proofs + 16;
         if (b->h_out_bytes < out_bytes) {
+            const size_t want = std::max<size_t>(grown(out_bytes, b->h_out_bytes, true), 64u << 10);
             if (b->h_out) (void)hipHostFree(b->h_out);
             b->h_out = nullptr;
             b->h_out_bytes = 0;
-            if (hipHostMalloc((void**)&b->h_out, out_bytes, hipHostMallocDefault) != hipSuccess) return NHIP_ERR_OOM;
-            b->h_out_bytes = out_bytes;
+            if (hipHostMalloc((void**)&b->h_out, want, hipHostMallocDefault) != hipSuccess) return NHIP_ERR_OOM;
+            b->h_out_bytes = want;
         }
     }
     hipStream_t st = b->main;
