@@ -81,7 +81,7 @@ def test_queue_verdicts_and_coalescing_rate(ctx, pool_batch):
     print(f"serialized {rate_ser:.0f} proofs/s, queue (64 threads) {rate_q:.0f} proofs/s, {st}")
     nb = max(prof["batches"], 1)
     print("queue per batch (ms): " + ", ".join(f"{k[3:]} {prof[k] / nb:.3f}" for k in prof if k.startswith("ms_")) +
-          f"; sizes {prof['size_hist']}")
+          f"; sizes {prof['size_hist']}, pinned proofs {prof['pinned_proofs']}")
     # the profile counts the warm-up call's batch too
     assert prof["batches"] == st["batches"] and sum(prof["size_hist"]) == prof["batches"]
     assert prof["proofs"] == st["proofs"] and prof["ms_device"] > 0 and prof["ms_turnaround"] >= prof["ms_window"]
