@@ -176,6 +176,11 @@ int nhip_air_info(const nhip_air *air, uint32_t *num_nodes, uint32_t *num_levels
 /* The OOD evaluator's value slots (liveness-allocated): those in LDS, and those past the LDS budget
  * (~6K XFEs), which live in a per-proof global area (an AIR of triton-air's size class). */
 int nhip_air_slots(const nhip_air *air, uint32_t *lds_slots, uint32_t *global_slots);
+/* The compiled OOD program (host only, for tools and tests of the compiler): steps + 1 step offsets
+ * and 4 u32 per instruction (op, a, b, dst; stark.hpp OodIns).  NULL arrays (or too
+ * small capacities) just report the sizes; NHIP_ERR_ARG when a given array is too small. */
+int nhip_air_program(const nhip_air *air, uint32_t *step_off, size_t step_cap, uint32_t *ins, size_t ins_cap,
+                     size_t *n_steps, size_t *n_ins);
 /* Host-only structural decode (no GPU needed): 1 = decodes, 0 = malformed, < 0 = bad argument. */
 int nhip_proof_decodes(const nhip_air *air, const nhip_stark_params *params, const nhip_claim *claim,
                        const nhip_proof *proof);

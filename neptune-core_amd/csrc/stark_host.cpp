@@ -259,13 +259,11 @@ int air_upload(nhip_ctx* ctx, nhip_air* a, nhip_air::Dev* out) {
 
 // Instructions per step of the compiled AIR program (NHIP_OOD_STEP_WIDTH overrides, A/B runs):
 // two per thread of k_ood_air's 256-thread workgroups.
+// Read at every nhip_air_create (rare: once per AIR at startup).
 uint32_t ood_step_width() {
-    static const uint32_t w = [] {
-        const char* e = std::getenv("NHIP_OOD_STEP_WIDTH");
-        const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 10) : 512u;
-        return v >= 16 && v <= (1u << 16) ? v : 512u;
-    }();
-    return w;
+    const char* e = std::getenv("NHIP_OOD_STEP_WIDTH");
+    const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 10) : 512u;
+    return v >= 16 && v <= (1u << 16) ? v : 512u;
 }
 
 // Compile the circuit into the slot program of k_ood_air (OodIns, stark.hpp): a sequence of
@@ -539,6 +537,28 @@ int nhip_air_slots(const nhip_air* a, uint32_t* lds_slots, uint32_t* global_slot
     const uint32_t l = std::min<uint32_t>(a->slots, a->lds_cap);
     if (lds_slots) *lds_slots = l;
     if (global_slots) *global_slots = a->slots - l;
+    return NHIP_OK;
+}
+
+int nhip_air_program(const nhip_air* a, uint32_t* step_off, size_t step_cap, uint32_t* ins, size_t ins_cap,
+                     size_t* n_steps, size_t* n_ins) {
+    if (!a) return NHIP_ERR_ARG;
+    const size_t ns = a->prog_off.size() - 1, ni = a->prog.size();
+    if (n_steps) *n_steps = ns;
+    if (n_ins) *n_ins = ni;
+    if (step_off) {
+        if (step_cap < ns + 1) return NHIP_ERR_ARG;
+        std::memcpy(step_off, a->prog_off.data(), (ns + 1) * 4);
+    }
+    if (ins) {
+        if (ins_cap < 4 * ni) return NHIP_ERR_ARG;
+        for (size_t i = 0; i < ni; ++i) {
+            ins[4 * i] = a->prog[i].op;
+            ins[4 * i + 1] = a->prog[i].a;
+            ins[4 * i + 2] = a->prog[i].b;
+            ins[4 * i + 3] = a->prog[i].dst;
+        }
+    }
     return NHIP_OK;
 }
 

@@ -119,6 +119,8 @@ SIGNATURES = {
     "nhip_air_destroy": ([_vp], None),
     "nhip_air_info": ([_vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                        ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+    "nhip_air_program": ([_vp, ctypes.c_void_p, _sz, ctypes.c_void_p, _sz, ctypes.POINTER(_sz), ctypes.POINTER(_sz)],
+                         ctypes.c_int),
     "nhip_air_slots": ([_vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
     "nhip_proof_from_be_bytes": ([ctypes.c_void_p, _sz, ctypes.c_void_p, _sz, ctypes.POINTER(_sz)], ctypes.c_int),
     "nhip_proof_to_be_bytes": ([ctypes.c_void_p, _sz, ctypes.c_void_p], ctypes.c_int),

@@ -117,6 +117,18 @@ class Air:
         return {"nodes": a.value, "levels": b.value, "constraints": c.value, "lds_slots": lds.value,
                 "global_slots": glob.value}
 
+    def program(self):
+        """The compiled OOD program (nhip_air_program): step offsets and an (n, 4) array of
+        (op, a, b, dst) instructions."""
+        ns, ni = ctypes.c_size_t(), ctypes.c_size_t()
+        check(self.lib.nhip_air_program(self.handle, None, 0, None, 0, ctypes.byref(ns), ctypes.byref(ni)),
+              "nhip_air_program")
+        off = np.zeros(ns.value + 1, dtype=np.uint32)
+        ins = np.zeros((max(ni.value, 1), 4), dtype=np.uint32)
+        check(self.lib.nhip_air_program(self.handle, off.ctypes.data, off.size, ins.ctypes.data, ins.size,
+                                        ctypes.byref(ns), ctypes.byref(ni)), "nhip_air_program")
+        return off, ins[:ni.value]
+
     def __del__(self):
         try:
             if self.handle:

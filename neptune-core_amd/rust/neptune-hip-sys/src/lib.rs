@@ -183,6 +183,8 @@ extern "C" {
     pub fn nhip_air_destroy(air: *mut nhip_air);
     pub fn nhip_air_info(air: *const nhip_air, num_nodes: *mut u32, num_levels: *mut u32,
                          num_constraints: *mut u32) -> c_int;
+    pub fn nhip_air_program(air: *const nhip_air, step_off: *mut u32, step_cap: usize, ins: *mut u32, ins_cap: usize,
+                            n_steps: *mut usize, n_ins: *mut usize) -> c_int;
     pub fn nhip_air_slots(air: *const nhip_air, lds_slots: *mut u32, global_slots: *mut u32) -> c_int;
     pub fn nhip_proof_decodes(air: *const nhip_air, params: *const nhip_stark_params,
                               claim: *const nhip_claim, proof: *const nhip_proof) -> c_int;
