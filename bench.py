@@ -1039,28 +1039,33 @@ def main():
     # 0 drives all of them while the other ranks wait at the barrier with their batches freed
     if args.group_batches > 0 and args.config == 4 and not under_profiler():
         if dist is not None:
-            dist.barrier()
-        if rank == 0:
+            dist.barrier()  # every rank's batches are closed
+
+        def leg():
+            job_claims, job_proofs, job_expect = claims, proofs, expect
+            if world > 1:
+                job_claims, job_proofs, job_expect, _, _, _ = make_config4(pool4, total, 0.01, 1, 0)
+            dcl, dpr = device_form(job_claims, job_proofs, mont)
+            # every GPU the job's ranks use (a gloo rehearsal puts several ranks on one GPU)
+            devs = sorted({r if dist is None or os.environ.get("NHIP_DIST_BACKEND", "nccl") == "nccl"
+                           else r % max(1, __import__("torch").cuda.device_count()) for r in range(world)})
             try:
-                job_claims, job_proofs = claims, proofs
-                job_expect = expect
-                if world > 1:
-                    job_claims, job_proofs, job_expect, _, _, _ = make_config4(pool4, total, 0.01, 1, 0)
-                dcl, dpr = device_form(job_claims, job_proofs, mont)
-                t = time.time()
-                # every GPU the job's ranks use (a gloo rehearsal puts several ranks on one GPU)
-                devs = sorted({r if dist is None or os.environ.get("NHIP_DIST_BACKEND", "nccl") == "nccl"
-                               else r % max(1, __import__("torch").cuda.device_count()) for r in range(world)})
-                res["group_stream"] = group_stream(devs, air_words, stark, dcl, dpr, job_expect, args.group_batches)
-                if "pcie_inclusive" in res:
-                    res["group_stream"]["vs_pcie_inclusive"] = res["group_stream"]["value"] / res["pcie_inclusive"]["value"]
-                correct = correct and res["group_stream"]["verdicts_correct"]
-                log(f"[group] {res['group_stream']['value']:.0f} proofs/s over {world} GPU(s) ({time.time() - t:.1f}s)")
+                return group_stream(devs, air_words, stark, dcl, dpr, job_expect, args.group_batches)
             except Exception as e:  # noqa: BLE001 -- a leg, never the headline
-                res["group_stream"] = {"error": repr(e)}
-            if dist is not None:
-                import torch
-                torch.cuda.set_device(dev_index)  # the members' threads ran on the other devices
+                return {"error": repr(e), "verdicts_correct": False}
+            finally:
+                if dist is not None:
+                    import torch
+                    torch.cuda.set_device(dev_index)  # the members' threads ran on the other devices
+
+        t = time.time()
+        g = shard.on_rank0(leg, dist, "nhip_group_stream_done")
+        if rank == 0:
+            res["group_stream"] = g
+            if "pcie_inclusive" in res and "value" in g:
+                g["vs_pcie_inclusive"] = g["value"] / res["pcie_inclusive"]["value"]
+            correct = correct and g["verdicts_correct"]
+            log(f"[group] {g.get('value', 0):.0f} proofs/s over {world} GPU(s) ({time.time() - t:.1f}s)")
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()

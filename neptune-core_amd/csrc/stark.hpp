@@ -113,7 +113,7 @@ struct AirNode {
 // value's last use), constants in a global table, OOD-row inputs loaded once into slots, and every
 // constraint folded into the weighted quotient sum one level after it is produced, so constraint
 // values do not stay live to the end.
-enum OodOp : uint32_t { OOD_ADD = AIR_ADD, OOD_SUB = AIR_SUB, OOD_MUL = AIR_MUL, OOD_LOAD = 5, OOD_ACC = 6, OOD_NOP = 7 };
+enum OodOp : uint32_t { OOD_ADD = AIR_ADD, OOD_SUB = AIR_SUB, OOD_MUL = AIR_MUL, OOD_LOAD = 5, OOD_ACC = 6 };
 // operand reference: [31:30] 0 = LDS slot, 1 = constant table index, 2 = input ([29:27] kind, [26:0] index)
 static constexpr uint32_t OOD_REF_SLOT = 0u << 30, OOD_REF_CONST = 1u << 30, OOD_REF_INPUT = 2u << 30;
 struct OodIns {

@@ -98,16 +98,24 @@ PinnedRanges& pinned() {
 }  // namespace
 
 // ====================================================================== AIR object
+// One compiled OOD program (air_compile): instructions, step offsets, constant table, slot count.
+struct OodProgram {
+    std::vector<OodIns> prog;
+    std::vector<uint32_t> prog_off;
+    std::vector<Xfe> consts;
+    uint32_t slots = 0;
+    uint32_t width = 0;
+};
+
 struct nhip_air {
     StarkDims dims_air{};  // num_main, num_aux, num_sampled, num_constraints filled
     std::vector<AirNode> nodes;
     std::vector<uint32_t> level_off;  // node-level histogram (nhip_air_info)
     uint4 cons_off{};
-    // compiled program (see OodIns in stark.hpp)
-    std::vector<OodIns> prog;
-    std::vector<uint32_t> prog_off;
-    std::vector<Xfe> consts;
-    uint32_t slots = 0;
+    // compiled programs (see OodIns in stark.hpp, air_compile): [0] narrow steps (fewer live values:
+    // more proofs per CU, for batches that fill the GPU), [1] wide steps (fewer barriers: lower
+    // latency per proof, for smaller batches); a batch takes one by its size (ood_program_for)
+    OodProgram progs[2];
     // slots held in LDS (the rest in the per-proof global area): AIR_LDS_SLOTS_MAX, or less when
     // NHIP_OOD_LDS_SLOTS asks for it at creation (tests of the global-slot path)
     uint32_t lds_cap = AIR_LDS_SLOTS_MAX;
@@ -116,9 +124,9 @@ struct nhip_air {
     // created on first use, freed with the AIR
     struct Dev {
         int device;
-        OodIns* d_prog;
-        uint32_t* d_prog_off;
-        Xfe* d_consts;
+        OodIns* d_prog[2];
+        uint32_t* d_prog_off[2];
+        Xfe* d_consts[2];
     };
     std::mutex mu;
     std::vector<Dev> devs;
@@ -229,27 +237,35 @@ int air_upload(nhip_ctx* ctx, nhip_air* a, nhip_air::Dev* out) {
             *out = d;
             return NHIP_OK;
         }
-    nhip_air::Dev d{device, nullptr, nullptr, nullptr};
-    hipError_t e = hipMalloc(&d.d_prog, a->prog.size() * sizeof(OodIns) + 16);
-    if (e == hipSuccess) e = hipMalloc(&d.d_prog_off, a->prog_off.size() * 4 + 4);
-    if (e == hipSuccess) e = hipMalloc(&d.d_consts, a->consts.size() * sizeof(Xfe) + 24);
-    if (e == hipSuccess && !a->prog.empty())
-        e = hipMemcpy(d.d_prog, a->prog.data(), a->prog.size() * sizeof(OodIns), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(d.d_prog_off, a->prog_off.data(), a->prog_off.size() * 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess && !a->consts.empty())
-        e = hipMemcpy(d.d_consts, a->consts.data(), a->consts.size() * sizeof(Xfe), hipMemcpyHostToDevice);
+    nhip_air::Dev d{device, {nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}};
+    auto free_dev = [&]() {
+        for (int k = 0; k < 2; ++k) {
+            if (d.d_prog[k]) (void)hipFree(d.d_prog[k]);
+            if (d.d_prog_off[k]) (void)hipFree(d.d_prog_off[k]);
+            if (d.d_consts[k]) (void)hipFree(d.d_consts[k]);
+        }
+    };
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+        const OodProgram& pg = a->progs[k];
+        e = hipMalloc(&d.d_prog[k], pg.prog.size() * sizeof(OodIns) + 16);
+        if (e == hipSuccess) e = hipMalloc(&d.d_prog_off[k], pg.prog_off.size() * 4 + 4);
+        if (e == hipSuccess) e = hipMalloc(&d.d_consts[k], pg.consts.size() * sizeof(Xfe) + 24);
+        if (e == hipSuccess && !pg.prog.empty())
+            e = hipMemcpy(d.d_prog[k], pg.prog.data(), pg.prog.size() * sizeof(OodIns), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(d.d_prog_off[k], pg.prog_off.data(), pg.prog_off.size() * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess && !pg.consts.empty())
+            e = hipMemcpy(d.d_consts[k], pg.consts.data(), pg.consts.size() * sizeof(Xfe), hipMemcpyHostToDevice);
+    }
     if (e != hipSuccess) {
-        if (d.d_prog) (void)hipFree(d.d_prog);
-        if (d.d_prog_off) (void)hipFree(d.d_prog_off);
-        if (d.d_consts) (void)hipFree(d.d_consts);
+        free_dev();
         return hipfail(e);
     }
     try {
         a->devs.reserve(a->devs.size() + 1);
     } catch (const std::bad_alloc&) {
-        (void)hipFree(d.d_prog);
-        (void)hipFree(d.d_prog_off);
-        (void)hipFree(d.d_consts);
+        free_dev();
         return NHIP_ERR_OOM;
     }
     a->devs.push_back(d);
@@ -266,6 +282,16 @@ uint32_t ood_step_width() {
     return v >= 16 && v <= (1u << 16) ? v : 512u;
 }
 
+// The program a batch of n proofs runs: the wide-step one up to NHIP_OOD_WIDE_PROG_MAX proofs (default
+// 2,048), where one proof's evaluation latency matters more than proofs per CU.
+int ood_program_for(uint32_t n) {
+    static const uint32_t lim = [] {
+        const char* e = std::getenv("NHIP_OOD_WIDE_PROG_MAX");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 2048u;
+    }();
+    return n <= lim ? 1 : 0;
+}
+
 // Compile the circuit into the slot program of k_ood_air (OodIns, stark.hpp): a sequence of
 // steps, each a set of independent instructions the workgroup runs between two barriers, every
 // value in a slot from the step that computes it to the step of its last use (a slot is reused
@@ -279,7 +305,9 @@ uint32_t ood_step_width() {
 // empty.  Constraint accumulations (OOD_ACC) run in the step after their value.  Within a step the
 // instructions are grouped by kind (loads, products, sums, accumulations): a wave then runs one kind
 // of XFE operation instead of the divergent union of several.
-void air_compile(nhip_air* a, const std::vector<uint32_t>& cons, uint32_t width) {
+void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t width, OodProgram& pg) {
+    pg = OodProgram{};
+    pg.width = width;
     const size_t NN = a->nodes.size();
     const auto is_op = [&](size_t i) {
         const uint32_t op = a->nodes[i].op;
@@ -309,8 +337,8 @@ void air_compile(nhip_air* a, const std::vector<uint32_t>& cons, uint32_t width)
     for (size_t i = 0; i < NN; ++i) {
         if (corder[i] == UINT32_MAX) continue;  // dead node
         if (a->nodes[i].op == AIR_CONST) {
-            ref[i] = OOD_REF_CONST | (uint32_t)a->consts.size();
-            a->consts.push_back(Xfe{a->nodes[i].k0, a->nodes[i].k1, a->nodes[i].k2});
+            ref[i] = OOD_REF_CONST | (uint32_t)pg.consts.size();
+            pg.consts.push_back(Xfe{a->nodes[i].k0, a->nodes[i].k1, a->nodes[i].k2});
         } else {
             slotted[i] = 1;
         }
@@ -358,7 +386,7 @@ void air_compile(nhip_air* a, const std::vector<uint32_t>& cons, uint32_t width)
     auto use = [&](uint32_t o) {  // a read of o in this step (its slot index is ref[o])
         if (slotted[o] && --remaining[o] == 0) to_free.push_back(ref[o]);
     };
-    a->prog_off.assign(1, 0);
+    pg.prog_off.assign(1, 0);
     while (!ready.empty() || !acc_next.empty()) {
         cur.swap(acc_next);  // the accumulations of the values of the step before
         acc_next.clear();
@@ -407,11 +435,11 @@ void air_compile(nhip_air* a, const std::vector<uint32_t>& cons, uint32_t width)
         };
         std::stable_sort(cur.begin(), cur.end(),
                          [&](const OodIns& x, const OodIns& y) { return kind_rank(x.op) < kind_rank(y.op); });
-        a->prog.insert(a->prog.end(), cur.begin(), cur.end());
-        a->prog_off.push_back((uint32_t)a->prog.size());
+        pg.prog.insert(pg.prog.end(), cur.begin(), cur.end());
+        pg.prog_off.push_back((uint32_t)pg.prog.size());
         cur.clear();
     }
-    a->slots = next_slot;
+    pg.slots = next_slot;
 }
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -505,7 +533,8 @@ int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
         cons[i] = (uint32_t)cw[i];
     }
     a->cons_off = make_uint4((uint32_t)nc[0], (uint32_t)(nc[0] + nc[1]), (uint32_t)(nc[0] + nc[1] + nc[2]), (uint32_t)C);
-    air_compile(a, cons, ood_step_width());
+    air_compile(a, cons, ood_step_width(), a->progs[0]);
+    air_compile(a, cons, 2 * ood_step_width(), a->progs[1]);
     if (const char* e = std::getenv("NHIP_OOD_LDS_SLOTS"))
         a->lds_cap = std::min<uint32_t>(AIR_LDS_SLOTS_MAX, (uint32_t)std::strtoul(e, nullptr, 10));
     *out = a;
@@ -516,9 +545,11 @@ void nhip_air_destroy(nhip_air* a) {
     if (!a) return;
     for (const auto& d : a->devs) {
         (void)hipSetDevice(d.device);
-        (void)hipFree(d.d_prog);
-        (void)hipFree(d.d_prog_off);
-        (void)hipFree(d.d_consts);
+        for (int k = 0; k < 2; ++k) {
+            (void)hipFree(d.d_prog[k]);
+            (void)hipFree(d.d_prog_off[k]);
+            (void)hipFree(d.d_consts[k]);
+        }
     }
     delete a;
 }
@@ -534,29 +565,30 @@ int nhip_air_info(const nhip_air* a, uint32_t* num_nodes, uint32_t* num_levels, 
 // Slots of the compiled AIR program: held in LDS, and past the LDS budget (global memory).
 int nhip_air_slots(const nhip_air* a, uint32_t* lds_slots, uint32_t* global_slots) {
     if (!a) return NHIP_ERR_ARG;
-    const uint32_t l = std::min<uint32_t>(a->slots, a->lds_cap);
+    const uint32_t l = std::min<uint32_t>(a->progs[0].slots, a->lds_cap);
     if (lds_slots) *lds_slots = l;
-    if (global_slots) *global_slots = a->slots - l;
+    if (global_slots) *global_slots = a->progs[0].slots - l;
     return NHIP_OK;
 }
 
 int nhip_air_program(const nhip_air* a, uint32_t* step_off, size_t step_cap, uint32_t* ins, size_t ins_cap,
                      size_t* n_steps, size_t* n_ins) {
     if (!a) return NHIP_ERR_ARG;
-    const size_t ns = a->prog_off.size() - 1, ni = a->prog.size();
+    const OodProgram& pg = a->progs[0];
+    const size_t ns = pg.prog_off.size() - 1, ni = pg.prog.size();
     if (n_steps) *n_steps = ns;
     if (n_ins) *n_ins = ni;
     if (step_off) {
         if (step_cap < ns + 1) return NHIP_ERR_ARG;
-        std::memcpy(step_off, a->prog_off.data(), (ns + 1) * 4);
+        std::memcpy(step_off, pg.prog_off.data(), (ns + 1) * 4);
     }
     if (ins) {
         if (ins_cap < 4 * ni) return NHIP_ERR_ARG;
         for (size_t i = 0; i < ni; ++i) {
-            ins[4 * i] = a->prog[i].op;
-            ins[4 * i + 1] = a->prog[i].a;
-            ins[4 * i + 2] = a->prog[i].b;
-            ins[4 * i + 3] = a->prog[i].dst;
+            ins[4 * i] = pg.prog[i].op;
+            ins[4 * i + 1] = pg.prog[i].a;
+            ins[4 * i + 2] = pg.prog[i].b;
+            ins[4 * i + 3] = pg.prog[i].dst;
         }
     }
     return NHIP_OK;
@@ -796,6 +828,8 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
             }
         }
         const uint32_t k = D.d.num_checks;
+        const int pk = ood_program_for((uint32_t)n);
+        const OodProgram& pg = air->progs[pk];
         // multiproof op capacity per (level, shard): a tree of height h has at most min(k, 2^(h-1-l))
         // parents at level l; shard = proof index % MP_SHARDS
         const uint32_t tpp = 4 + H.max_R;
@@ -842,7 +876,7 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
                              N1 * k * 8,
                              N1 * H.max_last_cw * 40,
                              // OOD slots past the LDS budget (an AIR larger than ~6K live XFEs)
-                             N1 * (size_t)(air->slots - std::min<uint32_t>(air->slots, air->lds_cap)) * 24 + 24,
+                             N1 * (size_t)(pg.slots - std::min<uint32_t>(pg.slots, air->lds_cap)) * 24 + 24,
                              // per (proof, tree group, level) op ranges of the plan (k_mp_climb)
                              N1 * (1 + H.max_R) * (size_t)(levels + 1) * 8,
                              N1 * (1 + H.max_R) * (size_t)(levels + 1) * 4,
@@ -924,13 +958,13 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         dv.lcw = (uint64_t*)ptr[20];
         dv.max_lcw = H.max_last_cw;
         dv.mp_cap_host = b->mp_cap.data();
-        dv.air_prog = adev.d_prog;
-        dv.air_prog_off = adev.d_prog_off;
-        dv.air_n_levels = (uint32_t)air->prog_off.size() - 1;
-        dv.air_consts = adev.d_consts;
+        dv.air_prog = adev.d_prog[pk];
+        dv.air_prog_off = adev.d_prog_off[pk];
+        dv.air_n_levels = (uint32_t)pg.prog_off.size() - 1;
+        dv.air_consts = adev.d_consts[pk];
         dv.air_cons_off = air->cons_off;
-        dv.air_lds_slots = std::min<uint32_t>(air->slots, air->lds_cap);
-        dv.air_gslot_n = air->slots - dv.air_lds_slots;
+        dv.air_lds_slots = std::min<uint32_t>(pg.slots, air->lds_cap);
+        dv.air_gslot_n = pg.slots - dv.air_lds_slots;
         dv.air_gslots = (Xfe*)ptr[21];
         dv.mp.lvl_g0 = (uint64_t*)ptr[22];
         dv.mp.lvl_cnt = (uint32_t*)ptr[23];

@@ -1056,11 +1056,7 @@ __device__ Xfe eval_terminal_wave(uint32_t n, Xfe c, Sym sym) {
 #ifndef NHIP_OOD_WAVES
 #define NHIP_OOD_WAVES 1
 #endif
-// instructions per thread and step batched by k_ood_air (loads of all in flight together)
-#ifndef NHIP_OOD_K
-#define NHIP_OOD_K 2
-#endif
-static constexpr uint32_t OOD_K = NHIP_OOD_K;
+
 template <uint32_t BLOCK, bool MW>
 __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_ood_air(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                                  uint32_t n_proofs, StarkDims dims, const OodIns* __restrict__ prog,
@@ -1148,55 +1144,27 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
                 return i < dims.num_sampled ? ld_xfe_raw(xs, xb + 3ull * (sl.chal + i)) : chal_derived[i - dims.num_sampled];
         }
     };
-    // The program step by step (air_compile: a step's instructions are independent).  Thread tid takes
-    // instructions tid, tid + BLOCK, ... of a step; the first OOD_K of them are batched: their
-    // instruction words were loaded during the previous step (before its barrier), every operand of
-    // all of them is requested before any is used, then they are computed and stored.  Instructions
-    // past OOD_K x BLOCK in a step (a wider program) take the plain loop.
+    // The program step by step (air_compile: a step's instructions are independent; a barrier
+    // between steps).  Batching a thread's instructions of a step (all operands requested first)
+    // and loading the next step's instruction words during the current one measured slower: config
+    // 4 -1.3% at 4,096 proofs, -1% at 512 (profiles/r04e), so each instruction runs on its own.
     Xfe acc = x_zero();
-    OodIns cur[OOD_K], nxt[OOD_K];
-    auto load_step = [&](uint32_t lvl, OodIns (&o)[OOD_K]) {
-        const uint32_t a = prog_off[lvl], b = prog_off[lvl + 1];
-#pragma unroll
-        for (uint32_t k = 0; k < OOD_K; ++k) {
-            const uint32_t q = a + tid + k * BLOCK;
-            o[k] = q < b ? prog[q] : OodIns{OOD_NOP, 0, 0, 0};
-        }
-    };
-    auto exec = [&](const OodIns& ins, const Xfe& x, const Xfe& y) {
-        if (ins.op == OOD_ACC) {
-            const uint32_t c = ins.b;
-            uint32_t t = 0;
-            while (t < 3 && c >= offs[t + 1]) ++t;
-            acc = x_add(acc, x_mul(y, x_mul(x, zinv[t])));  // y: the constraint's weight
-        } else if (ins.op == OOD_LOAD) {
-            slot(ins.dst) = x;
-        } else if (ins.op != OOD_NOP) {
-            slot(ins.dst) = ins.op == OOD_ADD ? x_add(x, y) : (ins.op == OOD_SUB ? x_sub(x, y) : x_mul(x, y));
-        }
-    };
-    auto second = [&](const OodIns& ins) -> Xfe {  // the operand after the first
-        if (ins.op == OOD_ACC) return ld_xfe_raw(xs, xb + 3ull * (sl.quot_w + ins.b));
-        if (ins.op == OOD_ADD || ins.op == OOD_SUB || ins.op == OOD_MUL) return fetch(ins.b);
-        return x_zero();
-    };
-    if (n_levels) load_step(0, cur);
     for (uint32_t lvl = 0; lvl < n_levels; ++lvl) {
-        Xfe xa[OOD_K], xb2[OOD_K];
-#pragma unroll
-        for (uint32_t k = 0; k < OOD_K; ++k) {
-            xa[k] = cur[k].op != OOD_NOP ? fetch(cur[k].a) : x_zero();
-            xb2[k] = second(cur[k]);
-        }
-        if (lvl + 1 < n_levels) load_step(lvl + 1, nxt);
-#pragma unroll
-        for (uint32_t k = 0; k < OOD_K; ++k) exec(cur[k], xa[k], xb2[k]);
-        for (uint32_t q = prog_off[lvl] + tid + OOD_K * BLOCK; q < prog_off[lvl + 1]; q += BLOCK) {
+        for (uint32_t q = prog_off[lvl] + tid; q < prog_off[lvl + 1]; q += blockDim.x) {
             const OodIns ins = prog[q];
-            exec(ins, ins.op == OOD_NOP ? x_zero() : fetch(ins.a), second(ins));
+            if (ins.op == OOD_ACC) {
+                const uint32_t c = ins.b;
+                uint32_t t = 0;
+                while (t < 3 && c >= offs[t + 1]) ++t;
+                const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.quot_w + c));
+                acc = x_add(acc, x_mul(w, x_mul(fetch(ins.a), zinv[t])));
+            } else if (ins.op == OOD_LOAD) {
+                slot(ins.dst) = fetch(ins.a);
+            } else {
+                const Xfe x = fetch(ins.a), y = fetch(ins.b);
+                slot(ins.dst) = ins.op == OOD_ADD ? x_add(x, y) : (ins.op == OOD_SUB ? x_sub(x, y) : x_mul(x, y));
+            }
         }
-#pragma unroll
-        for (uint32_t k = 0; k < OOD_K; ++k) cur[k] = nxt[k];
         __syncthreads();
     }
     const Xfe ood_q = block_sum_xfe_waves(acc, red);

@@ -40,6 +40,25 @@ def contiguous_shard(n: int, world: int, rank: int) -> range:
     return range(min(n, rank * per), min(n, (rank + 1) * per))
 
 
+def on_rank0(fn, dist, key: str = "nhip_rank0_leg", timeout_s: float = 900.0):
+    """Run ``fn()`` on rank 0 alone (e.g. one process driving every GPU of the node through
+    nhip_group_stream) while the other ranks wait on the HOST, at the rendezvous store, not in a
+    collective whose kernel would spin on the GPUs rank 0 drives.  Returns fn's result on rank 0 and
+    None elsewhere; rank 0 releases the others even if fn raises (the exception then propagates on
+    rank 0).  Without ``dist`` it is just ``fn()``."""
+    if dist is None:
+        return fn()
+    from datetime import timedelta
+    store = dist.distributed_c10d._get_default_store()
+    if dist.get_rank() != 0:
+        store.wait([key], timedelta(seconds=timeout_s))
+        return None
+    try:
+        return fn()
+    finally:
+        store.set(key, "1")
+
+
 def _device_for(dist):
     import torch
     backend = dist.get_backend()

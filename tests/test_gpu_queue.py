@@ -1,7 +1,9 @@
 """The coalescing queue (nhip_queue_*): concurrent single-proof callers, as the reference's
 `verify()` is called from many tokio tasks at once (verifier.rs:60-63, peer_loop.rs:1342).
-64 threads each verifying one proof at a time get the expected verdict every time, and together
-reach >= 10x the rate of the same calls serialized through nhip_verify_batch one proof each."""
+64 threads each verifying one proof at a time get the expected verdict every time, their calls are
+coalesced (>= 8 proofs per batch on average, every proof through the pinned arena), the worker's
+host time per batch stays within twice the device time, and together they reach >= 8x the rate of
+the same calls serialized through nhip_verify_batch one proof each (15-17x measured)."""
 import threading
 import time
 
@@ -85,9 +87,16 @@ def test_queue_verdicts_and_coalescing_rate(ctx, pool_batch):
     # the profile counts the warm-up call's batch too
     assert prof["batches"] == st["batches"] and sum(prof["size_hist"]) == prof["batches"]
     assert prof["proofs"] == st["proofs"] and prof["ms_device"] > 0 and prof["ms_turnaround"] >= prof["ms_window"]
-    # 13-16x on most boxes (7.6-9.7k vs 0.5-0.6k proofs/s); one box gave 9.3x (5.5k): the coalesced
-    # rate leans on the host's copy threads, so the bound is the coalescing itself, not one box's rate
-    assert rate_q >= 6 * rate_ser, (rate_q, rate_ser)
+    # every proof came through the pinned arena (its caller's thread copied it; the worker only DMAs)
+    assert prof["pinned_proofs"] == prof["proofs"], prof
+    # where a closed loop of 64 callers spends a batch: the worker's host part (stage +
+    # upload wait + launch) must stay within twice the device time; round 3's 9.3x box was the
+    # refilled buffers' growing hipFree / hipHostFree, each waiting for the device (r04d: host 2.2 ms
+    # vs device 1.6 ms per batch, 8.65k proofs/s; with geometric growth, r04e: 1.7 ms, 10.1k, 17x)
+    host = (prof["ms_stage"] + prof["ms_upload"] + prof["ms_launch"]) / nb
+    assert host <= 2 * prof["ms_device"] / nb, prof
+    assert prof["proofs"] / nb >= 8, prof  # coalesced: batches of >= 8 proofs on average
+    assert rate_q >= 8 * rate_ser, (rate_q, rate_ser)
 
 
 def test_queue_bad_arguments_stay_with_the_caller(ctx, pool_batch):

@@ -185,3 +185,52 @@ def test_two_rank_verdict_exchange_one_collective():
             assert got[k] == (all(full), full)
         assert got[4] == (True, steps[0])  # the extra post: local_ok as given, step 0's verdicts
         assert pair == (all(steps[1]), steps[1])
+
+
+def _rank0_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import time
+    import torch.distributed as dist
+    from neptune_hip import shard
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t0 = time.time()
+
+    def leg():
+        time.sleep(0.5)
+        return {"ran_on": dist.get_rank()}
+
+    got = shard.on_rank0(leg, dist, "leg_a")
+    waited = time.time() - t0
+
+    def bad():
+        raise RuntimeError("leg failed")
+
+    raised = None
+    try:
+        shard.on_rank0(bad, dist, "leg_b")
+    except RuntimeError as e:
+        raised = str(e)
+    dist.barrier()
+    q.put((rank, got, waited, raised))
+    dist.destroy_process_group()
+
+
+def test_rank0_leg_others_wait_on_the_store():
+    """shard.on_rank0 (bench.py's group_stream leg at N > 1): rank 0 runs the leg, the other ranks
+    wait on the host until it is done (no collective in flight meanwhile), get None, and are
+    released even when the leg raises on rank 0."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank0_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    (r0, g0, w0, e0), (r1, g1, w1, e1) = res
+    assert g0 == {"ran_on": 0} and g1 is None
+    assert w1 >= 0.45  # rank 1 waited for rank 0's leg
+    assert e0 == "leg failed" and e1 is None
