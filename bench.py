@@ -993,7 +993,9 @@ def main():
                                    f"region; per-launch HIP events (hipExtLaunchKernel start/stop)")
         assert res["roofline"]["launches_x_avg_ms"] <= step_ms, (res["roofline"], step_ms)
         res["roofline"]["inflight"] = {k: inflight[k] for k in ("achieved", "frac", "kernel_avg_ms",
-                                                                 "launches_x_avg_ms", "step_ms", "measured")}
+                                                                 "kernel_avg_ms_events", "launches_per_step",
+                                                                 "perms_per_launch", "launches_x_avg_ms", "step_ms",
+                                                                 "measured")}
     else:
         res["roofline"] = inflight
     valu_step, valu_tag = pmc_valu_per_step(args.config, len(proofs))

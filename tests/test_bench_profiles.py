@@ -102,6 +102,12 @@ def test_summary_reproduces_the_bench_roofline():
     frac_trace = float(line.split("T = ")[1].split(";")[0])
     frac_bench = float(line.rsplit("frac ", 1)[1])
     assert abs(frac_trace / frac_bench - 1) < 0.05, (frac_trace, frac_bench)
+    # the reported (isolated-launch) roofline: the trace of the one-at-a-time steps within 2%
+    iso = [x for x in text.splitlines() if x.startswith("isolated roofline frac from the trace:")]
+    if iso:  # (profiles from round 4 on)
+        f_t = float(iso[0].split(": ")[1].split(";")[0])
+        f_b = float(iso[0].rsplit("frac ", 1)[1])
+        assert abs(f_t / f_b - 1) < 0.02, (f_t, f_b)
 
 
 def test_inflight_defaults_and_queue_budget():

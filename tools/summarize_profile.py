@@ -63,17 +63,21 @@ if trace and b and b.get("roofline"):
     # --stream-batches 0 --paths-log2 0 for the profiled command
     rows = sorted(csv.DictReader(open(trace[0])), key=lambda r: int(r["Start_Timestamp"]))
     mh = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if kname(r["Kernel_Name"]).endswith(MERKLE)]
-    rf = b["roofline"]
+    # round 4: with isolated steps, `roofline` is theirs and `roofline.inflight` the timed steps'
+    # (round 3 lines: `roofline` timed, `roofline_isolated`)
+    if "inflight" in b["roofline"]:
+        ri, rf = b["roofline"], dict(b["roofline"], **b["roofline"]["inflight"])
+    else:
+        ri, rf = b.get("roofline_isolated"), b["roofline"]
     per_step = int(round(rf["launches_per_step"]))
     timed = b["steps"] * per_step
-    iso = b.get("iso_steps", 5) * per_step if b.get("roofline_isolated") else 0
+    iso = b.get("iso_steps", 5) * per_step if ri else 0
     if iso and len(mh) >= iso:
         i_ = mh[-iso:]
-        ri = b["roofline_isolated"]
         avg_i = sum(i_) / len(i_) / 1e6
         print(f"\nMerkle hash launches of the isolated steps: {len(i_)} calls, trace average {avg_i:.4f} ms; bench "
-              f"{ri['kernel_avg_ms']:.4f} ms ({(ri['kernel_avg_ms'] / avg_i - 1) * 100:+.1f}%); frac from the trace "
-              f"{frac_of(ri, avg_i):.4f}, bench {ri['frac']:.4f}")
+              f"{ri['kernel_avg_ms']:.4f} ms ({(ri['kernel_avg_ms'] / avg_i - 1) * 100:+.1f}%)")
+        print(f"isolated roofline frac from the trace: {frac_of(ri, avg_i):.4f}; bench frac {ri['frac']:.4f}")
     if len(mh) >= timed + iso:
         t = mh[len(mh) - iso - timed:len(mh) - iso]
         avg_ms = sum(t) / len(t) / 1e6
