@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "../../include/neptune_hip.h"
+#include "pinned_ring.hpp"
 
 // stark_host.cpp: true once every phase of a launched batch has completed (a stream query, no wait)
 extern "C" bool nhip_internal_batch_done(nhip_batch* b);
@@ -48,38 +49,6 @@ struct Req {
     int rc = NHIP_OK;
     bool done = false;
     uint64_t arena_at = ~0ull;  // its proofs' range in the pinned arena (~0: its own memory)
-};
-
-// Pinned receive arena of a queue: a ring of monotonically growing offsets.  A caller takes a
-// contiguous range for its proofs (under the queue lock), copies them in on its own thread (no
-// lock held), and the worker releases the range once the batch holding them has been uploaded
-// (nhip_batch_refill waits for its uploads).  Ranges are taken in arrival order but may be
-// released out of order (two slots); the ring's tail advances over released ranges only.
-struct PinnedRing {
-    uint8_t* base = nullptr;
-    uint64_t cap = 0, head = 0, tail = 0;
-    std::map<uint64_t, std::pair<uint64_t, bool>> live;  // start -> (bytes, released)
-
-    uint64_t take(uint64_t n) {
-        if (!base || n == 0 || n > cap) return ~0ull;
-        uint64_t at = head;
-        if (at % cap + n > cap) at += cap - at % cap;  // would wrap: start at the ring's beginning
-        if (at + n - tail > cap) return ~0ull;           // full
-        live.emplace(at, std::make_pair(n, false));
-        head = at + n;
-        return at;
-    }
-    void release(uint64_t at) {
-        auto it = live.find(at);
-        if (it == live.end()) return;
-        it->second.second = true;
-        while (!live.empty() && live.begin()->second.second) {
-            tail = live.begin()->first + live.begin()->second.first;
-            live.erase(live.begin());
-        }
-        if (live.empty()) tail = head;
-    }
-    uint8_t* ptr(uint64_t at) const { return base + at % cap; }
 };
 
 // arena size: about two full batches of config-4-sized proofs from concurrent callers
@@ -107,7 +76,7 @@ struct nhip_queue {
     std::vector<nhip_proof> proofs;
     std::vector<uint8_t> verdicts;
     std::atomic<uint64_t> n_batches{0}, n_proofs{0};
-    PinnedRing ring;  // guarded by mu
+    nhip::PinnedRing ring;  // guarded by mu
     // nhip_queue_profile: written by the worker under prof_mu, read by nhip_queue_profile_read
     mutable std::mutex prof_mu;
     nhip_queue_profile prof{};

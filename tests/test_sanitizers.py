@@ -56,3 +56,13 @@ def test_parsers_clean_under_asan_ubsan(fuzz_bin, tmp_path):
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     runs, ok = (int(x) for x in r.stdout.split()[1::2])
     assert runs > 20000 and ok > 0, r.stdout
+
+
+def test_queue_receive_ring_under_asan_ubsan(fuzz_bin):
+    """The queue's pinned receive arena (pinned_ring.hpp): random takes and out-of-order releases,
+    no live range overwritten or crossing the buffer end, the ring whole again at the end."""
+    ring = os.path.join(os.path.dirname(fuzz_bin), "ring_check")
+    for cap, iters in (("4096", "200000"), ("1000003", "50000")):
+        out = subprocess.run([ring, cap, iters], capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stdout + out.stderr
+        assert "ring ok" in out.stdout
