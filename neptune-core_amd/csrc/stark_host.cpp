@@ -283,11 +283,14 @@ uint32_t ood_step_width() {
 }
 
 // The program a batch of n proofs runs: the wide-step one up to NHIP_OOD_WIDE_PROG_MAX proofs (default
-// 2,048), where one proof's evaluation latency matters more than proofs per CU.
+// 1,024), where one proof's evaluation latency matters more than proofs per CU.  Config 4 per-GPU
+// shares (profiles/r04f): 512 proofs 416-419k proofs/s wide vs 398k narrow, 1,024: 427-430k vs 420k,
+// 2,048: 368-374k vs 440k (8 steps in flight: the wide program's one workgroup per CU is the
+// bottleneck there), 4,096: 425k vs 436-437k.
 int ood_program_for(uint32_t n) {
     static const uint32_t lim = [] {
         const char* e = std::getenv("NHIP_OOD_WIDE_PROG_MAX");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 2048u;
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1024u;
     }();
     return n <= lim ? 1 : 0;
 }

@@ -1149,10 +1149,6 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
     // and loading the next step's instruction words during the current one measured slower: config
     // 4 -1.3% at 4,096 proofs, -1% at 512 (profiles/r04e), so each instruction runs on its own.
     Xfe acc = x_zero();
-#ifdef NHIP_OOD_TYPED_ACC
-    // sum_c w_c C_c per constraint type, the zerofier inverses applied once per type at the end
-    Xfe acc_t[4] = {x_zero(), x_zero(), x_zero(), x_zero()};
-#endif
     for (uint32_t lvl = 0; lvl < n_levels; ++lvl) {
         for (uint32_t q = prog_off[lvl] + tid; q < prog_off[lvl + 1]; q += blockDim.x) {
             const OodIns ins = prog[q];
@@ -1161,13 +1157,7 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
                 uint32_t t = 0;
                 while (t < 3 && c >= offs[t + 1]) ++t;
                 const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.quot_w + c));
-#ifdef NHIP_OOD_TYPED_ACC
-                const Xfe v = x_mul(w, fetch(ins.a));
-#pragma unroll
-                for (uint32_t u = 0; u < 4; ++u) acc_t[u] = x_add(acc_t[u], t == u ? v : x_zero());
-#else
                 acc = x_add(acc, x_mul(w, x_mul(fetch(ins.a), zinv[t])));
-#endif
             } else if (ins.op == OOD_LOAD) {
                 slot(ins.dst) = fetch(ins.a);
             } else {
@@ -1177,10 +1167,6 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
         }
         __syncthreads();
     }
-#ifdef NHIP_OOD_TYPED_ACC
-#pragma unroll
-    for (uint32_t u = 0; u < 4; ++u) acc = x_add(acc, x_mul(acc_t[u], zinv[u]));
-#endif
     const Xfe ood_q = block_sum_xfe_waves(acc, red);
     // OOD linear combinations (DEEP needs them): lin weights = [main | aux | quot segs | deep]
     const uint32_t M = dims.num_main, A = dims.num_aux, Q = dims.num_quot_seg;
