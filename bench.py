@@ -91,7 +91,9 @@ def log(*a):
 FETCH_CORRECTION = {"FETCH_SIZE": 2.0, "WRITE_SIZE": 1.0}
 
 
-LIB_PATH = os.path.join(ROOT, "neptune-core_amd", "neptune_hip", "libneptune_hip.so")
+# the library neptune_hip loads (NHIP_LIB selects a variant for A/B runs): the one whose hash keys
+# the committed profiles and is reported in config.lib_sha256
+LIB_PATH = os.environ.get("NHIP_LIB") or os.path.join(ROOT, "neptune-core_amd", "neptune_hip", "libneptune_hip.so")
 
 
 def lib_sha256(path: str = LIB_PATH) -> str:

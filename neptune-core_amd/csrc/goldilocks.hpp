@@ -86,12 +86,15 @@ __host__ __device__ __forceinline__ uint64_t mont_mul_lat(uint64_t a, uint64_t b
     return (E + ~M) + (neg ? GL_P + 1 : 1ull);
 }
 
-// a + b mod p for a, b in [0, p)
+// a + b mod p for a, b in [0, p).  The sum a + b < 2p needs one subtraction of p exactly when it
+// carries out of 64 bits or is >= p, and s - p == s + (2^32 - 1) mod 2^64, so one select of
+// s + EPS does both cases (8 VALU instead of 11: the carry flag is the add's own).
 __host__ __device__ __forceinline__ uint64_t gl_add(uint64_t a, uint64_t b) {
-    const uint64_t s = a + b;
-    const bool ovf = s < a;
-    uint64_t t = ovf ? s + GL_EPS : s;  // wrap: 2^64 == 2^32 - 1 (mod p); cannot overflow again
-    return t >= GL_P ? t - GL_P : t;
+    unsigned int c0, c1;
+    const uint32_t s0 = __builtin_addc((uint32_t)a, (uint32_t)b, 0u, &c0);
+    const uint32_t s1 = __builtin_addc((uint32_t)(a >> 32), (uint32_t)(b >> 32), c0, &c1);
+    const uint64_t s = ((uint64_t)s1 << 32) | s0;
+    return (c1 || s >= GL_P) ? s + GL_EPS : s;
 }
 
 // a - b mod p for a, b in [0, p)

@@ -108,11 +108,11 @@ struct AirNode {
     uint64_t k0, k1, k2;  // AIR_CONST value (raw Montgomery)
 };
 
-// The AIR compiled for k_ood_air (nhip_air_create): per circuit level a list of instructions whose
-// results live in reusable LDS slots (liveness-allocated: a slot is reused from the level after its
-// value's last use), constants in a global table, OOD-row inputs loaded once into slots, and every
-// constraint folded into the weighted quotient sum one level after it is produced, so constraint
-// values do not stay live to the end.
+// The AIR compiled for k_ood_air (nhip_air_create, stark_host.cpp air_compile): steps of independent
+// instructions whose results live in reusable slots (liveness-allocated: a slot is reused from the
+// step after its value's last use), constants in a global table, OOD-row inputs loaded once into
+// slots, and every constraint value copied (ACC) into its own slot among the top C, which the kernel
+// weighs into the quotient sum after the last step.
 enum OodOp : uint32_t { OOD_ADD = AIR_ADD, OOD_SUB = AIR_SUB, OOD_MUL = AIR_MUL, OOD_LOAD = 5, OOD_ACC = 6 };
 // operand reference: [31:30] 0 = LDS slot, 1 = constant table index, 2 = input ([29:27] kind, [26:0] index)
 static constexpr uint32_t OOD_REF_SLOT = 0u << 30, OOD_REF_CONST = 1u << 30, OOD_REF_INPUT = 2u << 30;
@@ -120,7 +120,7 @@ struct OodIns {
     uint32_t op;   // OodOp
     uint32_t a;    // operand ref (LOAD: input ref, ACC: value ref)
     uint32_t b;    // operand ref (ACC: constraint index)
-    uint32_t dst;  // LDS slot (ADD/SUB/MUL/LOAD)
+    uint32_t dst;  // slot written (ACC: the constraint's own slot, slots - C + constraint index)
 };
 
 }  // namespace nhip

@@ -305,9 +305,11 @@ int ood_program_for(uint32_t n) {
 // then in the order of the first constraint that needs them, so constraints are finished one after
 // another and their values released (the same circuit: ~2.3k slots, all in LDS, 3x the steps).
 // A step never takes a node past the LDS slot budget unless it retires a value or the step would be
-// empty.  Constraint accumulations (OOD_ACC) run in the step after their value.  Within a step the
-// instructions are grouped by kind (loads, products, sums, accumulations): a wave then runs one kind
-// of XFE operation instead of the divergent union of several.
+// empty.  A constraint's value is copied (OOD_ACC) in the step after it is computed into its own slot
+// of the top C slots (slots - C + c), and the kernel weighs all C of them in full waves after the last
+// step: folded into the steps, each step paid one mostly idle wave of two XFE products per lane for
+// its handful of constraints.  Within a step the instructions are grouped by kind (copies, products,
+// sums): a wave then runs one kind of XFE operation instead of the divergent union of several.
 void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t width, OodProgram& pg) {
     pg = OodProgram{};
     pg.width = width;
@@ -373,7 +375,8 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
     std::vector<uint32_t> ready;
     for (size_t i = 0; i < NN; ++i)
         if (slotted[i] && deps[i] == 0) ready.push_back((uint32_t)i);
-    const uint32_t budget = AIR_LDS_SLOTS_MAX;
+    // working slots; the C constraint slots above them take their share of the LDS first
+    const uint32_t budget = AIR_LDS_SLOTS_MAX > cons.size() + 256 ? AIR_LDS_SLOTS_MAX - (uint32_t)cons.size() : 256u;
     std::vector<uint32_t> free_slots, to_free;
     uint32_t next_slot = 0, live = 0;
     std::vector<OodIns> cur, acc_next = step0_acc;
@@ -397,9 +400,12 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
             if (slotted[cons[ins.b]]) use(cons[ins.b]);
         for (uint32_t i : ready) key[i] = {-retires(i), ((uint64_t)corder[i] << 32) | i};
         std::sort(ready.begin(), ready.end(), [&](uint32_t x, uint32_t y) { return key[x] < key[y]; });
+        // the step's constraint copies count against its width (width + a few would be one more,
+        // nearly empty pass of the workgroup)
+        const size_t room = width > cur.size() ? width - cur.size() : 1;
         std::vector<uint32_t> chosen, rest;
         for (uint32_t i : ready) {
-            if (chosen.size() < width && (live < budget || key[i].first < 0 || chosen.empty())) {
+            if (chosen.size() < room && (live < budget || key[i].first < 0 || chosen.empty())) {
                 chosen.push_back(i);
                 ++live;
             } else {
@@ -433,16 +439,16 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
         live -= (uint32_t)to_free.size();
         free_slots.insert(free_slots.end(), to_free.begin(), to_free.end());
         to_free.clear();
-        auto kind_rank = [](uint32_t op) {
-            return op == OOD_LOAD ? 0 : (op == AIR_MUL ? 1 : (op == OOD_ACC ? 3 : 2));
-        };
+        auto kind_rank = [](uint32_t op) { return op == OOD_LOAD || op == OOD_ACC ? 0 : (op == AIR_MUL ? 1 : 2); };
         std::stable_sort(cur.begin(), cur.end(),
                          [&](const OodIns& x, const OodIns& y) { return kind_rank(x.op) < kind_rank(y.op); });
         pg.prog.insert(pg.prog.end(), cur.begin(), cur.end());
         pg.prog_off.push_back((uint32_t)pg.prog.size());
         cur.clear();
     }
-    pg.slots = next_slot;
+    for (OodIns& ins : pg.prog)
+        if (ins.op == OOD_ACC) ins.dst = next_slot + ins.b;
+    pg.slots = next_slot + (uint32_t)cons.size();
 }
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }

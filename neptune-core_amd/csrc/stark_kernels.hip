@@ -1046,10 +1046,10 @@ __device__ Xfe eval_terminal_wave(uint32_t n, Xfe c, Sym sym) {
 }
 
 // ------------------------------------------------------------------ OOD: AIR + quotient identity
-// One workgroup per proof.  The compiled AIR program (OodIns, stark.hpp) runs level by level:
+// One workgroup per proof.  The compiled AIR program (OodIns, stark.hpp) runs step by step:
 // OOD-row inputs are loaded into LDS slots, each ADD/SUB/MUL writes its value (XFE) to a reusable
-// slot, and each constraint is folded into this thread's share of sum_i w_i * C_i * Z_type(i)^-1
-// one level after it is produced.  The sum is then compared with sum_k z^k * segment_k(z^4).  Also
+// slot, and each constraint value is copied into its own slot one step after it is produced; after
+// the last step the workgroup forms sum_i w_i * C_i * Z_type(i)^-1 over those slots.  The sum is then compared with sum_k z^k * segment_k(z^4).  Also
 // stores the OOD linear combinations used by DEEP: [sum w*curr row, sum w*next row, sum w*segs].
 // BLOCK = 256 for batches that fill the GPU (the hashing needs the wave slots); 1,024 for small ones
 // (OOD_WIDE_MAX_PROOFS), where one proof's evaluation is on the critical path and the CUs are idle.
@@ -1148,17 +1148,10 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
     // between steps).  Batching a thread's instructions of a step (all operands requested first)
     // and loading the next step's instruction words during the current one measured slower: config
     // 4 -1.3% at 4,096 proofs, -1% at 512 (profiles/r04e), so each instruction runs on its own.
-    Xfe acc = x_zero();
     for (uint32_t lvl = 0; lvl < n_levels; ++lvl) {
         for (uint32_t q = prog_off[lvl] + tid; q < prog_off[lvl + 1]; q += blockDim.x) {
             const OodIns ins = prog[q];
-            if (ins.op == OOD_ACC) {
-                const uint32_t c = ins.b;
-                uint32_t t = 0;
-                while (t < 3 && c >= offs[t + 1]) ++t;
-                const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.quot_w + c));
-                acc = x_add(acc, x_mul(w, x_mul(fetch(ins.a), zinv[t])));
-            } else if (ins.op == OOD_LOAD) {
+            if (ins.op >= OOD_LOAD) {  // an input into its slot, or a constraint into its own slot
                 slot(ins.dst) = fetch(ins.a);
             } else {
                 const Xfe x = fetch(ins.a), y = fetch(ins.b);
@@ -1166,6 +1159,15 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
             }
         }
         __syncthreads();
+    }
+    // sum_c w_c * C_c * Z_type(c)^-1 over the constraint slots (the top C), every lane busy
+    const uint32_t C = dims.num_constraints, cbase = lds_slots + gslot_n - C;
+    Xfe acc = x_zero();
+    for (uint32_t c = tid; c < C; c += blockDim.x) {
+        uint32_t t = 0;
+        while (t < 3 && c >= offs[t + 1]) ++t;
+        const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.quot_w + c));
+        acc = x_add(acc, x_mul(w, x_mul(slot(cbase + c), zinv[t])));
     }
     const Xfe ood_q = block_sum_xfe_waves(acc, red);
     // OOD linear combinations (DEEP needs them): lin weights = [main | aux | quot segs | deep]

@@ -1,4 +1,4 @@
-"""goldilocks.hpp compiled for the host: the closed-form to_mont equals the Montgomery product by
+"""goldilocks.hpp and xfe.hpp compiled for the host: the closed-form to_mont equals the Montgomery product by
 2^128 mod p (BFieldElement::new -> raw word) on edge words (limbs near 0, 2^31, 2^32 - 1; words
 around p and 2^64) and 2M random words.  CPU only."""
 import os
@@ -31,6 +31,20 @@ def test_mds_folded_round_constant_matches_stepwise(tmp_path):
     subprocess.check_call([HIPCC, "-O2", "-std=c++17", "-x", "hip", "--offload-arch=gfx950",
                            "-I", os.path.join(ROOT, "neptune-core_amd", "csrc"),
                            os.path.join(ROOT, "tests", "native", "mds_fold_check.cpp"), "-o", str(exe)],
+                          stderr=subprocess.DEVNULL)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "bad 0" in out.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_lazy_xfe_product_and_field_sum_match_integer_arithmetic(tmp_path):
+    """x_mul's lazily reduced form (nine 128-bit products, three Montgomery reductions) and gl_add's
+    single-select form equal 128-bit integer arithmetic mod p on edge and 3M random operands."""
+    exe = tmp_path / "xfe_check"
+    subprocess.check_call([HIPCC, "-O2", "-std=c++17", "-x", "hip", "--offload-arch=gfx950",
+                           "-I", os.path.join(ROOT, "neptune-core_amd", "csrc"),
+                           os.path.join(ROOT, "tests", "native", "xfe_check.cpp"), "-o", str(exe)],
                           stderr=subprocess.DEVNULL)
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr

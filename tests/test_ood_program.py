@@ -5,7 +5,8 @@ instruction of the same step writes, nor write a slot twice; values come from ea
 Interpreting the program step by step under exactly those rules (reads see the state before the
 step) on random inputs gives, for every constraint, the value of the oracle's circuit evaluation
 (stark_ref.AirCircuit.evaluate), for the synthetic AIR, its triton-air-sized bloat and several step
-widths, with every slot in LDS or with the LDS part capped."""
+widths, with every slot in LDS or with the LDS part capped; each constraint ends in its own slot
+among the top C, where the kernel weighs it into the quotient sum."""
 import numpy as np
 import pytest
 
@@ -23,7 +24,7 @@ def airs():
     return {"synthetic": syn, "triton-size": S.bloat_air(syn, 24000)}
 
 
-def _run_program(off, ins, consts, inputs, n_cons):
+def _run_program(off, ins, consts, inputs, n_cons, n_slots):
     state, got = {}, {}
     for st in range(len(off) - 1):
         step = ins[off[st]:off[st + 1]]
@@ -40,11 +41,11 @@ def _run_program(off, ins, consts, inputs, n_cons):
 
         out = {}
         for op, a, b, dst in (tuple(int(v) for v in row) for row in step):
-            if op == OOD_ACC:
-                assert b not in got, f"constraint {b} accumulated twice"
-                got[b] = val(a)
-                continue
-            if op == OOD_LOAD:
+            if op == OOD_ACC:  # the constraint's value into its own slot, the top n_cons
+                assert b not in got, f"constraint {b} copied twice"
+                assert dst == n_slots - n_cons + b, (dst, b)
+                got[b] = v = val(a)
+            elif op == OOD_LOAD:
                 v = val(a)
             else:
                 x, y = val(a), val(b)
@@ -55,6 +56,8 @@ def _run_program(off, ins, consts, inputs, n_cons):
         assert not (reads & writes), f"step {st}: slots read and written in one step: {sorted(reads & writes)[:5]}"
         state.update(out)
     assert sorted(got) == list(range(n_cons))
+    # the kernel reads the constraints from their slots after the last step
+    assert all(state[n_slots - n_cons + c] == got[c] for c in range(n_cons))
     return [got[c] for c in range(n_cons)]
 
 
@@ -72,14 +75,14 @@ def test_compiled_program_is_a_race_free_schedule_of_the_circuit(airs, monkeypat
     info = g.info()
     off, ins = g.program()
     steps = len(off) - 1
-    slots = 1 + max(int(r[3]) for r in ins if r[0] not in (OOD_ACC,))
+    slots = 1 + max(int(r[3]) for r in ins)
     assert slots == info["lds_slots"] + info["global_slots"]
     if lds_cap:
         assert info["lds_slots"] == lds_cap
     else:
         assert info["global_slots"] == 0
     per_step = np.diff(off.astype(np.int64))
-    assert per_step.max() <= (width or 512) + air.num_constraints  # nodes per step + that step's accumulations
+    assert per_step.max() <= (width or 512)  # nodes per step + that step's constraint copies
     rng = np.random.default_rng(0x00D)
     rnd = lambda: tuple(int(v) for v in rng.integers(0, S.P, size=3, dtype=np.uint64))
     kinds = {S.INPUT_MAIN_CURR: air.num_main, S.INPUT_AUX_CURR: air.num_aux, S.INPUT_MAIN_NEXT: air.num_main,
@@ -91,7 +94,7 @@ def test_compiled_program_is_a_race_free_schedule_of_the_circuit(airs, monkeypat
     want = [v for cs in air.evaluate(vals[S.INPUT_MAIN_CURR], vals[S.INPUT_AUX_CURR], vals[S.INPUT_MAIN_NEXT],
                                      vals[S.INPUT_AUX_NEXT], vals[S.INPUT_CHALLENGE]) for v in cs]
     live_consts = _live_consts(air)
-    got = _run_program(off, ins, [consts[i] for i in live_consts], inputs, air.num_constraints)
+    got = _run_program(off, ins, [consts[i] for i in live_consts], inputs, air.num_constraints, slots)
     assert got == want
     print(f"{name} width {width or 512}: {steps} steps, {info['lds_slots']} LDS + {info['global_slots']} "
           f"global slots, {len(ins)} instructions")
