@@ -309,7 +309,8 @@ int ood_program_for(uint32_t n) {
 // of the top C slots (slots - C + c), and the kernel weighs all C of them in full waves after the last
 // step: folded into the steps, each step paid one mostly idle wave of two XFE products per lane for
 // its handful of constraints.  Within a step the instructions are grouped by kind (copies, products,
-// sums): a wave then runs one kind of XFE operation instead of the divergent union of several.
+// sums, differences): a wave then runs one kind of XFE operation instead of the divergent union of
+// several.
 void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t width, OodProgram& pg) {
     pg = OodProgram{};
     pg.width = width;
@@ -439,7 +440,9 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
         live -= (uint32_t)to_free.size();
         free_slots.insert(free_slots.end(), to_free.begin(), to_free.end());
         to_free.clear();
-        auto kind_rank = [](uint32_t op) { return op == OOD_LOAD || op == OOD_ACC ? 0 : (op == AIR_MUL ? 1 : 2); };
+        auto kind_rank = [](uint32_t op) {
+            return op == OOD_LOAD || op == OOD_ACC ? 0 : (op == AIR_MUL ? 1 : (op == AIR_ADD ? 2 : 3));
+        };
         std::stable_sort(cur.begin(), cur.end(),
                          [&](const OodIns& x, const OodIns& y) { return kind_rank(x.op) < kind_rank(y.op); });
         pg.prog.insert(pg.prog.end(), cur.begin(), cur.end());
