@@ -122,5 +122,6 @@ struct OodIns {
     uint32_t b;    // operand ref (ACC: constraint index)
     uint32_t dst;  // slot written (ACC: the constraint's own slot, slots - C + constraint index)
 };
+static_assert(sizeof(OodIns) == 16, "k_ood_air loads an instruction as one uint4");
 
 }  // namespace nhip

@@ -337,17 +337,18 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
             }
         }
     }
-    // operand refs: constants in the table, inputs and results in slots
-    std::vector<uint32_t> ref(NN, 0);
+    // every live value in a slot: inputs and constants are copied in (LOAD from the inputs or the
+    // constant table), so the operands of ADD / SUB / MUL are slots only and the kernel reads them
+    // from LDS without telling slots from constants (each constant is used about once)
+    std::vector<uint32_t> ref(NN, 0), cidx(NN, 0);
     std::vector<uint8_t> slotted(NN, 0);
     for (size_t i = 0; i < NN; ++i) {
         if (corder[i] == UINT32_MAX) continue;  // dead node
         if (a->nodes[i].op == AIR_CONST) {
-            ref[i] = OOD_REF_CONST | (uint32_t)pg.consts.size();
+            cidx[i] = (uint32_t)pg.consts.size();
             pg.consts.push_back(Xfe{a->nodes[i].k0, a->nodes[i].k1, a->nodes[i].k2});
-        } else {
-            slotted[i] = 1;
         }
+        slotted[i] = 1;
     }
     // remaining uses of each slotted value (operand occurrences + accumulations), pending operands of
     // each node, and the users of each value (CSR)
@@ -367,12 +368,8 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
                 for (uint32_t o : {a->nodes[i].a, a->nodes[i].b})
                     if (slotted[o]) users[fill[o]++] = (uint32_t)i;
     }
-    std::vector<std::vector<uint32_t>> acc_of(NN);  // constraint indices accumulating a slotted node
-    std::vector<OodIns> step0_acc;                  // constraints on constants: accumulated in step 0
-    for (size_t c = 0; c < cons.size(); ++c) {
-        if (slotted[cons[c]]) acc_of[cons[c]].push_back((uint32_t)c);
-        else step0_acc.push_back(OodIns{OOD_ACC, ref[cons[c]], (uint32_t)c, 0});
-    }
+    std::vector<std::vector<uint32_t>> acc_of(NN);  // the constraints each node's value is
+    for (size_t c = 0; c < cons.size(); ++c) acc_of[cons[c]].push_back((uint32_t)c);
     std::vector<uint32_t> ready;
     for (size_t i = 0; i < NN; ++i)
         if (slotted[i] && deps[i] == 0) ready.push_back((uint32_t)i);
@@ -380,7 +377,7 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
     const uint32_t budget = AIR_LDS_SLOTS_MAX > cons.size() + 256 ? AIR_LDS_SLOTS_MAX - (uint32_t)cons.size() : 256u;
     std::vector<uint32_t> free_slots, to_free;
     uint32_t next_slot = 0, live = 0;
-    std::vector<OodIns> cur, acc_next = step0_acc;
+    std::vector<OodIns> cur, acc_next;
     std::vector<std::pair<int32_t, uint64_t>> key(NN);
     auto retires = [&](uint32_t i) {  // operands whose last use this node is
         if (!is_op(i)) return 0;
@@ -425,6 +422,8 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
                 const AirNode& nd = a->nodes[i];
             if (nd.op == AIR_INPUT) {
                 cur.push_back(OodIns{OOD_LOAD, OOD_REF_INPUT | (nd.a << 27) | nd.b, 0, sl});
+            } else if (nd.op == AIR_CONST) {
+                cur.push_back(OodIns{OOD_LOAD, OOD_REF_CONST | cidx[i], 0, sl});
             } else {
                 cur.push_back(OodIns{nd.op, ref[nd.a], ref[nd.b], sl});
                 use(nd.a);

@@ -1057,7 +1057,9 @@ __device__ Xfe eval_terminal_wave(uint32_t n, Xfe c, Sym sym) {
 #define NHIP_OOD_WAVES 1
 #endif
 
-template <uint32_t BLOCK, bool MW>
+// GS: the program has slots past the LDS part (gslot_n > 0); without them every slot access is a
+// plain LDS access (ds_read / ds_write) instead of a branch between LDS and the global area.
+template <uint32_t BLOCK, bool MW, bool GS>
 __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_ood_air(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                                  uint32_t n_proofs, StarkDims dims, const OodIns* __restrict__ prog,
                                                  const uint32_t* __restrict__ prog_off, uint32_t n_levels,
@@ -1079,7 +1081,11 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
     // proof's global slot area; the slot allocator reuses low slots first, so the hot ones stay in
     // LDS.  The barrier after each level orders the global writes for the workgroup as well.
     Xfe* gval = gslots + (uint64_t)p * gslot_n;
-    auto slot = [&](uint32_t s) -> Xfe& { return s < lds_slots ? val[s] : gval[s - lds_slots]; };
+    auto slot_ld = [&](uint32_t s) -> Xfe { return !GS || s < lds_slots ? val[s] : gval[s - lds_slots]; };
+    auto slot_st = [&](uint32_t s, const Xfe& v) {
+        if (!GS || s < lds_slots) val[s] = v;
+        else gval[s - lds_slots] = v;
+    };
     if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
     const ProofDesc& d = desc[p];
     const SampleLayout sl = SampleLayout::of(dims, d.R);
@@ -1132,7 +1138,7 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
     const uint32_t offs[5] = {0u, cons_type_off.x, cons_type_off.y, cons_type_off.z, cons_type_off.w};
     auto fetch = [&](uint32_t ref) -> Xfe {
         const uint32_t t = ref >> 30;
-        if (t == 0) return slot(ref);
+        if (t == 0) return slot_ld(ref);
         if (t == 1) return consts[ref & 0x3FFFFFFFu];
         const uint32_t kind = (ref >> 27) & 7u, i = ref & 0x7FFFFFFu;
         switch (kind) {
@@ -1150,12 +1156,13 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
     // 4 -1.3% at 4,096 proofs, -1% at 512 (profiles/r04e), so each instruction runs on its own.
     for (uint32_t lvl = 0; lvl < n_levels; ++lvl) {
         for (uint32_t q = prog_off[lvl] + tid; q < prog_off[lvl + 1]; q += blockDim.x) {
-            const OodIns ins = prog[q];
-            if (ins.op >= OOD_LOAD) {  // an input into its slot, or a constraint into its own slot
-                slot(ins.dst) = fetch(ins.a);
+            const uint4 ins = reinterpret_cast<const uint4*>(prog)[q];  // (op, a, b, dst): one 16-B load
+            if (ins.x >= OOD_LOAD) {  // an input into its slot, or a constraint into its own slot
+                slot_st(ins.w, fetch(ins.y));
             } else {
-                const Xfe x = fetch(ins.a), y = fetch(ins.b);
-                slot(ins.dst) = ins.op == OOD_ADD ? x_add(x, y) : (ins.op == OOD_SUB ? x_sub(x, y) : x_mul(x, y));
+                // operands are slots (air_compile copies inputs and constants into slots first)
+                const Xfe x = slot_ld(ins.y), y = slot_ld(ins.z);
+                slot_st(ins.w, ins.x == OOD_ADD ? x_add(x, y) : (ins.x == OOD_SUB ? x_sub(x, y) : x_mul(x, y)));
             }
         }
         __syncthreads();
@@ -1167,7 +1174,7 @@ __global__ void __launch_bounds__(BLOCK, BLOCK == 256 ? NHIP_OOD_WAVES : 1) k_oo
         uint32_t t = 0;
         while (t < 3 && c >= offs[t + 1]) ++t;
         const Xfe w = ld_xfe_raw(xs, xb + 3ull * (sl.quot_w + c));
-        acc = x_add(acc, x_mul(w, x_mul(slot(cbase + c), zinv[t])));
+        acc = x_add(acc, x_mul(w, x_mul(slot_ld(cbase + c), zinv[t])));
     }
     const Xfe ood_q = block_sum_xfe_waves(acc, red);
     // OOD linear combinations (DEEP needs them): lin weights = [main | aux | quot segs | deep]
@@ -1663,14 +1670,19 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
         mark(10, st);
         if (!small) (void)hipStreamWaitEvent(sa, tm->ev[10], 0);  // small: OOD right after the plan
         mark(11, sa);
-        if (ood_wide(n))
-            hipLaunchKernelGGL((k_ood_air<1024, MW>), dim3(n), dim3(1024), b.air_lds_bytes, sa, b.words, b.desc, n, b.dims,
-                               b.air_prog, b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs, b.ood,
-                               b.fail, b.air_lds_slots, b.air_gslots, b.air_gslot_n);
-        else
-            hipLaunchKernelGGL((k_ood_air<256, MW>), dim3(n), dim3(b.air_block), b.air_lds_bytes, sa, b.words, b.desc, n,
-                               b.dims, b.air_prog, b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs,
-                               b.ood, b.fail, b.air_lds_slots, b.air_gslots, b.air_gslot_n);
+#define NHIP_OOD_LAUNCH(BLK, GS, THREADS)                                                                       \
+    hipLaunchKernelGGL((k_ood_air<BLK, MW, GS>), dim3(n), dim3(THREADS), b.air_lds_bytes, sa, b.words, b.desc, n,    \
+                       b.dims, b.air_prog, b.air_prog_off, b.air_n_levels, b.air_consts, b.air_cons_off, b.xs, b.ood, \
+                       b.fail, b.air_lds_slots, b.air_gslots, b.air_gslot_n)
+        const bool gs = b.air_gslot_n > 0;
+        if (ood_wide(n)) {
+            if (gs) NHIP_OOD_LAUNCH(1024, true, 1024);
+            else NHIP_OOD_LAUNCH(1024, false, 1024);
+        } else {
+            if (gs) NHIP_OOD_LAUNCH(256, true, b.air_block);
+            else NHIP_OOD_LAUNCH(256, false, b.air_block);
+        }
+#undef NHIP_OOD_LAUNCH
         mark(6, sa);
         if (small) {
             (void)hipStreamWaitEvent(sa, tm->ev[7], 0);  // FRI done (main stream)
@@ -1763,11 +1775,11 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
 
 template <bool MW>
 static hipError_t set_attributes() {
-    hipError_t e = hipFuncSetAttribute((const void*)k_ood_air<256, MW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       AIR_LDS_BUDGET);
-    if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void*)k_ood_air<1024, MW>, hipFuncAttributeMaxDynamicSharedMemorySize, AIR_LDS_BUDGET);
-    if (e != hipSuccess) return e;
+    for (const void* f : {(const void*)k_ood_air<256, MW, false>, (const void*)k_ood_air<256, MW, true>,
+                          (const void*)k_ood_air<1024, MW, false>, (const void*)k_ood_air<1024, MW, true>}) {
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, AIR_LDS_BUDGET);
+        if (e != hipSuccess) return e;
+    }
     return hipFuncSetAttribute((const void*)k_deep_rows8<MW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                160 * 1024 - 8192);
 }
