@@ -374,7 +374,9 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
     for (size_t i = 0; i < NN; ++i)
         if (slotted[i] && deps[i] == 0) ready.push_back((uint32_t)i);
     // working slots; the C constraint slots above them take their share of the LDS first
-    const uint32_t budget = AIR_LDS_SLOTS_MAX > cons.size() + 256 ? AIR_LDS_SLOTS_MAX - (uint32_t)cons.size() : 256u;
+    // (NHIP_OOD_SLOT_BUDGET lowers it, A/B runs)
+    uint32_t budget = AIR_LDS_SLOTS_MAX > cons.size() + 256 ? AIR_LDS_SLOTS_MAX - (uint32_t)cons.size() : 256u;
+    if (const char* e = std::getenv("NHIP_OOD_SLOT_BUDGET")) budget = std::min<uint32_t>(budget, std::max(64ul, std::strtoul(e, nullptr, 10)));
     std::vector<uint32_t> free_slots, to_free;
     uint32_t next_slot = 0, live = 0;
     std::vector<OodIns> cur, acc_next;

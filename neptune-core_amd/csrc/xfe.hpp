@@ -98,16 +98,22 @@ __host__ __device__ __forceinline__ uint64_t red160(U160 x) {
 // (a0 + a1 x + a2 x^2)(b0 + b1 x + b2 x^2) with x^3 = x - 1, x^4 = x^2 - x:
 //   c0 = a0b0 - (a1b2 + a2b1),  c1 = a0b1 + a1b0 + (a1b2 + a2b1) - a2b2,  c2 = a0b2 + a1b1 + a2b0 + a2b2
 __host__ __device__ __forceinline__ Xfe x_mul(Xfe a, Xfe b) {
-    const U128 p00 = mul128(a.c0, b.c0), p01 = mul128(a.c0, b.c1), p02 = mul128(a.c0, b.c2);
-    const U128 p10 = mul128(a.c1, b.c0), p11 = mul128(a.c1, b.c1), p12 = mul128(a.c1, b.c2);
-    const U128 p20 = mul128(a.c2, b.c0), p21 = mul128(a.c2, b.c1), p22 = mul128(a.c2, b.c2);
+    // three groups of three products, each group's coefficient reduced before the next group's
+    // products are formed: fewer live 128-bit values (k_ood_air 121 -> 97 VGPRs, k_deep_rows8's
+    // spill 96 -> 56 bytes per lane), the same instructions.  The 128-bit products with
+    // v_mad_u64_u32's carry-out (mad_carry3, tip5_device.hpp: ~180 instead of ~200 VALU per XFE
+    // product) measured -1.1% at 4,096 proofs, the OOD kernel's dependent chain longer (ab_r04l).
+    const U128 p12 = mul128(a.c1, b.c2), p21 = mul128(a.c2, b.c1), p00 = mul128(a.c0, b.c0);
     const U160 n = add160(wide(p12), p21);  // < 2p^2
-    const U160 s0 = sub160_2p(wide(p00), n);
+    Xfe r;
+    r.c0 = red160(sub160_2p(wide(p00), n));
+    const U128 p01 = mul128(a.c0, b.c1), p10 = mul128(a.c1, b.c0), p22 = mul128(a.c2, b.c2);
     U160 s1 = add160(add160(wide(p01), p10), U128{n.lo, n.hi});
     s1.top += n.top;
-    s1 = sub160_2p(s1, wide(p22));
-    const U160 s2 = add160(add160(add160(wide(p02), p11), p20), p22);
-    return {red160(s0), red160(s1), red160(s2)};
+    r.c1 = red160(sub160_2p(s1, wide(p22)));
+    const U128 p02 = mul128(a.c0, b.c2), p11 = mul128(a.c1, b.c1), p20 = mul128(a.c2, b.c0);
+    r.c2 = red160(add160(add160(add160(wide(p02), p11), p20), p22));
+    return r;
 }
 
 // x^(2^n) (n successive Montgomery squarings)
