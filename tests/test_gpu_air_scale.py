@@ -73,4 +73,12 @@ def test_triton_air_sized_circuit_matches_oracle_in_lds_and_with_global_slots(ct
     print(f"k_ood_air, 256 proofs, {len(big.nodes)} nodes / {info['lds_slots']} LDS + "
           f"{info['global_slots']} global slots: {st['ms_ood_air']:.3f} ms")
     many.close()
+    # the 256-thread evaluator with global slots (batches past OOD_WIDE_MAX_PROOFS): accepting and
+    # OOD-mutated proofs interleaved
+    mixed = [proof if i % 2 == 0 else muts[i % 3] for i in range(256)]
+    want_m = [i % 2 == 0 for i in range(256)]
+    bm = NS.Batch(ctx, gair_g, NS.Stark.default(), [NS.Claim(*claim)] * 256, mixed)
+    vm, _ = bm.run()
+    assert [bool(x) for x in vm] == want_m
+    bm.close()
     b.close()
