@@ -17,7 +17,7 @@ verdict copy back (nhip_batch_launch / nhip_batch_wait) and, for N > 1, the verd
 verdict is the MIN of the leading bytes; block validation needs every transaction's verdict:
 SURVEY.md §8e), posted without waiting and completed one step later, the last one inside the timed
 region (shard.VerdictExchange); config 3 one all-reduce(MIN) of the batch verdict.  Steps are pipelined as a node verifying a stream
-of batches runs them (--inflight; 2 at >= 4,096 proofs per GPU, 8 from 1,024, 10 below): resident copies rotate, step k+1 is launched before step k
+of batches runs them (--inflight; 8 from 1,024 proofs per GPU, 10 below): resident copies rotate, step k+1 is launched before step k
 is waited on, so one step's latency-bound phases overlap the other's VALU-bound hashing; every timed
 step is launched and waited inside the timed region.  Two copies x 2 streams need more than HIP's
 default 4 hardware queues per process, so GPU_MAX_HW_QUEUES is raised here before HIP starts (to
@@ -278,12 +278,16 @@ def make_batch(pool, collections: int, corrupt_frac: float, seed: int):
 
 
 def default_inflight(n: int) -> int:
-    """Steps in flight for an n-proof batch per GPU: 2 from 4,096 proofs, 8 from 1,024, 10 below
-    (the N = 2 / 4 / 8 shares of config 4; config 5's 8-64 proofs: 10 vs 8 in flight +10-11%,
-    profiles/r03s).  512 proofs 342-348k (4) -> 366-367k (8) proofs/s, 1,024 388-390k -> 393-397k,
-    2,048 412-414k -> 416-417k, 4,096 423-426k (2) vs 421-422k (4); 12 or more in flight (24
-    hardware queues) collapse to ~120k (profiles/r03j, 2 repetitions each)."""
-    return 2 if n >= 4096 else (8 if n >= 1024 else 10)
+    """Steps in flight for an n-proof batch per GPU: 8 from 1,024 proofs, 10 below (the N = 1 / 2 / 4
+    / 8 shares of config 4; config 5's 8-64 proofs: 10 vs 8 in flight +10-11%, profiles/r03s).
+    Round 4, the driver's command (20 timed steps after 5 warm-up steps; `gpurun_out/ab_r04q`):
+    4,096 proofs 461.6-462.0k at 8 in flight vs 453.7-455.9k at 2; 512 proofs 393.7-396.4k at 10,
+    367.6-377.9k at 6, 340.4-345.5k at 4; 200 steps: 4,096 at 8 461.5-463.7k vs 450.1-451.6k at 2
+    (`ab_r04n`, `ab_r04o`).  (Before the library made a batch's streams, events and pinned readback
+    at its preparation, a resident batch whose first launch fell inside the timed region stalled the
+    others: with 5 warm-up steps, 512 proofs ran at 91-93k with 10 in flight.)  More than 11 in
+    flight would take more than the 24 hardware queues below."""
+    return 8 if n >= 1024 else 10
 
 
 def hw_queues_wanted(inflight: int, multi_rank: bool) -> int:

@@ -1011,25 +1011,39 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         return NHIP_ERR_HIP;                                \
     }
 
+static int launch_resources(nhip_batch* b);
+
+// A resident batch: prepared, and its launch resources made now rather than at its first launch (a
+// failure there is left to the launch to report)
+static int prepare_resident(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
+                            const nhip_proof* proofs, size_t n, nhip_batch** out, nhip_batch* reuse) {
+    const int rc = batch_prepare(ctx, air, sp, claims, proofs, n, out, nullptr, reuse);
+    if (rc != NHIP_OK || !*out) return rc;
+    std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
+    (void)hipSetDevice((*out)->device);
+    (void)launch_resources(*out);
+    return NHIP_OK;
+}
+
 int nhip_batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
                        const nhip_proof* proofs, size_t n, nhip_batch** out) {
-    NHIP_GUARD(batch_prepare(ctx, air, sp, claims, proofs, n, out, nullptr))
+    NHIP_GUARD(prepare_resident(ctx, air, sp, claims, proofs, n, out, nullptr))
 }
 
 int nhip_batch_refill(nhip_ctx* ctx, nhip_batch* b, nhip_air* air, const nhip_stark_params* sp,
                       const nhip_claim* claims, const nhip_proof* proofs, size_t n) {
     if (!b) return NHIP_ERR_ARG;
     nhip_batch* out = b;
-    NHIP_GUARD(batch_prepare(ctx, air, sp, claims, proofs, n, &out, nullptr, b))
+    NHIP_GUARD(prepare_resident(ctx, air, sp, claims, proofs, n, &out, b))
 }
 
-// Enqueue every device phase of the batch on the batch's own two streams (no host wait).  Batches
-// launched back to back run concurrently on the device.
-int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
-    if (!ctx || !b) return NHIP_ERR_ARG;
-    std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
-    (void)hipSetDevice(b->device);
-    if (b->in_flight) return NHIP_ERR_ARG;
+// The batch's launch resources: its two streams and timing events (or a verify scratch's) and the
+// pinned readback.  Made when the batch is prepared (and on the first launch of one prepared
+// before): creating streams, events and pinned memory waits on the device, so doing it at a
+// batch's first launch stalled the other batches in flight (a run whose resident batches first
+// launch inside a timed region: config 4 at 512 proofs and 10 in flight, 5 warm-up steps, ran at a
+// quarter of its rate).
+static int launch_resources(nhip_batch* b) {
     if (!b->timed) {
         const char* al = std::getenv("NHIP_AUX_AFTER_LEVEL");
         b->tm.aux_after_level = al ? (uint32_t)std::strtoul(al, nullptr, 10) : AUX_AFTER_LEVEL_DEFAULT;
@@ -1079,6 +1093,17 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
             b->h_out_bytes = want;
         }
     }
+    return NHIP_OK;
+}
+
+// Enqueue every device phase of the batch on the batch's own two streams (no host wait).  Batches
+// launched back to back run concurrently on the device.
+int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
+    if (!ctx || !b) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
+    (void)hipSetDevice(b->device);
+    if (b->in_flight) return NHIP_ERR_ARG;
+    if (int rc = launch_resources(b)) return rc;
     hipStream_t st = b->main;
     const uint32_t n = b->dev.n_proofs;
     hipError_t e = hipSuccess;

@@ -114,7 +114,7 @@ def test_inflight_defaults_and_queue_budget():
     """Steps in flight per per-GPU batch size (the driver's N = 1 / 2 / 4 / 8 shares of config 4
     and config 5's small batches) and the hardware queues bench.py provisions for them: every batch
     stream keeps its own queue, below the 24 past which the device time-slices queues."""
-    assert [bench.default_inflight(n) for n in (4096, 2048, 1024, 512, 64, 8)] == [2, 8, 8, 10, 10, 10]
+    assert [bench.default_inflight(n) for n in (4096, 2048, 1024, 512, 64, 8)] == [8, 8, 8, 10, 10, 10]
     for n in (4096, 2048, 1024, 512, 64, 8):
         for multi in (False, True):
             r = bench.default_inflight(n)
