@@ -93,15 +93,18 @@ def test_latest_profile_files_and_pmc_figures(monkeypatch):
 
 
 def test_summary_reproduces_the_bench_roofline():
-    """SUMMARY.md's figure from the kernel trace of the timed (in-flight) steps agrees with the bench's
-    frac under the profiler within 5% (the all-dispatch average also holds the warmup's launches)."""
+    """SUMMARY.md's figures from the kernel traces agree with the bench's under the profiler: the
+    reported (isolated-launch) roofline within 2%.  The in-flight side field is a looser check: with
+    8 steps in flight (round 4) a launch's HIP start event is stamped while its dispatch still waits
+    behind the other steps' kernels, so the bench's average runs above the trace's dispatch time
+    (+14% in profiles/r04r; within 1% at round 3's 2 in flight)."""
     tag, _, _ = _latest()
     _profiled_lib(tag)
     text = open(os.path.join(ROOT, "profiles", tag, "SUMMARY.md")).read()
     line = next(x for x in text.splitlines() if x.startswith("roofline frac from the trace:"))
     frac_trace = float(line.split("T = ")[1].split(";")[0])
     frac_bench = float(line.rsplit("frac ", 1)[1])
-    assert abs(frac_trace / frac_bench - 1) < 0.05, (frac_trace, frac_bench)
+    assert 0.97 < frac_trace / frac_bench < 1.25, (frac_trace, frac_bench)
     # the reported (isolated-launch) roofline: the trace of the one-at-a-time steps within 2%
     iso = [x for x in text.splitlines() if x.startswith("isolated roofline frac from the trace:")]
     if iso:  # (profiles from round 4 on)
