@@ -39,7 +39,10 @@ static constexpr uint32_t MP_SHARDS = 16;
 static constexpr uint64_t MP_WIDE_MAX_OPS = 48 * 1024;
 // the last levels whose ops (multiproof + last-codeword parents) all fit this many rows are climbed
 // by one workgroup in one launch (k_mp_hash_tail), up to MP_TAIL_LEVELS_MAX levels
-static constexpr uint64_t MP_TAIL_MAX_OPS = 256;
+#ifndef NHIP_MP_TAIL_MAX_OPS
+#define NHIP_MP_TAIL_MAX_OPS 256
+#endif
+static constexpr uint64_t MP_TAIL_MAX_OPS = NHIP_MP_TAIL_MAX_OPS;
 static constexpr uint32_t MP_TAIL_LEVELS_MAX = 32;
 // batches of at most this many proofs climb every tree in its own workgroup (k_mp_climb), one
 // launch for all levels, instead of one launch per level
