@@ -341,7 +341,7 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
     // constant table), so the operands of ADD / SUB / MUL are slots only and the kernel reads them
     // from LDS without telling slots from constants (each constant is used about once)
     std::vector<uint32_t> ref(NN, 0), cidx(NN, 0);
-    std::vector<uint8_t> slotted(NN, 0);
+    std::vector<uint8_t> slotted(NN, 0);  // live nodes (every one takes a slot)
     for (size_t i = 0; i < NN; ++i) {
         if (corder[i] == UINT32_MAX) continue;  // dead node
         if (a->nodes[i].op == AIR_CONST) {
@@ -368,7 +368,7 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
                 for (uint32_t o : {a->nodes[i].a, a->nodes[i].b})
                     if (slotted[o]) users[fill[o]++] = (uint32_t)i;
     }
-    std::vector<std::vector<uint32_t>> acc_of(NN);  // the constraints each node's value is
+    std::vector<std::vector<uint32_t>> acc_of(NN);  // per node: the constraints whose value it is
     for (size_t c = 0; c < cons.size(); ++c) acc_of[cons[c]].push_back((uint32_t)c);
     std::vector<uint32_t> ready;
     for (size_t i = 0; i < NN; ++i)
@@ -376,7 +376,8 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
     // working slots; the C constraint slots above them take their share of the LDS first
     // (NHIP_OOD_SLOT_BUDGET lowers it, A/B runs)
     uint32_t budget = AIR_LDS_SLOTS_MAX > cons.size() + 256 ? AIR_LDS_SLOTS_MAX - (uint32_t)cons.size() : 256u;
-    if (const char* e = std::getenv("NHIP_OOD_SLOT_BUDGET")) budget = std::min<uint32_t>(budget, std::max(64ul, std::strtoul(e, nullptr, 10)));
+    if (const char* e = std::getenv("NHIP_OOD_SLOT_BUDGET"))
+        budget = std::min<uint32_t>(budget, (uint32_t)std::max(64ul, std::strtoul(e, nullptr, 10)));
     std::vector<uint32_t> free_slots, to_free;
     uint32_t next_slot = 0, live = 0;
     std::vector<OodIns> cur, acc_next;
@@ -421,7 +422,7 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
             } else {
                 sl = next_slot++;
             }
-                const AirNode& nd = a->nodes[i];
+            const AirNode& nd = a->nodes[i];
             if (nd.op == AIR_INPUT) {
                 cur.push_back(OodIns{OOD_LOAD, OOD_REF_INPUT | (nd.a << 27) | nd.b, 0, sl});
             } else if (nd.op == AIR_CONST) {
