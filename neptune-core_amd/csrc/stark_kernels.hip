@@ -1049,8 +1049,9 @@ __device__ Xfe eval_terminal_wave(uint32_t n, Xfe c, Sym sym) {
 // One workgroup per proof.  The compiled AIR program (OodIns, stark.hpp) runs step by step:
 // OOD-row inputs are loaded into LDS slots, each ADD/SUB/MUL writes its value (XFE) to a reusable
 // slot, and each constraint value is copied into its own slot one step after it is produced; after
-// the last step the workgroup forms sum_i w_i * C_i * Z_type(i)^-1 over those slots.  The sum is then compared with sum_k z^k * segment_k(z^4).  Also
-// stores the OOD linear combinations used by DEEP: [sum w*curr row, sum w*next row, sum w*segs].
+// the last step the workgroup forms sum_i w_i * C_i * Z_type(i)^-1 over those slots and compares it
+// with sum_k z^k * segment_k(z^4).  Also stores the OOD linear combinations used by DEEP:
+// [sum w*curr row, sum w*next row, sum w*segs].
 // BLOCK = 256 for batches that fill the GPU (the hashing needs the wave slots); 1,024 for small ones
 // (OOD_WIDE_MAX_PROOFS), where one proof's evaluation is on the critical path and the CUs are idle.
 #ifndef NHIP_OOD_WAVES
