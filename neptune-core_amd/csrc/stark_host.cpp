@@ -1013,6 +1013,11 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     }
 
 static int launch_resources(nhip_batch* b);
+// start / stop events on every Merkle hash launch of a resident batch (the bench's roofline timing);
+// 0 builds a variant without them (A/B of their cost)
+#ifndef NHIP_HASH_LAUNCH_EVENTS
+#define NHIP_HASH_LAUNCH_EVENTS 1
+#endif
 
 // A resident batch: prepared, and its launch resources made now rather than at its first launch (a
 // failure there is left to the launch to report)
@@ -1072,7 +1077,7 @@ static int launch_resources(nhip_batch* b) {
         } else {
             for (int i = 0; i < STARK_EVENTS; ++i)
                 if (hipEventCreate(&b->tm.ev[i]) != hipSuccess) return NHIP_ERR_HIP;
-            for (uint32_t i = 0; i < 2 * MAX_HASH_LAUNCHES; ++i)  // per hash launch (device-resident batches)
+            for (uint32_t i = 0; i < (NHIP_HASH_LAUNCH_EVENTS ? 2 * MAX_HASH_LAUNCHES : 0); ++i)  // per hash launch
                 if (hipEventCreate(&b->tm.lev[i]) != hipSuccess) {
                     for (uint32_t j = 0; j < i; ++j) (void)hipEventDestroy(b->tm.lev[j]);
                     for (uint32_t j = 0; j < 2 * MAX_HASH_LAUNCHES; ++j) b->tm.lev[j] = nullptr;
