@@ -61,16 +61,21 @@ def _run_program(off, ins, consts, inputs, n_cons, n_slots):
     return [got[c] for c in range(n_cons)]
 
 
-@pytest.mark.parametrize("name,width,lds_cap", [("synthetic", None, None), ("triton-size", None, None),
-                                                 ("triton-size", 256, None), ("triton-size", 1024, None),
-                                                 ("triton-size", 512, 600)])
-def test_compiled_program_is_a_race_free_schedule_of_the_circuit(airs, monkeypatch, name, width, lds_cap):
+@pytest.mark.parametrize("name,width,lds_cap,budget", [("synthetic", None, None, None),
+                                                        ("triton-size", None, None, None),
+                                                        ("triton-size", 256, None, None),
+                                                        ("triton-size", 1024, None, None),
+                                                        ("triton-size", 512, 600, None),
+                                                        ("triton-size", 512, None, 1200)])
+def test_compiled_program_is_a_race_free_schedule_of_the_circuit(airs, monkeypatch, name, width, lds_cap, budget):
     import neptune_hip.stark as NS
     air = airs[name]
     if width:
         monkeypatch.setenv("NHIP_OOD_STEP_WIDTH", str(width))
     if lds_cap:
         monkeypatch.setenv("NHIP_OOD_LDS_SLOTS", str(lds_cap))
+    if budget:  # a tight working-slot budget: nodes wait unless they retire a value
+        monkeypatch.setenv("NHIP_OOD_SLOT_BUDGET", str(budget))
     g = NS.Air(air.to_words())
     info = g.info()
     off, ins = g.program()
