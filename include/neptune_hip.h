@@ -15,8 +15,13 @@
  *     (SURVEY.md §8b).
  *   - Thread safety: a context may be shared by threads; calls on one context are serialized
  *     onto that context's HIP stream.
- *   - One context drives one GPU (one process per GPU; multi-GPU sharding is done by the
- *     caller, see bench.py / DESIGN.md).
+ *   - Every entry point leaves the calling thread's current HIP device as it found it (a host
+ *     with its own HIP user, e.g. torch, is not disturbed).
+ *   - One context drives one GPU.  Every GPU of a node is driven from the one neptune-core
+ *     process by a group (nhip_group_*: one context per member device, batches LPT-sharded at
+ *     proof granularity, verdicts merged on the host; nhip_group_stream_* for batch after batch).
+ *     The multi-process form (one rank per GPU, one RCCL verdict all-gather per step) is the
+ *     Python host's neptune_hip.shard / bench.py.
  *
  * Reference interfaces replaced (paths relative to /root/reference):
  *   nhip_tip5_hash_pair     <- twenty-first 1.0.0 Tip5::hash_pair, as called by
@@ -230,7 +235,10 @@ void nhip_batch_destroy(nhip_batch *batch);
  * max_wait_us after the oldest arrival) into one device batch, with the next batch collected while
  * the current one runs.  Each caller copies its proofs into the queue's pinned arena itself (in
  * parallel with the other callers), so the worker only DMAs them; a request the arena cannot hold
- * at the time goes through the context's staging instead.  max_batch 0 = 4096. */
+ * at the time goes through the context's staging instead.  max_batch 0 = 4096.
+ * Pinned footprint: the arena is min(256 MB, max(16 MB, 4 MB x max_batch)) of pinned host memory
+ * per queue; the environment variable NHIP_QUEUE_ARENA_MB (read at create) sets it instead, 0 for
+ * none. */
 typedef struct nhip_queue nhip_queue;
 int nhip_queue_create(nhip_ctx *ctx, nhip_air *air, const nhip_stark_params *params, uint32_t max_batch,
                       uint32_t max_wait_us, nhip_queue **out);

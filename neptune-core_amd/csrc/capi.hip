@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/neptune_hip.h"
+#include "device_scope.hpp"
 #include "kernels.hpp"
 
 struct nhip_ctx {
@@ -181,7 +182,7 @@ int nhip_init(uint32_t device_mask, nhip_ctx** out) {
 
 void nhip_destroy(nhip_ctx* c) {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (auto& p : c->pending) {
         (void)hipEventDestroy(p.first);
@@ -233,14 +234,14 @@ void* nhip_internal_staging(nhip_ctx* c, size_t bytes) {
 int nhip_dev_alloc(nhip_ctx* c, size_t bytes, void** dptr) {
     if (!c || !dptr) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     return hip_fail(hipMalloc(dptr, bytes ? bytes : 1));
 }
 
 int nhip_dev_free(nhip_ctx* c, void* d) {
     if (!c) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     (void)hipStreamSynchronize(c->stream);
     return hip_fail(hipFree(d));
 }
@@ -248,7 +249,7 @@ int nhip_dev_free(nhip_ctx* c, void* d) {
 int nhip_memcpy_h2d(nhip_ctx* c, void* dst, const void* src, size_t bytes) {
     if (!c) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     return hip_fail(e);
@@ -257,7 +258,7 @@ int nhip_memcpy_h2d(nhip_ctx* c, void* dst, const void* src, size_t bytes) {
 int nhip_memcpy_d2h(nhip_ctx* c, void* dst, const void* src, size_t bytes) {
     if (!c) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     return hip_fail(e);
@@ -266,35 +267,35 @@ int nhip_memcpy_d2h(nhip_ctx* c, void* dst, const void* src, size_t bytes) {
 int nhip_synchronize(nhip_ctx* c) {
     if (!c) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     return hip_fail(hipStreamSynchronize(c->stream));
 }
 
 int nhip_tip5_permutation_dev(nhip_ctx* c, uint64_t* d_states, size_t n) {
     if (!c || (n && !d_states)) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     return timed_launch(c, [&] { return nhip::launch_permutation(d_states, n, c->stream); });
 }
 
 int nhip_tip5_hash_pair_dev(nhip_ctx* c, const uint64_t* l, const uint64_t* r, size_t n, uint64_t* o) {
     if (!c || (n && (!l || !r || !o))) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     return timed_launch(c, [&] { return nhip::launch_hash_pair(l, r, o, n, c->stream); });
 }
 
 int nhip_tip5_hash_varlen_dev(nhip_ctx* c, const uint64_t* d, const uint64_t* off, size_t n, uint64_t* o) {
     if (!c || (n && (!off || !o))) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     return timed_launch(c, [&] { return nhip::launch_hash_varlen(d, off, n, o, c->stream); });
 }
 
 int nhip_mtree_build_dev(nhip_ctx* c, const uint64_t* d_leafs, size_t n, uint64_t* d_nodes) {
     if (!c || !is_pow2(n) || !d_leafs || !d_nodes) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     return build_tree_dev(c, d_leafs, n, d_nodes);
 }
 
@@ -303,7 +304,7 @@ int nhip_mtree_verify_dev(nhip_ctx* c, const uint64_t* roots, size_t n_roots, co
     if (!c || (n_roots != 1 && n_roots != n)) return NHIP_ERR_ARG;
     if (n && (!roots || !idx || !leafs || !v || (depth && !paths))) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     const int per_path = (n_roots == n && n != 1) ? 1 : 0;
     return timed_launch(c, [&] {
         return nhip::launch_mtree_verify(roots, per_path, idx, leafs, paths, depth, n, v, c->stream);
@@ -313,7 +314,7 @@ int nhip_mtree_verify_dev(nhip_ctx* c, const uint64_t* roots, size_t n_roots, co
 int nhip_verdicts_all_dev(nhip_ctx* c, const uint8_t* d_v, size_t n, uint8_t* all_ok) {
     if (!c || !all_ok || (n && !d_v)) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     size_t sizes[1] = {sizeof(uint32_t)};
     void* p[1];
     int rc = carve(c, sizes, p);
@@ -343,7 +344,7 @@ int nhip_tip5_permutation(nhip_ctx* c, uint64_t* states, size_t n) {
     if (!c || (n && !states)) return NHIP_ERR_ARG;
     if (n == 0) return NHIP_OK;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     const size_t bytes = n * 16 * sizeof(uint64_t);
     size_t sizes[1] = {bytes};
     void* p[1];
@@ -362,7 +363,7 @@ int nhip_tip5_hash_pair(nhip_ctx* c, const uint64_t* l, const uint64_t* r, size_
     if (!c || (n && (!l || !r || !o))) return NHIP_ERR_ARG;
     if (n == 0) return NHIP_OK;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     const size_t db = n * 5 * sizeof(uint64_t);
     size_t sizes[3] = {db, db, db};
     void* p[3];
@@ -388,7 +389,7 @@ int nhip_tip5_hash_varlen(nhip_ctx* c, const uint64_t* data, const uint64_t* off
     const size_t total = (size_t)offsets[n];
     if (total && !data) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     size_t sizes[3] = {total * sizeof(uint64_t), (n + 1) * sizeof(uint64_t), n * 5 * sizeof(uint64_t)};
     void* p[3];
     int rc = carve(c, sizes, p);
@@ -409,7 +410,7 @@ int nhip_tip5_hash_varlen(nhip_ctx* c, const uint64_t* data, const uint64_t* off
 int nhip_mtree_build(nhip_ctx* c, const uint64_t* leafs, size_t n, uint64_t* nodes_out) {
     if (!c || !is_pow2(n) || !leafs || !nodes_out) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     const size_t db = n * 5 * sizeof(uint64_t);
     size_t sizes[2] = {db, db};
     void* p[2];
@@ -430,7 +431,7 @@ int nhip_mtree_verify(nhip_ctx* c, const uint64_t* roots, size_t n_roots, const 
     if (n == 0) return NHIP_OK;
     if (!roots || !idx || !leafs || !v || (depth && !paths)) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     size_t sizes[5] = {n_roots * 5 * sizeof(uint64_t), n * sizeof(uint64_t), n * 5 * sizeof(uint64_t),
                        n * (size_t)depth * 5 * sizeof(uint64_t), n};
     void* p[5];
@@ -464,7 +465,7 @@ int nhip_timing_enable(nhip_ctx* c, int on) {
 int nhip_timing_read(nhip_ctx* c, double* total_ms, uint64_t* launches, int reset) {
     if (!c) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(e);
     for (auto& pr : c->pending) {
@@ -498,7 +499,7 @@ int nhip_mast_hash_batch(nhip_ctx* c, const uint64_t* data, const uint64_t* offs
     uint32_t pow2 = 1;
     while (pow2 < fields) pow2 <<= 1;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     size_t sizes[4] = {total * 8, (nl + 1) * 8, nl * 40, n * 40};
     void* p[4];
     int rc = carve(c, sizes, p);
@@ -536,7 +537,7 @@ int nhip_absolute_index_sets(nhip_ctx* c, const uint64_t* items, const uint64_t*
             in[15 * i + 10 + q] = receiver_preimages[5 * i + q];
         }
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    const DeviceScope device_scope(c->device);
     size_t sizes[4] = {15 * n * 8, n * 8, 2 * n * 8, 45 * n * 4};
     void* p[4];
     int rc = carve(c, sizes, p);

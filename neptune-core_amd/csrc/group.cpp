@@ -192,7 +192,7 @@ struct MemberSlots {
     bool in_flight[2] = {false, false};
     std::vector<nhip_claim> claims;
     std::vector<nhip_proof> proofs;
-    std::vector<uint8_t> v;
+    std::vector<uint8_t> v[2];  // per slot: sized to that slot's share when the slot is refilled
 };
 
 }  // namespace
@@ -236,9 +236,10 @@ struct nhip_group_stream {
         ms.in_flight[s] = false;
         StreamBatch& B = sb[s];
         const size_t cnt = B.idx[mm].size();
-        const int rc = nhip_batch_wait(g->members[mm], ms.b[s], ms.v.data(), nullptr);
+        if (ms.v[s].size() < cnt) return NHIP_ERR_ARG;  // sized at submit; never written past
+        const int rc = nhip_batch_wait(g->members[mm], ms.b[s], ms.v[s].data(), nullptr);
         if (rc) return rc;
-        for (size_t q = 0; q < cnt; ++q) B.verdicts[B.idx[mm][q]] = ms.v[q];
+        for (size_t q = 0; q < cnt; ++q) B.verdicts[B.idx[mm][q]] = ms.v[s][q];
         nhip_stats st{};
         nhip_batch_stats(ms.b[s], &st);
         dev_ms[mm] += st.ms_device_total;
@@ -320,7 +321,10 @@ int nhip_group_stream_submit(nhip_group_stream* st, const nhip_claim* claims, co
                 ms.claims.push_back(claims[i]);
                 ms.proofs.push_back(proofs[i]);
             }
-            ms.v.resize(std::max<size_t>(1, st->sb[sp].idx[mm].size()));  // the previous share's verdicts
+            // slot s is idle (its batch k - 2 was completed by the previous submit): size its verdict
+            // buffer to THIS share, the one complete_member(mm, s) will read back (here, on the
+            // calling thread, so an allocation failure is a return code, not a throw in a member thread)
+            ms.v[s].resize(std::max<size_t>(1, B.idx[mm].size()));
             if (!B.idx[mm].empty() || ms.in_flight[sp]) who.push_back(mm);
         }
         B.live = true;  // an empty batch too: its AND (1) is written with the others'

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../../include/neptune_hip.h"
+#include "device_scope.hpp"
 #include "goldilocks.hpp"
 #include "pow.hpp"
 
@@ -89,7 +90,7 @@ int nhip_pow_preprocess(nhip_ctx* ctx, uint32_t height, const nhip_pow_mast_path
     if (!b) return NHIP_ERR_OOM;
     b->height = height;
     b->device = nhip_internal_device(ctx);
-    (void)hipSetDevice(b->device);
+    const DeviceScope device_scope(b->device);
     for (int q = 0; q < 5; ++q) b->prev_block_digest[q] = prev_block_digest[q] % GL_P;
     const size_t bytes = ((size_t)1 << height) * 40;
     hipError_t e = hipMalloc(&b->d_a, bytes);
@@ -113,7 +114,7 @@ int nhip_pow_preprocess(nhip_ctx* ctx, uint32_t height, const nhip_pow_mast_path
 
 void nhip_pow_buffer_destroy(nhip_pow_buffer* b) {
     if (!b) return;
-    (void)hipSetDevice(b->device);
+    const DeviceScope device_scope(b->device);
     if (b->d_a) (void)hipFree(b->d_a);
     if (b->d_b) (void)hipFree(b->d_b);
     delete b;
@@ -147,7 +148,7 @@ int nhip_pow_guess_batch(nhip_ctx* ctx, const nhip_pow_buffer* b, const nhip_pow
     if (!ctx || !b || !mast || !index_picker_preimage || !target || (n && (!nonces || !success_out))) return NHIP_ERR_ARG;
     if (n == 0) return NHIP_OK;
     std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
-    (void)hipSetDevice(b->device);
+    const DeviceScope device_scope(b->device);
     hipStream_t st = nhip_internal_stream(ctx);
     std::vector<uint64_t> nr(5 * n);
     for (size_t i = 0; i < 5 * n; ++i) nr[i] = to_mont(nonces[i]);
@@ -222,7 +223,7 @@ int nhip_pow_validate_batch(nhip_ctx* ctx, uint32_t height, const uint64_t* root
         b.reboot = reboot_rules[i] ? 1u : 0u;
     }
     std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
-    (void)hipSetDevice(nhip_internal_device(ctx));
+    const DeviceScope device_scope(nhip_internal_device(ctx));
     hipStream_t st = nhip_internal_stream(ctx);
     PowBlock* d_b = nullptr;
     uint8_t* d_v = nullptr;

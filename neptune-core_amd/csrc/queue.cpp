@@ -19,6 +19,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -51,8 +52,17 @@ struct Req {
     uint64_t arena_at = ~0ull;  // its proofs' range in the pinned arena (~0: its own memory)
 };
 
-// arena size: about two full batches of config-4-sized proofs from concurrent callers
-constexpr uint64_t ARENA_BYTES = 256ull << 20;
+// Arena size: at most 256 MB (about two full batches of config-4-sized proofs from concurrent
+// callers), at most 2 MB per proof of two max_batch batches (a Stark::default() proof of padded
+// height 2^23 is ~1.4 MB), at least 16 MB.  NHIP_QUEUE_ARENA_MB overrides it (read at create; 0 =
+// no arena: every request goes through the context's staging).  A node with one queue per GPU
+// pins this much host memory per queue.
+constexpr uint64_t ARENA_MAX_BYTES = 256ull << 20, ARENA_MIN_BYTES = 16ull << 20;
+static uint64_t arena_bytes(uint32_t max_batch) {
+    if (const char* e = std::getenv("NHIP_QUEUE_ARENA_MB")) return (uint64_t)std::strtoull(e, nullptr, 10) << 20;
+    const uint64_t by_batch = (uint64_t)max_batch * 2 * (2ull << 20);
+    return std::max(ARENA_MIN_BYTES, std::min(ARENA_MAX_BYTES, by_batch));
+}
 
 }  // namespace
 
@@ -236,9 +246,10 @@ int nhip_queue_create(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* par
     q->max_wait = std::chrono::microseconds(max_wait_us);
     {
         void* a = nullptr;
-        if (nhip_host_alloc(ARENA_BYTES, &a) == NHIP_OK) {  // without it every request is staged
+        const uint64_t ab = arena_bytes(q->max_batch);
+        if (ab && nhip_host_alloc(ab, &a) == NHIP_OK) {  // without it every request is staged
             q->ring.base = (uint8_t*)a;
-            q->ring.cap = ARENA_BYTES;
+            q->ring.cap = ab;
         }
     }
     try {

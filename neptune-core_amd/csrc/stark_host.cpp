@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/neptune_hip.h"
+#include "device_scope.hpp"
 #include "../../include/nhip_challenge_id.h"
 #include "goldilocks.hpp"
 #include "kernels.hpp"
@@ -558,7 +559,7 @@ int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
 void nhip_air_destroy(nhip_air* a) {
     if (!a) return;
     for (const auto& d : a->devs) {
-        (void)hipSetDevice(d.device);
+        const DeviceScope device_scope(d.device);
         for (int k = 0; k < 2; ++k) {
             (void)hipFree(d.d_prog[k]);
             (void)hipFree(d.d_prog_off[k]);
@@ -646,7 +647,7 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
             claims[i].output_len > 0xFFFFFFFFull)
             return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
-    (void)hipSetDevice(nhip_internal_device(ctx));
+    const DeviceScope device_scope(nhip_internal_device(ctx));
     nhip_batch* b = reuse ? reuse : new (std::nothrow) nhip_batch();
     if (!b) return NHIP_ERR_OOM;
     // on failure: a new batch is deleted; a refilled one is left empty (n = 0) but usable
@@ -715,10 +716,11 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
             void** dw = scr ? &scr->dwords : &b->dwords;
             size_t* dwb = scr ? &scr->dwords_bytes : &b->dwords_bytes;
             if (*dwb < wbytes) {
+                const size_t have = *dwb;  // read before the free: the growth rule doubles from it
                 if (*dw) (void)hipFree(*dw);
                 *dw = nullptr;
                 *dwb = 0;
-                const size_t want = grown(wbytes, *dwb, reuse || scr);
+                const size_t want = grown(wbytes, have, reuse || scr);
                 const hipError_t ea = hipMalloc(dw, want);
                 if (ea != hipSuccess) {
                     if (scr) b->dwords = nullptr;
@@ -1026,7 +1028,7 @@ static int prepare_resident(nhip_ctx* ctx, nhip_air* air, const nhip_stark_param
     const int rc = batch_prepare(ctx, air, sp, claims, proofs, n, out, nullptr, reuse);
     if (rc != NHIP_OK || !*out) return rc;
     std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
-    (void)hipSetDevice((*out)->device);
+    const DeviceScope device_scope((*out)->device);
     (void)launch_resources(*out);
     return NHIP_OK;
 }
@@ -1107,7 +1109,7 @@ static int launch_resources(nhip_batch* b) {
 int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
     if (!ctx || !b) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
-    (void)hipSetDevice(b->device);
+    const DeviceScope device_scope(b->device);
     if (b->in_flight) return NHIP_ERR_ARG;
     if (int rc = launch_resources(b)) return rc;
     hipStream_t st = b->main;
@@ -1131,7 +1133,7 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
 // copy) are on the main stream, which joins the aux chain before them.
 bool nhip_internal_batch_done(nhip_batch* b) {
     if (!b || !b->in_flight) return true;
-    (void)hipSetDevice(b->device);
+    const DeviceScope device_scope(b->device);
     return hipStreamQuery(b->main) != hipErrorNotReady;
 }
 
@@ -1139,7 +1141,7 @@ bool nhip_internal_batch_done(nhip_batch* b) {
 int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* all_ok) {
     if (!ctx || !b) return NHIP_ERR_ARG;
     if (!b->in_flight) return NHIP_ERR_ARG;
-    (void)hipSetDevice(b->device);
+    const DeviceScope device_scope(b->device);
     hipError_t e = hipStreamSynchronize(b->main);
     b->in_flight = false;
     if (e != hipSuccess) return hipfail(e);
@@ -1234,7 +1236,7 @@ int nhip_batch_transcript(nhip_ctx* ctx, const nhip_batch* b, size_t proof, uint
                           uint32_t* idx_out, size_t idx_cap, uint32_t* fail_out, size_t* n_xfe) {
     if (!ctx || !b || proof >= b->dev.n_proofs || b->in_flight) return NHIP_ERR_ARG;
     std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
-    (void)hipSetDevice(b->device);
+    const DeviceScope device_scope(b->device);
     hipStream_t st = nhip_internal_stream(ctx);
     ProofDesc pd{};
     hipError_t e = hipMemcpyAsync(&pd, b->dev.desc + proof, sizeof(pd), hipMemcpyDeviceToHost, st);
@@ -1260,7 +1262,7 @@ int nhip_batch_transcript(nhip_ctx* ctx, const nhip_batch* b, size_t proof, uint
 
 void nhip_batch_destroy(nhip_batch* b) {
     if (!b) return;
-    (void)hipSetDevice(b->device);
+    const DeviceScope device_scope(b->device);
     if (b->in_flight && b->main) (void)hipStreamSynchronize(b->main);
     if (b->scratch) {  // resources belong to the context's verify scratch
         delete b;

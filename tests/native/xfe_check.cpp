@@ -1,8 +1,9 @@
 // Host-side check of xfe.hpp / goldilocks.hpp against 128-bit integer arithmetic mod p: the lazily
 // reduced x_mul (nine 128-bit products, three reductions) equals the Montgomery-domain product
 // c_k = (sum of +-a_i b_j) * 2^-64 mod p, and gl_add equals (a + b) mod p, on edge words (0, 1,
-// p - 1, 2^32 +- 1, words with all-ones limbs) and random canonical words (run by
-// tests/test_goldilocks_host.py).
+// p - 1, 2^32 +- 1, words with all-ones limbs) and random canonical words, and with the second
+// operand any u64 (p, p + 1, 2^64 - 1, random full-range words), as DEEP passes raw proof words
+// (run by tests/test_goldilocks_host.py).
 #include "xfe.hpp"
 #include <cstdio>
 #include <random>
@@ -49,6 +50,7 @@ int main() {
                                 (unsigned long long)b.c1, (unsigned long long)b.c2);
             ++bad;
         }
+        if (b.c0 >= GL_P) return;  // gl_add takes canonical operands only
         const uint64_t s = gl_add(a.c0, b.c0);
         if (s != addmod(a.c0, b.c0)) {
             if (bad < 5) printf("gl_add %llx %llx\n", (unsigned long long)a.c0, (unsigned long long)b.c0);
@@ -65,6 +67,19 @@ int main() {
             }
     auto word = [&]() -> uint64_t { return (g() & 7) == 0 ? edge[g() % NE] : g() % GL_P; };
     for (int i = 0; i < 3000000; ++i) chk(Xfe{word(), word(), word()}, Xfe{word(), word(), word()});
+    // the second operand as k_deep_rows8 passes it (ld_xfe_raw of proof words): any u64, words at or
+    // above p included, against a canonical first operand (the raw Montgomery weight)
+    const uint64_t raw_edge[] = {GL_P, GL_P + 1, GL_P + GL_EPS, 0xFFFFFFFFFFFFFFFFull, 0xFFFFFFFFFFFFFFFEull,
+                                 0xFFFFFFFF80000000ull, 0xFFFFFFFF00000001ull, 0, 1, GL_P - 1};
+    const int NR = sizeof(raw_edge) / sizeof(raw_edge[0]);
+    for (int i = 0; i < NE; ++i)
+        for (int j = 0; j < NR; ++j)
+            for (int k = 0; k < NR; ++k) {
+                chk(Xfe{edge[i], edge[(i + 3) % NE], edge[(i + 7) % NE]}, Xfe{raw_edge[j], raw_edge[k], raw_edge[(j + k) % NR]});
+                chk(Xfe{GL_P - 1, GL_P - 1, GL_P - 1}, Xfe{raw_edge[j], raw_edge[k], raw_edge[j]});
+            }
+    auto any = [&]() -> uint64_t { return (g() & 7) == 0 ? raw_edge[g() % NR] : g(); };
+    for (int i = 0; i < 2000000; ++i) chk(Xfe{word(), word(), word()}, Xfe{any(), any(), any()});
     printf("checked %llu, bad %llu\n", (unsigned long long)n, (unsigned long long)bad);
     return bad != 0;
 }

@@ -49,3 +49,31 @@ def test_group_stream_verdicts(batches, members, mont):
         assert v == [bool(x) for x in expect]
         assert ok == bool(expect.all())
     assert stats["proofs"] == sum(len(b[1]) for b in bs) and stats["ms_device"] > 0
+
+
+@pytest.mark.parametrize("sizes", [(64,), (3, 7, 300), (1, 256)])
+def test_group_stream_growing_last_share(batches, sizes):
+    """One submit then finish, and batches that grow so the last share is larger than every share
+    before it: each member's verdict buffer is sized to the share it reads back (the round-4 advisor
+    finding: the buffer was sized to the previous share, and finish wrote past it)."""
+    import neptune_hip.stark as NS
+    air_words, bs = batches
+    air = NS.Air([int(w) for w in air_words])
+    stark = NS.Stark.default()
+    pool_c = [c for b in bs[:4] for c in b[0]]
+    pool_p = [p for b in bs[:4] for p in b[1]]
+    pool_e = np.concatenate([b[2] for b in bs[:4]])
+    got, want, at = [], [], 0
+    with NS.Group([0, 0]) as g, NS.GroupStream(g, air, stark) as st:
+        for n in sizes:
+            cl = [NS.Claim(*c) for c in pool_c[at:at + n]]
+            r = st.submit(list(zip(cl, pool_p[at:at + n])))
+            want.append(pool_e[at:at + n])
+            at += n
+            if r is not None:
+                got.append(r)
+        got.append(st.finish())
+    assert len(got) == len(sizes)
+    for (v, ok), expect in zip(got, want):
+        assert v == [bool(x) for x in expect]
+        assert ok == bool(expect.all())
