@@ -414,24 +414,17 @@ def cpu_baseline(air_words, claims, proofs, expect, target_s: float, threads: in
 # ------------------------------------------------------------------ config 1: single-proof latency
 def config1_case(air_words):
     """BASELINE config 1 substitute (the reference's SingleProof is unavailable
-    offline): one SingleProof-shaped proof at log2 padded height 21, seed 0xC1 (the claim of
-    single_proof.rs:295-304: input = a 5-word kernel MAST hash reversed, output empty; synthetic
-    program digest).  Constant-codeword prover (oracle/stark_prover_const.py): the verifier's work
-    does not depend on the values, and the proof takes a second to make."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import stark_prover_const as K  # test-data generator (proof construction only)
-    import stark_ref as S
-    import tip5_ref as T
-    T.use_c_backend()
-    params = S.StarkParams()
-    _, recipe = S.synth_air(params, seed=1)
-    air = S.AirCircuit.from_words([int(w) for w in air_words])
-    rng = np.random.default_rng(0xC1)
-    kernel_mast_hash = [int(x) for x in rng.integers(0, P, size=5, dtype=np.uint64)]
-    program_digest = [int(x) for x in rng.integers(0, P, size=5, dtype=np.uint64)]
-    claim = (program_digest, 0, kernel_mast_hash[::-1], [])
-    proof, _ = K.prove(params, air, recipe, claim, 21, seed=0xC1)
-    return claim, np.asarray(proof, dtype=np.uint64)
+    offline): one SingleProof-shaped proof at log2 padded height 21 (FRI domain 2^24, 15 FRI
+    rounds), the claim of single_proof.rs:295-304 (input = a 5-word kernel MAST hash reversed,
+    output empty; synthetic program digest, seed 0xC1).  tests/golden/config1.npz, made by the
+    sparse synthetic prover (tests/golden/make_config1.py): every FRI codeword non-zero, a
+    non-empty last polynomial (the constant-codeword proof used before folded zeros).  Returns
+    (claim, proof, oracle samples, oracle FRI indices)."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "config1.npz"))
+    m = json.loads(bytes(z["meta"]).decode())
+    claim = (m["digest"], m["version"], m["input"], m["output"])
+    samples = [tuple(int(c) for c in x) for x in z["samples"]]
+    return claim, np.asarray(z["proof"], dtype=np.uint64), samples, [int(i) for i in z["indices"]]
 
 
 def config1_latency(ctx, gair, stark, air_words, cpu_seconds: float, reps: int = 50):
@@ -442,18 +435,20 @@ def config1_latency(ctx, gair, stark, air_words, cpu_seconds: float, reps: int =
     import coracle as C  # oracle: CPU baseline leg only
     import neptune_hip.stark as NS
     import stark_ref as S
-    claim, proof = config1_case(air_words)
+    claim, proof, samples, indices = config1_case(air_words)
     dcl, dpr = device_form([claim], [proof], stark.input_form == 1)
     ncl, dproof = NS.Claim(*dcl[0]), dpr[0]
     b = NS.Batch(ctx, gair, stark, [ncl], [dproof])
     for _ in range(5):
         v, _ = b.run()
+    xs, idx, fail = b.transcript(0)
+    transcript_ok = fail == 0 and xs == samples and idx == indices
     res_ms = []
     for _ in range(reps):
         t = time.perf_counter()
         v, _ = b.run()
         res_ms.append((time.perf_counter() - t) * 1e3)
-    ok = bool(v[0])
+    ok = bool(v[0]) and transcript_ok
     b.close()
     host_ms = []
     for _ in range(max(5, reps // 5)):
@@ -472,13 +467,79 @@ def config1_latency(ctx, gair, stark, air_words, cpu_seconds: float, reps: int =
     cpu = float(np.median(cpu_ms))
     return {"workload": "BASELINE config 1 substitute: one SingleProof-shaped proof, log2 padded height 21 "
                         "(FRI domain 2^24, 15 FRI rounds), seed 0xC1, Stark::default()",
-            "proof_words": int(proof.size), "verdict_accept": ok,
+            "proof": "tests/golden/config1.npz (sparse synthetic prover: non-zero FRI codewords, last polynomial "
+                     "of degree 122)",
+            "proof_words": int(proof.size), "verdict_accept": ok, "transcript_equals_oracle": transcript_ok,
             "gpu_resident_ms": gpu, "gpu_from_host_ms": float(np.median(host_ms)),
             "cpu_ms": cpu, "cpu_threads": 1, "cpu_kind": "port", "cpu_runs": len(cpu_ms),
             "gpu_speedup": cpu / gpu,
             "measured": f"medians: {reps} resident runs (launch to verdicts back), {len(host_ms)} nhip_verify_batch "
                         f"calls from host memory, {len(cpu_ms)} single-thread runs of the C restatement "
                         f"(oracle/stark_oracle.c)"}
+
+
+def config5_leg(ctx, gair, stark, proofs_n: int = 64, steps: int = 20, inflight: int = 4):
+    """BASELINE config 5 beside the headline: `proofs_n` proofs at log2 padded height 23 (FRI domain
+    2^26, 16 folding rounds) on one GPU.  The proof is tests/golden/deep_fri.npz's height-23 case
+    (the sparse synthetic prover: every FRI codeword non-zero, a non-empty last polynomial), its
+    words copied once per proof; `inflight` resident batches, `steps` steps after 3 warm-up steps.
+    Beside the rate: one batch alone (phase split; the sequential Fiat-Shamir sponge replay's share
+    of that batch's device time) and proof 0's transcript against the oracle's, stored with the
+    fixture."""
+    import neptune_hip.stark as NS
+    z = np.load(os.path.join(ROOT, "tests", "golden", "deep_fri.npz"))
+    meta = json.loads(bytes(z["meta"]).decode())["cases"]["23"]
+    claim = (meta["digest"], meta["version"], meta["input"], meta["output"])
+    proof = z["proof_23"]
+    samples = [tuple(int(c) for c in x) for x in z["samples_23"]]
+    indices = [int(i) for i in z["indices_23"]]
+    dcl, dpr = device_form([claim], [proof], stark.input_form == 1)
+    ncl = [NS.Claim(*dcl[0])] * proofs_n
+    prs = [np.array(dpr[0], dtype=np.uint64, copy=True) for _ in range(proofs_n)]
+    ring = [NS.Batch(ctx, gair, stark, ncl, prs) for _ in range(inflight)]
+    ok = True
+    # alone: phase split and the transcript
+    v, _ = ring[0].run()
+    alone = ring[0].stats()
+    xs, idx, fail = ring[0].transcript(0)
+    transcript_ok = fail == 0 and xs == samples and idx == indices
+    ok = ok and bool(np.asarray(v, dtype=bool).all()) and transcript_ok
+
+    def region(k):
+        nonlocal ok
+        inflight_q = []
+        for i in range(min(inflight, k)):
+            ring[i].launch()
+            inflight_q.append(i)
+        launched = len(inflight_q)
+        while inflight_q:
+            i = inflight_q.pop(0)
+            vv, _ = ring[i].wait()
+            ok = ok and bool(np.asarray(vv, dtype=bool).all())
+            if launched < k:
+                ring[i].launch()
+                inflight_q.append(i)
+                launched += 1
+
+    region(3)
+    ctx.synchronize()
+    t = time.perf_counter()
+    region(steps)
+    ctx.synchronize()
+    dt = time.perf_counter() - t
+    for b in ring:
+        b.close()
+    dev = max(alone["ms_device_total"], 1e-9)
+    return {"workload": f"BASELINE config 5: {proofs_n} proofs at log2 padded height 23 (FRI domain 2^26, 16 FRI "
+                        f"rounds), one GPU, Stark::default()",
+            "proof": "tests/golden/deep_fri.npz height 23 (sparse synthetic prover: non-zero FRI codewords)",
+            "proof_words": int(proof.size), "value": proofs_n * steps / dt, "unit": "proofs/s",
+            "ms_per_step": dt / steps * 1e3, "steps": steps, "inflight": inflight,
+            "alone_ms": {k[3:]: round(alone[k], 4) for k in ("ms_device_decode", "ms_fiat_shamir", "ms_row_hash",
+                                                               "ms_merkle", "ms_ood_air", "ms_fri", "ms_deep",
+                                                               "ms_device_total")},
+            "sponge_replay_share": alone["ms_fiat_shamir"] / dev,
+            "transcript_equals_oracle": transcript_ok, "verdicts_correct": ok}
 
 
 # ------------------------------------------------------------------ config 2 Tip5 path microbench
@@ -535,7 +596,7 @@ def pcie_stream(ctx, gair, stark, claims, proofs, expect, batches: int):
     launch / wait, so each upload overlaps the other batch's device run.  Beside it the raw
     host-to-device rate of one copy of the same bytes: the link's measured ceiling."""
     import neptune_hip.stark as NS
-    pinned = NS.PinnedProofs(proofs)
+    pinned = NS.PinnedProofs(proofs, near=ctx)  # the receive path: pinned, on the GPU's NUMA node
     ncl = [NS.Claim(*c) for c in claims]
     nbytes = sum(len(p) for p in proofs) * 8
     # raw DMA of the proof bytes, pinned -> device (best of 3)
@@ -598,16 +659,27 @@ def device_form(claims, proofs, mont: bool):
     return [(words(c[0]), c[1], words(c[2]), words(c[3])) for c in claims], [conv(p) for p in proofs]
 
 
-def group_stream(devices, air_words, stark, claims, proofs, expect, batches: int):
+def group_stream(devices, air_words, stark, claims, proofs, expect, batches: int, pageable: bool = False):
     """The in-process multi-GPU form neptune-core runs: ONE process driving every GPU through
     nhip_group_stream (GpuNode::verify_stream in the Rust crate).  The job's whole batch is submitted
-    `batches` times from pinned host memory; each member's share of batch k is staged and uploaded
-    while its share of batch k - 1 runs, the members in parallel.  Two warm submissions first (each
-    member's two device batches are allocated on first use)."""
+    `batches` times from host memory; each member's share of batch k is staged and uploaded while
+    its share of batch k - 1 runs, the members in parallel.  Two warm submissions first (each
+    member's two device batches are allocated on first use).
+    pageable=False: the proofs in pinned memory (nhip_host_alloc_near on the first member's node,
+    the receive path), DMA'd as they lie.  pageable=True: every proof in its own ordinary
+    allocation, as the Rust drop-in hands `proof.0.as_ptr()` of each `Vec` over
+    (rust/neptune-hip/src/lib.rs marshal): the library copies the words into each member's pinned
+    staging on copy threads bound to that GPU's NUMA node, then DMAs them."""
     import neptune_hip.stark as NS
-    pinned = NS.PinnedProofs(proofs)
     ncl = [NS.Claim(*c) for c in claims]
-    m = NS.marshal(ncl, pinned.views)
+    pinned = None
+    if pageable:
+        # distinct allocations: config 4 reuses 256 pool proofs, which would stay cache-resident
+        src = [np.array(p, dtype=np.uint64, copy=True) for p in proofs]
+    else:
+        pinned = NS.PinnedProofs(proofs)
+        src = pinned.views
+    m = NS.marshal(ncl, src)
     gair = NS.Air([int(w) for w in air_words])
     want = [bool(x) for x in expect]
     ok = True
@@ -623,15 +695,20 @@ def group_stream(devices, air_words, stark, claims, proofs, expect, batches: int
         ok = ok and st.finish()[0] == want
         dt = time.perf_counter() - t
         st1 = st.stats()
-    pinned.close()
+        numa = g.numa()
+    if pinned is not None:
+        pinned.close()
     nbytes = sum(len(p) for p in proofs) * 8
     d = {k: (st1[k] - st0[k]) / batches for k in ("ms_stage", "ms_upload", "ms_device")}
     return {"value": len(proofs) * batches / dt, "unit": "proofs/s", "gpus": len(devices), "batches": batches,
             "proofs_per_batch": len(proofs), "h2d_GBps": nbytes * batches / dt / 1e9,
             "per_batch_ms": {"wall": dt / batches * 1e3, "stage_sum_members": d["ms_stage"],
                              "upload_wait_sum_members": d["ms_upload"], "device_sum_members": d["ms_device"]},
-            "verdicts_correct": ok,
-            "measured": f"{batches} submissions of the whole batch from pinned host memory through "
+            "verdicts_correct": ok, "source": "pageable (one allocation per proof)" if pageable else "pinned",
+            "numa": [{"device": d["device"], "node": d["node"], "cpus": len(d["cpus"])} for d in numa],
+            "numa_binding": os.environ.get("NHIP_NUMA", "1") != "0",
+            "measured": f"{batches} submissions of the whole batch from "
+                        f"{'pageable' if pageable else 'pinned'} host memory through "
                         f"nhip_group_stream over devices {list(devices)} (one process)"}
 
 
@@ -672,6 +749,8 @@ def main():
     ap.add_argument("--config1-seconds", type=float, default=8.0,
                     help="config-1 single-proof latency leg: CPU-restatement time budget (0 = skip the leg)")
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
+    ap.add_argument("--config5-proofs", type=int, default=64,
+                    help="config-5 leg at N = 1: proofs at log2 padded height 23 (0 = skip)")
     ap.add_argument("--stream-batches", type=int, default=6,
                     help="PCIe-inclusive leg: batches streamed from pinned host memory (0 = skip)")
     ap.add_argument("--shuffle", action="store_true",
@@ -998,6 +1077,21 @@ def main():
                                    f"the kernel's own rate: {iso_steps} steps one at a time right after the timed "
                                    f"region; per-launch HIP events (hipExtLaunchKernel start/stop)")
         assert res["roofline"]["launches_x_avg_ms"] <= step_ms, (res["roofline"], step_ms)
+        # the row-hashing launch of the same isolated steps (k_hash_rows: one lane per revealed row,
+        # every main / aux / quotient row's hash_varlen; dispatch begin / end events), beside the
+        # Merkle launches: permutations per launch = proofs x checks x sum over the three trees of
+        # (width // 10 + 1), priced at the same 7,520 lane-ops per permutation
+        rows_ms = acc_iso.get("ms_row_hash_exec", 0.0) / iso_steps
+        if rows_ms > 0:
+            widths = (stark.num_main, 3 * stark.num_aux, 3 * stark.num_quotient_segments)
+            rows_perms = n * stark.num_collinearity_checks * sum(w // 10 + 1 for w in widths)
+            ach = rows_perms * TIP5_VALU_OPS_PER_PERM / (rows_ms / 1e3)
+            res["roofline"]["rows_kernel"] = {
+                "kernel": "k_hash_rows", "kernel_avg_ms": rows_ms, "perms_per_launch": rows_perms,
+                "achieved": ach / 1e12, "frac": ach / VALU_PEAK_LANE_OPS,
+                "frac_of_measured_ceiling": ach / (VALU_ISSUE_CEILING * 64),
+                "row_bytes_per_launch": n * stark.num_collinearity_checks * sum(widths) * 8,
+                "measured": f"the same {iso_steps} isolated steps; hipExtLaunchKernel start/stop of the row launch"}
         res["roofline"]["inflight"] = {k: inflight[k] for k in ("achieved", "frac", "kernel_avg_ms",
                                                                  "kernel_avg_ms_events", "launches_per_step",
                                                                  "perms_per_launch", "launches_x_avg_ms", "step_ms",
@@ -1035,6 +1129,11 @@ def main():
         res["pcie_inclusive"] = pcie_stream(ctx, gair, stark, dev_claims, dev_proofs, expect, args.stream_batches)
     if world == 1 and args.paths_log2 > 0:
         res["tip5_paths"] = tip5_paths(ctx, args.paths_log2, 5)
+    if world == 1 and args.config5_proofs > 0:
+        t = time.time()
+        res["config5"] = config5_leg(ctx, gair, stark, args.config5_proofs)
+        correct = correct and res["config5"]["verdicts_correct"]
+        log(f"[config5] {res['config5']['value']:.0f} proofs/s ({time.time() - t:.1f}s)")
     if world == 1 and args.config1_seconds > 0 and not args.no_cpu:
         res["config1_latency"] = config1_latency(ctx, gair, stark, air_words, args.config1_seconds)
         correct = correct and res["config1_latency"]["verdict_accept"]
@@ -1057,23 +1156,34 @@ def main():
             # every GPU the job's ranks use (a gloo rehearsal puts several ranks on one GPU)
             devs = sorted({r if dist is None or os.environ.get("NHIP_DIST_BACKEND", "nccl") == "nccl"
                            else r % max(1, __import__("torch").cuda.device_count()) for r in range(world)})
+            out = {}
             try:
-                return group_stream(devs, air_words, stark, dcl, dpr, job_expect, args.group_batches)
+                out["pinned"] = group_stream(devs, air_words, stark, dcl, dpr, job_expect, args.group_batches)
+                out["pageable"] = group_stream(devs, air_words, stark, dcl, dpr, job_expect, args.group_batches,
+                                               pageable=True)
             except Exception as e:  # noqa: BLE001 -- a leg, never the headline
-                return {"error": repr(e), "verdicts_correct": False}
+                out.setdefault("pinned", {"error": repr(e), "verdicts_correct": False})
+                out["pageable"] = out.get("pageable", {"error": repr(e), "verdicts_correct": False})
             finally:
                 if dist is not None:
                     import torch
                     torch.cuda.set_device(dev_index)  # the members' threads ran on the other devices
+            return out
 
         t = time.time()
-        g = shard.on_rank0(leg, dist, "nhip_group_stream_done")
+        legs = shard.on_rank0(leg, dist, "nhip_group_stream_done")
         if rank == 0:
+            g, gp = legs["pinned"], legs["pageable"]
             res["group_stream"] = g
-            if "pcie_inclusive" in res and "value" in g:
-                g["vs_pcie_inclusive"] = g["value"] / res["pcie_inclusive"]["value"]
-            correct = correct and g["verdicts_correct"]
-            log(f"[group] {g.get('value', 0):.0f} proofs/s over {world} GPU(s) ({time.time() - t:.1f}s)")
+            res["group_stream_pageable"] = gp
+            for x in (g, gp):
+                if "pcie_inclusive" in res and "value" in x:
+                    x["vs_pcie_inclusive"] = x["value"] / res["pcie_inclusive"]["value"]
+            if "value" in g and "value" in gp:
+                gp["vs_pinned"] = gp["value"] / g["value"]
+            correct = correct and g["verdicts_correct"] and gp["verdicts_correct"]
+            log(f"[group] {g.get('value', 0):.0f} proofs/s pinned, {gp.get('value', 0):.0f} pageable, over {world} "
+                f"GPU(s) ({time.time() - t:.1f}s)")
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()

@@ -169,6 +169,9 @@ typedef struct {
     /* the same hash launches' own durations (dispatch begin / end timestamps of each launch, as the
      * rocprofv3 kernel trace reports them), summed: ms_mp_hash_kernel minus the gaps between them */
     double ms_mp_hash_exec;
+    /* the row-hashing launch's own duration (k_hash_rows: every revealed main / aux / quotient row's
+     * hash_varlen; dispatch begin / end timestamps) */
+    double ms_row_hash_exec;
 } nhip_stats;
 
 typedef struct nhip_air nhip_air;
@@ -196,6 +199,30 @@ int nhip_host_alloc(size_t bytes, void **out);
 int nhip_host_free(void *p);
 int nhip_host_register(void *p, size_t bytes);
 int nhip_host_unregister(void *p);
+/* ---- host topology of the feed path (NUMA) -------------------------------------------------
+ * The receive path of a node feeding GPU ctx: pinned memory whose pages lie on the NUMA node of
+ * ctx's GPU (the socket its PCIe link ends at).  A proof deserialized into it is DMA'd as it lies
+ * (no staging copy, no inter-socket traffic); free with nhip_host_free.  Falls back to unplaced
+ * pinned memory when the platform reports no node.  Replaces the `Vec<BFieldElement>` a peer
+ * message is decoded into (peer_loop.rs:315-323, state/mod.rs:2226-2272). */
+int nhip_host_alloc_near(nhip_ctx *ctx, size_t bytes, void **out);
+/* The NUMA node of ctx's GPU (-1: none reported) and that node's CPUs this process may use, read
+ * from sysfs through the device's PCI bus id.  The context's pinned staging is placed on that node
+ * and its staging copy threads are bound to those CPUs (NHIP_NUMA=0 disables both).  cpus may be
+ * NULL (count query). */
+int nhip_device_numa(nhip_ctx *ctx, int *numa_node, int *cpus, size_t cpu_cap, size_t *n_cpus);
+/* The same lookup under another sysfs root (host-only, no GPU: tests use fixture trees) for a PCI
+ * bus id "dddd:bb:dd.f": <root>/bus/pci/devices/<id>/numa_node, then
+ * <root>/devices/system/node/node<N>/cpulist. */
+int nhip_numa_from_sysfs(const char *sysfs_root, const char *pci_bus_id, int *numa_node, int *cpus, size_t cpu_cap,
+                         size_t *n_cpus);
+/* Parse a kernel cpulist ("0-3,8,10-15:2") into sorted CPU ids (host-only). */
+int nhip_cpulist_parse(const char *list, int *cpus, size_t cpu_cap, size_t *n_cpus);
+/* The NUMA node holding the page at ptr (-1 if unknown; host-only). */
+int nhip_host_page_node(const void *ptr);
+/* Staging copy threads per upload for this context (0 = default: up to 16, at most its NUMA
+ * node's CPUs).  A group sets each member's share of its node's CPUs. */
+int nhip_set_host_threads(nhip_ctx *ctx, unsigned threads);
 /* One-shot: upload, decode (on the device), verify, verdicts[n]. */
 int nhip_verify_batch(nhip_ctx *ctx, nhip_air *air, const nhip_stark_params *params, const nhip_claim *claims,
                       const nhip_proof *proofs, size_t n, uint8_t *verdicts, nhip_stats *stats);

@@ -6,6 +6,7 @@
 // tokio tasks: neptune-core/src/protocol/proof_abstractions/verifier.rs:60-63).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <mutex>
 #include <new>
@@ -13,6 +14,7 @@
 
 #include "../../include/neptune_hip.h"
 #include "device_scope.hpp"
+#include "host_numa.hpp"
 #include "kernels.hpp"
 
 struct nhip_ctx {
@@ -30,6 +32,8 @@ struct nhip_ctx {
     std::vector<hipEvent_t> free_events;
     double timed_ms = 0.0;
     uint64_t timed_launches = 0;
+    nhip::HostTopo topo;       // the GPU's NUMA node and its CPUs (host_numa.cpp)
+    unsigned host_threads = 0;  // staging copy threads per upload (0: the default)
 };
 
 namespace {
@@ -136,7 +140,10 @@ bool is_pow2(size_t n) { return n >= 2 && (n & (n - 1)) == 0; }
 extern "C" {
 
 // 2000: nhip_stark_params.input_form (the struct grew), nhip_set_fs_form, the streaming group
-int nhip_abi_version(void) { return 2000; }
+// 2100: nhip_stats.ms_row_hash_exec (the struct grew), the NUMA entry points (nhip_host_alloc_near,
+// nhip_device_numa, nhip_numa_from_sysfs, nhip_cpulist_parse, nhip_host_page_node,
+// nhip_set_host_threads)
+int nhip_abi_version(void) { return 2100; }
 
 int nhip_set_fs_form(int form) { return nhip::set_fs_form(form) == 0 ? NHIP_OK : NHIP_ERR_ARG; }
 
@@ -175,6 +182,11 @@ int nhip_init(uint32_t device_mask, nhip_ctx** out) {
     if (!ok) {
         delete c;
         return NHIP_ERR_HIP;
+    }
+    try {
+        c->topo = nhip::device_topo(dev);
+    } catch (const std::bad_alloc&) {
+        c->topo = nhip::HostTopo{};
     }
     *out = c;
     return NHIP_OK;
@@ -222,12 +234,33 @@ void* nhip_internal_staging(nhip_ctx* c, size_t bytes) {
     // headroom, at least doubling: hipHostFree waits for the device, so a context whose batches
     // vary in size should stop reallocating after a few calls
     const size_t want = std::max(bytes + bytes / 4, 2 * have);
-    if (hipHostMalloc(&c->staging, want, hipHostMallocDefault) != hipSuccess) {
+    // on the GPU's NUMA node: the copy threads (bound there) write it and the DMA reads it locally
+    if (nhip::host_malloc_on(&c->staging, want, c->topo.numa_node, hipHostMallocDefault) != hipSuccess) {
         c->staging = nullptr;
         return nullptr;
     }
     c->staging_bytes = want;
     return c->staging;
+}
+
+const void* nhip_internal_topo(nhip_ctx* c) { return &c->topo; }  // a const nhip::HostTopo*
+unsigned nhip_internal_host_threads(nhip_ctx* c) { return c->host_threads; }
+void nhip_internal_set_host_threads(nhip_ctx* c, unsigned n) { c->host_threads = n; }
+
+int nhip_device_numa(nhip_ctx* c, int* numa_node, int* cpus, size_t cpu_cap, size_t* n_cpus) {
+    if (!c || !numa_node) return NHIP_ERR_ARG;
+    *numa_node = c->topo.numa_node;
+    if (n_cpus) *n_cpus = c->topo.cpus.size();
+    if (cpus)
+        for (size_t i = 0; i < std::min(cpu_cap, c->topo.cpus.size()); ++i) cpus[i] = c->topo.cpus[i];
+    return NHIP_OK;
+}
+
+int nhip_set_host_threads(nhip_ctx* c, unsigned threads) {
+    if (!c || threads > 256) return NHIP_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->host_threads = threads;
+    return NHIP_OK;
 }
 
 // ------------------------------------------------------------------ device-resident form

@@ -24,10 +24,43 @@
 #include <vector>
 
 #include "../../include/neptune_hip.h"
+#include "host_numa.hpp"
 
 struct nhip_group {
     std::vector<nhip_ctx*> members;
+    std::vector<std::vector<int>> cpus;  // per member: its GPU's NUMA-node CPUs (empty: unknown)
 };
+
+// Each member's host work on its GPU's NUMA node: the member threads a group starts are bound to
+// the node's CPUs, and the node's CPUs are divided among the members on it for their staging copy
+// threads (8 GPUs on two sockets: 4 members share a socket's cores instead of 8 x 16 unbound
+// threads contending for them).
+static void place_members(nhip_group* g) {
+    const size_t M = g->members.size();
+    g->cpus.assign(M, {});
+    std::vector<int> node(M, -1);
+    for (size_t m = 0; m < M; ++m) {
+        size_t n = 0;
+        int nd = -1;
+        if (nhip_device_numa(g->members[m], &nd, nullptr, 0, &n) != NHIP_OK) continue;
+        node[m] = nd;
+        g->cpus[m].resize(n);
+        size_t got = 0;
+        (void)nhip_device_numa(g->members[m], &nd, g->cpus[m].data(), n, &got);
+        g->cpus[m].resize(std::min(n, got));
+    }
+    for (size_t m = 0; m < M; ++m) {
+        if (node[m] < 0 || g->cpus[m].empty()) continue;
+        size_t sharing = 0;
+        for (size_t q = 0; q < M; ++q) sharing += node[q] == node[m] ? 1 : 0;
+        const size_t per = std::max<size_t>(1, g->cpus[m].size() / std::max<size_t>(1, sharing));
+        (void)nhip_set_host_threads(g->members[m], (unsigned)std::min<size_t>(16, per));
+    }
+}
+
+static void bind_member_thread(const nhip_group* g, size_t m) {
+    if (m < g->cpus.size()) (void)nhip::bind_thread(g->cpus[m]);
+}
 
 extern "C" {
 
@@ -54,6 +87,11 @@ int nhip_group_create(const int* devices, size_t n_devices, nhip_group** out) {
             return rc;
         }
         g->members.push_back(c);
+    }
+    try {
+        place_members(g);
+    } catch (const std::bad_alloc&) {
+        g->cpus.clear();  // unplaced: still correct
     }
     *out = g;
     return NHIP_OK;
@@ -143,7 +181,10 @@ int nhip_group_verify_batch(nhip_group* g, nhip_air* air, const nhip_stark_param
         for (size_t m = 1; m < M; ++m) {
             if (idx[m].empty()) continue;
             try {
-                threads.emplace_back(run, m);
+                threads.emplace_back([&, m] {
+                    bind_member_thread(g, m);
+                    run(m);
+                });
             } catch (const std::system_error&) {
                 inline_members.push_back(m);
             } catch (const std::bad_alloc&) {
@@ -216,7 +257,10 @@ struct nhip_group_stream {
         inline_k.reserve(who.size());
         for (size_t k = 1; k < who.size(); ++k) {
             try {
-                th.emplace_back([&, k] { rcs[k] = f(who[k]); });
+                th.emplace_back([&, k] {
+                    bind_member_thread(g, who[k]);
+                    rcs[k] = f(who[k]);
+                });
             } catch (const std::system_error&) {
                 inline_k.push_back(k);
             }

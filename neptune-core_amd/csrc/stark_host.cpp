@@ -10,6 +10,8 @@
 // neptune_proof.rs:118-133 empty / all-zero proofs) must come out as `false`.
 #include <hip/hip_runtime.h>
 
+#include <emmintrin.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -24,6 +26,7 @@
 
 #include "../../include/neptune_hip.h"
 #include "device_scope.hpp"
+#include "host_numa.hpp"
 #include "../../include/nhip_challenge_id.h"
 #include "goldilocks.hpp"
 #include "kernels.hpp"
@@ -67,6 +70,40 @@ void encode_claim(const nhip_claim& claim, bool mont, uint64_t* c) {
     for (size_t i = 0; i < claim.input_len; ++i) *c++ = canon(claim.input[i]);
     *c++ = len(claim.version);
     for (int i = 0; i < 5; ++i) *c++ = canon(claim.program_digest[i]);
+}
+
+// The staging copy of a proof (pageable caller memory -> pinned staging) with non-temporal
+// stores: the staging is written once and read only by the DMA engine, so ordinary stores would
+// first read every destination line into the cache (a read-for-ownership) and then evict it: one
+// more host-DRAM pass per proof byte.  The feed path's host bandwidth is what an 8-GPU node runs
+// out of first, so the copy streams: 8-byte head to 16-byte alignment, 64-byte
+// blocks of four 16-byte streaming stores, then the tail.  The caller fences (_mm_sfence) before
+// the DMA of the chunk is issued.  NHIP_STAGE_NT=0: plain memcpy (A/B).
+static bool stage_nt() {
+    static const bool on = [] {
+        const char* v = std::getenv("NHIP_STAGE_NT");
+        return !v || std::strtol(v, nullptr, 10) != 0;
+    }();
+    return on;
+}
+static void copy_words_nt(uint64_t* dst, const uint64_t* src, size_t words) {
+    if (((uintptr_t)dst & 15u) && words) {
+        *dst++ = *src++;
+        --words;
+    }
+    __m128i* d = (__m128i*)dst;
+    const __m128i* sv = (const __m128i*)src;
+    size_t blocks = words / 8;
+    for (; blocks; --blocks, d += 4, sv += 4) {
+        const __m128i a = _mm_loadu_si128(sv), b = _mm_loadu_si128(sv + 1), c = _mm_loadu_si128(sv + 2),
+                      e = _mm_loadu_si128(sv + 3);
+        _mm_stream_si128(d, a);
+        _mm_stream_si128(d + 1, b);
+        _mm_stream_si128(d + 2, c);
+        _mm_stream_si128(d + 3, e);
+    }
+    const size_t done = words / 8 * 8;
+    for (size_t i = done; i < words; ++i) dst[i] = src[i];
 }
 
 // Host threads for staging copies (NHIP_HOST_THREADS overrides; at most 16, the GPU box's CPU
@@ -186,6 +223,7 @@ struct nhip_batch {
     } ph{};
     double stage_ms = 0, upload_ms = 0;
     double mp_hash_exec_ms = 0;  // summed dispatch durations of the hash launches
+    double row_hash_exec_ms = 0;  // the row-hashing launch's dispatch duration
     uint64_t merkle_perms = 0;
     std::vector<uint64_t> mp_cap;  // multiproof op capacity per level
 };
@@ -196,6 +234,9 @@ extern "C" int nhip_internal_device(nhip_ctx* c);
 extern "C" std::mutex* nhip_internal_mutex(nhip_ctx* c);
 extern "C" void* nhip_internal_staging(nhip_ctx* c, size_t bytes);
 extern "C" void* nhip_internal_verify_scratch(nhip_ctx* c, void* (*make)(), void (*freefn)(void*));
+extern "C" const void* nhip_internal_topo(nhip_ctx* c);
+extern "C" unsigned nhip_internal_host_threads(nhip_ctx* c);
+static const nhip::HostTopo& ctx_topo(nhip_ctx* c) { return *(const nhip::HostTopo*)nhip_internal_topo(c); }
 
 namespace {
 
@@ -779,20 +820,35 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
                 for (size_t q = cut[c]; q < cut[c + 1]; ++q) chunk_of[q] = c;
             }
             std::atomic<size_t> next{0};
+            const bool nt = stage_nt() && stage != pageable.data();
             auto work = [&]() {
                 for (size_t q; (q = next.fetch_add(1)) < todo.size();) {
                     const size_t i = todo[q];
-                    std::memcpy(stage + pin[i].off, proofs[i].words, proofs[i].len * 8);
+                    if (nt) {
+                        copy_words_nt(stage + pin[i].off, proofs[i].words, proofs[i].len);
+                        _mm_sfence();  // the streaming stores are globally visible before the chunk is released
+                    } else {
+                        std::memcpy(stage + pin[i].off, proofs[i].words, proofs[i].len * 8);
+                    }
                     left[chunk_of[q]].fetch_sub(1, std::memory_order_release);
                 }
             };
             std::vector<std::thread> pool;
-            const unsigned threads = host_threads(staged_bytes);
+            // copy threads on the CPUs of the GPU's NUMA node, where the staging lives (host_numa.cpp):
+            // at most that node's CPUs, or the count set by nhip_set_host_threads (a group divides a
+            // node's CPUs among the members on it)
+            const nhip::HostTopo& topo = ctx_topo(ctx);
+            unsigned threads = host_threads(staged_bytes);
+            if (const unsigned set = nhip_internal_host_threads(ctx); set && threads > 1) threads = set;
+            if (!topo.cpus.empty() && nhip::numa_enabled()) threads = std::min<unsigned>(threads, (unsigned)topo.cpus.size());
             if (threads > 1 && stage != pageable.data()) {
                 pool.reserve(threads);
                 for (unsigned t = 0; t < threads; ++t) {
                     try {
-                        pool.emplace_back(work);
+                        pool.emplace_back([&]() {
+                            (void)nhip::bind_thread(topo.cpus);
+                            work();
+                        });
                     } catch (const std::system_error&) {
                         break;  // fewer threads: the running ones (and this one, below) take the rest
                     }
@@ -1085,6 +1141,11 @@ static int launch_resources(nhip_batch* b) {
                     for (uint32_t j = 0; j < 2 * MAX_HASH_LAUNCHES; ++j) b->tm.lev[j] = nullptr;
                     break;  // untimed hash launches: a fault of the timing only
                 }
+            if (NHIP_HASH_LAUNCH_EVENTS && (hipEventCreate(&b->tm.rev[0]) != hipSuccess ||
+                                            hipEventCreate(&b->tm.rev[1]) != hipSuccess)) {
+                if (b->tm.rev[0]) (void)hipEventDestroy(b->tm.rev[0]);
+                b->tm.rev[0] = b->tm.rev[1] = nullptr;  // an untimed row launch
+            }
             if (hipStreamCreateWithFlags(&b->main, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
             if (hipStreamCreateWithFlags(&b->aux, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
         }
@@ -1165,6 +1226,8 @@ int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* al
             if (hipEventElapsedTime(&ms, b->tm.lev[2 * i], b->tm.lev[2 * i + 1]) == hipSuccess) exec += ms;
         }
         b->mp_hash_exec_ms = exec;
+        float rms = 0.f;
+        b->row_hash_exec_ms = b->tm.rev[0] && hipEventElapsedTime(&rms, b->tm.rev[0], b->tm.rev[1]) == hipSuccess ? rms : 0.0;
     }
     b->H.perms_static = cnt[CNT_PERMS_STATIC];
     b->H.perms_lcw = cnt[CNT_PERMS_LCW];
@@ -1222,6 +1285,7 @@ int nhip_batch_stats(const nhip_batch* b, nhip_stats* s) {
     s->ms_device_total = b->ph.total;
     s->ms_device_decode = b->ph.decode;
     s->ms_mp_hash_exec = b->mp_hash_exec_ms;
+    s->ms_row_hash_exec = b->row_hash_exec_ms;
     s->tip5_perms_static = b->H.perms_static;
     s->tip5_perms_merkle = b->merkle_perms;
     // every Merkle hash launch (k_mp_hash + the 16-lane-row k_mp_hash_wide): back to back on the
@@ -1272,6 +1336,8 @@ void nhip_batch_destroy(nhip_batch* b) {
         for (int i = 0; i < STARK_EVENTS; ++i) (void)hipEventDestroy(b->tm.ev[i]);
         for (uint32_t i = 0; i < 2 * MAX_HASH_LAUNCHES; ++i)
             if (b->tm.lev[i]) (void)hipEventDestroy(b->tm.lev[i]);
+        for (hipEvent_t e : b->tm.rev)
+            if (e) (void)hipEventDestroy(e);
     }
     if (b->main) (void)hipStreamDestroy(b->main);
     if (b->aux) (void)hipStreamDestroy(b->aux);
@@ -1286,6 +1352,23 @@ int nhip_host_alloc(size_t bytes, void** out) {
     *out = nullptr;
     void* p = nullptr;
     if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return NHIP_ERR_OOM;
+    try {
+        std::lock_guard<std::mutex> g(pinned().mu);
+        pinned().r.emplace_back((uintptr_t)p, bytes);
+    } catch (const std::bad_alloc&) {
+        (void)hipHostFree(p);
+        return NHIP_ERR_OOM;
+    }
+    *out = p;
+    return NHIP_OK;
+}
+
+int nhip_host_alloc_near(nhip_ctx* ctx, size_t bytes, void** out) {
+    if (!ctx || !out) return NHIP_ERR_ARG;
+    *out = nullptr;
+    void* p = nullptr;
+    if (nhip::host_malloc_on(&p, bytes ? bytes : 1, ctx_topo(ctx).numa_node, hipHostMallocPortable) != hipSuccess)
+        return NHIP_ERR_OOM;
     try {
         std::lock_guard<std::mutex> g(pinned().mu);
         pinned().r.emplace_back((uintptr_t)p, bytes);

@@ -352,6 +352,110 @@ __global__ void __launch_bounds__(256, NHIP_ROWS_WAVES) k_hash_rows(const uint64
     }
 }
 
+// The same hashing with each wave's row words staged through LDS (round 5).  k_hash_rows gives
+// every lane its own row, so one load instruction of a wave touches 64 rows 3 KB apart (64 cache
+// lines, 8 bytes used of each per instruction) and the 80-byte chunks of a row straddle lines that
+// are evicted between chunks: the round-4 PMC pass counted 1.5x the row bytes fetched, waves
+// waiting 69% of their cycles.  Here a wave fetches chunk c of its 64 rows with five
+// global_load_lds_dwordx4 (each 16-byte piece P = 64 i + lane is part P % 5 of row P / 5, so ten
+// lanes read one row's 80 bytes back to back), the pieces landing lane-linear in the wave's 5 KB
+// LDS slice = row-major [64][10] words; each lane then reads its row's 10 words (ds_read at stride
+// 80 B: the 16 lanes of a b128 group start on 16 distinct 4-bank groups, conflict-free).  Chunk
+// c + 1 is requested right after chunk c is read, so its fetch runs under chunk c's permutation
+// (no VGPRs hold it: the DMA writes LDS).  The words and the sponge are k_hash_rows's, so every
+// digest is bit-identical.  NHIP_ROWS_LDS=1 selects it (A/B only: measured slower).
+typedef __attribute__((address_space(3))) void lds_void_t;
+static constexpr uint32_t ROWS_PIECES = TIP5_RATE / 2;  // 16-byte pieces per row chunk
+// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
+static constexpr int WAIT_VMCNT0 = 0x0F70, WAIT_LGKMCNT0 = 0xC07F;
+template <bool MW>
+__global__ void __launch_bounds__(256, NHIP_ROWS_WAVES)
+    k_hash_rows_lds(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc, uint32_t n_proofs,
+                    uint32_t k, StarkDims dims, uint64_t* __restrict__ dig, const uint32_t* __restrict__ fail) {
+    __shared__ Tip5Lds lds;
+    __shared__ __attribute__((aligned(16))) uint64_t rowbuf[4][64 * TIP5_RATE];
+    // per wave: each lane's row offset (~0: none) and digest slot, in LDS rather than registers so
+    // nothing but the sponge state is live across a permutation (84 VGPRs, 5 waves, no scratch)
+    __shared__ uint64_t rowbase[4][64], rowdig[4][64];
+    tip5_lds_init(lds);
+    const uint32_t tree = blockIdx.y;
+    const uint32_t width = tree == 0 ? dims.num_main : (tree == 1 ? 3 * dims.num_aux : 3 * dims.num_quot_seg);
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    uint64_t* const buf = rowbuf[wv];
+    const uint64_t rows = (uint64_t)n_proofs * k;
+    const uint32_t nchunks = width / TIP5_RATE + 1;
+    for (uint64_t tw = (uint64_t)blockIdx.x * blockDim.x + 64u * wv; tw < rows; tw += (uint64_t)gridDim.x * blockDim.x) {
+        {
+            const uint64_t t = tw + lane;
+            uint64_t base = ~0ull, o = 0;  // ~0: no row (past the end, or a failed proof)
+            if (t < rows) {
+                const uint32_t p = (uint32_t)(t / k), j = (uint32_t)(t % k);
+                if (!fail[p]) {
+                    const ProofDesc& d = desc[p];
+                    base = (tree == 0 ? d.main_rows_off : (tree == 1 ? d.aux_rows_off : d.quot_rows_off)) +
+                           (uint64_t)j * width;
+                    o = (((uint64_t)p * 3 + tree) * k + j) * 5;
+                }
+            }
+            rowbase[wv][lane] = base;
+            rowdig[wv][lane] = o;
+            __builtin_amdgcn_wave_barrier();
+        }
+        // request chunk c of the wave's 64 rows into buf (pieces past a row's last word are skipped;
+        // a piece holding the last word of an odd remainder reads one word past the row: the word
+        // buffer always has words after the rows, the claims and an 8-byte pad)
+        auto request = [&](uint32_t c) {
+            const uint32_t pos = c * TIP5_RATE;
+            const uint32_t rem = min(width - pos, (uint32_t)TIP5_RATE);
+            // the piece indices recomputed per chunk from an opaque copy of the lane id: hoisted out
+            // of the chunk loop they would hold ten more VGPRs across every permutation
+            uint32_t ln = lane;
+            asm volatile("" : "+v"(ln));
+#pragma unroll
+            for (uint32_t i = 0; i < ROWS_PIECES; ++i) {
+                const uint32_t P = i * 64u + ln, r = (P * 13108u) >> 16, part = P - ROWS_PIECES * r;  // P / 5 for P < 320
+                const uint64_t rb = rowbase[wv][r];
+                if (rb != ~0ull && 2 * part < rem)
+                    __builtin_amdgcn_global_load_lds((const void*)(words + rb + pos + 2 * part), (lds_void_t*)(buf + i * 128u),
+                                                     16, 0, 0);
+            }
+        };
+        uint64_t s[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) s[q] = 0;
+        request(0);
+        for (uint32_t c = 0; c < nchunks; ++c) {
+            const uint32_t pos = c * TIP5_RATE;
+            const bool last = c + 1 == nchunks;
+            __builtin_amdgcn_s_waitcnt(WAIT_VMCNT0);  // chunk c has landed (hipcc does not count LDS-DMA)
+            const uint64_t* mine = buf + lane * TIP5_RATE;
+            if (!last) {
+#pragma unroll
+                for (int q = 0; q < TIP5_RATE; ++q) s[q] = word_mont<MW>(mine[q]);
+            } else {
+                const uint32_t rem = width - pos;
+#pragma unroll
+                for (int q = 0; q < TIP5_RATE; ++q) {
+                    const uint32_t qq = (uint32_t)q;
+                    s[q] = qq < rem ? word_mont<MW>(mine[q]) : (qq == rem ? MONT_ONE : 0ull);
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(WAIT_LGKMCNT0);  // the reads are done before the buffer is refilled
+            if (!last) request(c + 1);                  // fetched under this chunk's permutation
+            tip5_rounds_0_3(s, lds.lut);
+            tip5_last_sbox(s, lds.lut);
+            if (!last) tip5_last_mds<10, 16>(s);
+            else tip5_last_mds<0, 5>(s);
+        }
+        if (rowbase[wv][lane] != ~0ull) {
+            uint64_t* __restrict__ o = dig + rowdig[wv][lane];
+#pragma unroll
+            for (int q = 0; q < 5; ++q) o[q] = s[q];
+        }
+        __builtin_amdgcn_wave_barrier();  // every lane's reads of rowbase / rowdig precede the next writes
+    }
+}
+
 // ------------------------------------------------------------------ workgroup helpers
 __device__ __forceinline__ void hash_pair_raw(const uint64_t* l, const uint64_t* r, uint64_t* out,
                                               const uint8_t* __restrict__ lut) {
@@ -1654,7 +1758,17 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
         const uint64_t rows = (uint64_t)n * k;
         unsigned gx = (unsigned)((rows + 255) / 256);
         if (gx > 16384) gx = 16384;
-        hipLaunchKernelGGL(k_hash_rows<MW>, dim3(gx, 3), dim3(256), 0, st, b.words, b.desc, n, k, b.dims, b.dig, b.fail);
+        static const bool rows_lds = [] {  // NHIP_ROWS_LDS=1: the LDS-staged row loads (A/B, measured slower)
+            const char* v = std::getenv("NHIP_ROWS_LDS");
+            return v && std::strtoul(v, nullptr, 10) != 0;
+        }();
+        // dispatch begin / end events (the row kernel's own duration, as the kernel trace has it)
+        if (rows_lds)
+            hipExtLaunchKernelGGL(k_hash_rows_lds<MW>, dim3(gx, 3), dim3(256), 0, st, tm->rev[0], tm->rev[1], 0, b.words,
+                                  b.desc, n, k, b.dims, b.dig, b.fail);
+        else
+            hipExtLaunchKernelGGL(k_hash_rows<MW>, dim3(gx, 3), dim3(256), 0, st, tm->rev[0], tm->rev[1], 0, b.words,
+                                  b.desc, n, k, b.dims, b.dig, b.fail);
     }
     mark(2, st);
     if (small) {

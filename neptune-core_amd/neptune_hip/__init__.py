@@ -73,6 +73,15 @@ class DeviceBuffer:
         return out
 
 
+def numa_of(lib, ctx_handle) -> dict:
+    node, n = ctypes.c_int(-1), ctypes.c_size_t(0)
+    check(lib.nhip_device_numa(ctx_handle, ctypes.byref(node), None, 0, ctypes.byref(n)), "nhip_device_numa")
+    cpus = (ctypes.c_int * max(1, n.value))()
+    got = ctypes.c_size_t(0)
+    check(lib.nhip_device_numa(ctx_handle, ctypes.byref(node), cpus, n.value, ctypes.byref(got)), "nhip_device_numa")
+    return {"node": node.value, "cpus": list(cpus[:min(n.value, got.value)])}
+
+
 class Context:
     """One GPU (one process per GPU).  Wraps an ``nhip_ctx``."""
 
@@ -185,6 +194,11 @@ class Context:
         return bool(ok.value)
 
     # ------------------------------------------------------------ timing
+    def numa(self) -> dict:
+        """The NUMA node of this context's GPU and that node's CPUs (nhip_device_numa): where its
+        pinned staging lives and where its staging copy threads run."""
+        return numa_of(self.lib, self.handle)
+
     def timing(self, on: bool = True):
         check(self.lib.nhip_timing_enable(self.handle, 1 if on else 0), "timing_enable")
 

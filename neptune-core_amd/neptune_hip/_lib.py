@@ -55,7 +55,8 @@ class Stats(ctypes.Structure):
                 ("ms_device_total", ctypes.c_double), ("ms_merkle_hash", ctypes.c_double),
                 ("merkle_hash_launches", ctypes.c_uint64), ("ms_mp_hash_kernel", ctypes.c_double),
                 ("mp_hash_kernel_launches", ctypes.c_uint64), ("mp_hash_kernel_perms", ctypes.c_uint64),
-                ("ms_device_decode", ctypes.c_double), ("ms_mp_hash_exec", ctypes.c_double)]
+                ("ms_device_decode", ctypes.c_double), ("ms_mp_hash_exec", ctypes.c_double),
+                ("ms_row_hash_exec", ctypes.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -134,6 +135,14 @@ SIGNATURES = {
     "nhip_host_alloc": ([_sz, ctypes.POINTER(_vp)], ctypes.c_int),
     "nhip_host_free": ([_vp], ctypes.c_int),
     "nhip_host_register": ([_vp, _sz], ctypes.c_int),
+    "nhip_host_alloc_near": ([_vp, _sz, ctypes.POINTER(_vp)], ctypes.c_int),
+    "nhip_device_numa": ([_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), _sz,
+                          ctypes.POINTER(_sz)], ctypes.c_int),
+    "nhip_numa_from_sysfs": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int),
+                              ctypes.POINTER(ctypes.c_int), _sz, ctypes.POINTER(_sz)], ctypes.c_int),
+    "nhip_cpulist_parse": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), _sz, ctypes.POINTER(_sz)], ctypes.c_int),
+    "nhip_host_page_node": ([_vp], ctypes.c_int),
+    "nhip_set_host_threads": ([_vp, ctypes.c_uint], ctypes.c_int),
     "nhip_host_unregister": ([_vp], ctypes.c_int),
     "nhip_pow_mast_commit": ([_vp, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "nhip_pow_preprocess": ([_vp, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,

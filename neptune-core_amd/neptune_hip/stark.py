@@ -306,12 +306,17 @@ class PinnedProofs:
     staged from them are DMA'd straight from this memory (no staging copy).  ``views`` are the
     proofs as numpy arrays over the pinned buffer."""
 
-    def __init__(self, proofs: Sequence[Sequence[int]]):
+    def __init__(self, proofs: Sequence[Sequence[int]], near=None):
+        """``near``: a Context whose GPU's NUMA node the buffer is placed on (nhip_host_alloc_near,
+        the receive path of a node feeding that GPU); None: nhip_host_alloc."""
         self.lib = _lib.load()
         arrs = [np.asarray(p, dtype=np.uint64) for p in proofs]
         total = sum(a.size for a in arrs)
         h = ctypes.c_void_p()
-        check(self.lib.nhip_host_alloc(max(total, 1) * 8, ctypes.byref(h)), "nhip_host_alloc")
+        if near is not None:
+            check(self.lib.nhip_host_alloc_near(near.handle, max(total, 1) * 8, ctypes.byref(h)), "nhip_host_alloc_near")
+        else:
+            check(self.lib.nhip_host_alloc(max(total, 1) * 8, ctypes.byref(h)), "nhip_host_alloc")
         self.ptr = h.value
         buf = (ctypes.c_uint64 * max(total, 1)).from_address(self.ptr)
         self.flat = np.frombuffer(buf, dtype=np.uint64, count=max(total, 1))
@@ -350,6 +355,17 @@ class Group:
 
     def __len__(self) -> int:
         return int(self.lib.nhip_group_size(self.handle))
+
+    def numa(self) -> List[dict]:
+        """Per member: its GPU's NUMA node and CPUs (the member's threads and staging live there)."""
+        from . import numa_of
+        out = []
+        for i in range(len(self)):
+            h = self.lib.nhip_group_member(self.handle, i)
+            d = numa_of(self.lib, h)
+            d["device"] = int(self.lib.nhip_device_ordinal(h))
+            out.append(d)
+        return out
 
     def close(self):
         if self.handle:

@@ -9,7 +9,7 @@
 #![allow(non_camel_case_types)]
 #![no_std]
 
-use core::ffi::{c_char, c_int, c_void};
+use core::ffi::{c_char, c_int, c_uint, c_void};
 
 pub const NHIP_OK: c_int = 0;
 pub const NHIP_ERR_NO_DEVICE: c_int = 1;
@@ -90,6 +90,7 @@ pub struct nhip_stats {
     pub mp_hash_kernel_perms: u64,
     pub ms_device_decode: f64,
     pub ms_mp_hash_exec: f64,
+    pub ms_row_hash_exec: f64,
 }
 
 #[repr(C)]
@@ -191,6 +192,14 @@ extern "C" {
     pub fn nhip_host_alloc(bytes: usize, out: *mut *mut c_void) -> c_int;
     pub fn nhip_host_free(p: *mut c_void) -> c_int;
     pub fn nhip_host_register(p: *mut c_void, bytes: usize) -> c_int;
+    pub fn nhip_host_alloc_near(ctx: *mut nhip_ctx, bytes: usize, out: *mut *mut c_void) -> c_int;
+    pub fn nhip_device_numa(ctx: *mut nhip_ctx, numa_node: *mut c_int, cpus: *mut c_int, cpu_cap: usize,
+                            n_cpus: *mut usize) -> c_int;
+    pub fn nhip_numa_from_sysfs(sysfs_root: *const c_char, pci_bus_id: *const c_char, numa_node: *mut c_int,
+                                cpus: *mut c_int, cpu_cap: usize, n_cpus: *mut usize) -> c_int;
+    pub fn nhip_cpulist_parse(list: *const c_char, cpus: *mut c_int, cpu_cap: usize, n_cpus: *mut usize) -> c_int;
+    pub fn nhip_host_page_node(ptr: *const c_void) -> c_int;
+    pub fn nhip_set_host_threads(ctx: *mut nhip_ctx, threads: c_uint) -> c_int;
     pub fn nhip_host_unregister(p: *mut c_void) -> c_int;
     pub fn nhip_verify_batch(ctx: *mut nhip_ctx, air: *mut nhip_air, params: *const nhip_stark_params,
                              claims: *const nhip_claim, proofs: *const nhip_proof, n: usize,

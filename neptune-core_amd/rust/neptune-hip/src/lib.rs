@@ -265,9 +265,128 @@ impl GpuNode {
     }
 }
 
+impl GpuNode {
+    /// (NUMA node, CPUs) of member `i`'s GPU: where its staging lives and its copy threads run.
+    pub fn member_numa(&self, i: usize) -> Option<(i32, Vec<i32>)> {
+        let ctx = unsafe { sys::nhip_group_member(self.group, i) };
+        if ctx.is_null() {
+            return None;
+        }
+        let (mut node, mut n) = (-1i32, 0usize);
+        ok(unsafe { sys::nhip_device_numa(ctx, &mut node, ptr::null_mut(), 0, &mut n) }).ok()?;
+        let mut cpus = vec![0i32; n];
+        let mut got = 0usize;
+        ok(unsafe { sys::nhip_device_numa(ctx, &mut node, cpus.as_mut_ptr(), n, &mut got) }).ok()?;
+        cpus.truncate(got.min(n));
+        Some((node, cpus))
+    }
+
+    /// The batch's proofs from a [`ProofArena`] (pinned receive memory): DMA'd as they lie, no
+    /// staging copy.  `claims[i]` belongs to `arena.proof(i)`.
+    pub fn verify_arena(&self, claims: &[Claim], arena: &ProofArena) -> Result<(Vec<bool>, bool), GpuFault> {
+        if claims.len() != arena.len() {
+            return Err(GpuFault(sys::NHIP_ERR_ARG));
+        }
+        let mut cs = Vec::with_capacity(claims.len());
+        let mut ps = Vec::with_capacity(claims.len());
+        for (i, c) in claims.iter().enumerate() {
+            cs.push(sys::nhip_claim {
+                program_digest: raw_digest(&c.program_digest),
+                version: c.version,
+                input: raw_words(&c.input),
+                input_len: c.input.len(),
+                output: raw_words(&c.output),
+                output_len: c.output.len(),
+            });
+            let p = arena.proof(i);
+            ps.push(sys::nhip_proof { words: raw_words(p), len: p.len() });
+        }
+        let mut v = vec![0u8; claims.len()];
+        let mut all = 0u8;
+        ok(unsafe {
+            sys::nhip_group_verify_batch(self.group, self.air.0, &self.params, cs.as_ptr(), ps.as_ptr(), claims.len(),
+                                         v.as_mut_ptr(), &mut all)
+        })?;
+        Ok((v.into_iter().map(|b| b == 1).collect(), all == 1))
+    }
+}
+
 impl Drop for GpuNode {
     fn drop(&mut self) {
         unsafe { sys::nhip_group_destroy(self.group) }
+    }
+}
+
+/// Pinned receive memory for proofs, on the NUMA node of one GPU (`nhip_host_alloc_near`): the node
+/// decodes a peer's proof (`peer_loop.rs:315-323`, `state/mod.rs:2226-2272`) straight into it with
+/// [`ProofArena::push_with`] instead of into a `Proof`'s `Vec`, and the verifier DMAs it from there:
+/// no staging copy (the pageable path's host copy reads and writes every proof word once more on
+/// the host; DESIGN.md §6 budgets both).  Words are `BFieldElement`s as twenty-first keeps them
+/// (Montgomery), the form the crate's params declare.
+pub struct ProofArena {
+    base: *mut BFieldElement,
+    cap: usize,
+    used: usize,
+    spans: Vec<(usize, usize)>,
+}
+unsafe impl Send for ProofArena {}
+
+impl ProofArena {
+    /// `cap_words` words on the NUMA node of `node`'s member `member`.
+    pub fn new(node: &GpuNode, member: usize, cap_words: usize) -> Result<Self, GpuFault> {
+        let ctx = unsafe { sys::nhip_group_member(node.group, member) };
+        if ctx.is_null() {
+            return Err(GpuFault(sys::NHIP_ERR_ARG));
+        }
+        let mut p = ptr::null_mut();
+        ok(unsafe { sys::nhip_host_alloc_near(ctx, cap_words.max(1) * 8, &mut p) })?;
+        Ok(ProofArena { base: p as *mut BFieldElement, cap: cap_words, used: 0, spans: Vec::new() })
+    }
+
+    /// Reserve `len` words for the next proof and let `fill` write them (a deserializer); None when
+    /// the arena is full (verify what it holds, then [`ProofArena::clear`]).
+    pub fn push_with(&mut self, len: usize, fill: impl FnOnce(&mut [BFieldElement])) -> Option<usize> {
+        if self.cap - self.used < len {
+            return None;
+        }
+        // SAFETY: [used, used + len) lies inside the allocation and is not borrowed elsewhere
+        let dst = unsafe { std::slice::from_raw_parts_mut(self.base.add(self.used), len) };
+        fill(dst);
+        self.spans.push((self.used, len));
+        self.used += len;
+        Some(self.spans.len() - 1)
+    }
+
+    /// Copy a decoded proof in (when the decoder cannot write in place).
+    pub fn push(&mut self, proof: &Proof) -> Option<usize> {
+        self.push_with(proof.0.len(), |d| d.copy_from_slice(&proof.0))
+    }
+
+    pub fn proof(&self, i: usize) -> &[BFieldElement] {
+        let (at, len) = self.spans[i];
+        // SAFETY: a span handed out by push_with, inside the allocation
+        unsafe { std::slice::from_raw_parts(self.base.add(at), len) }
+    }
+
+    pub fn len(&self) -> usize {
+        self.spans.len()
+    }
+
+    pub fn is_empty(&self) -> bool {
+        self.spans.is_empty()
+    }
+
+    pub fn clear(&mut self) {
+        self.spans.clear();
+        self.used = 0;
+    }
+}
+
+impl Drop for ProofArena {
+    fn drop(&mut self) {
+        unsafe {
+            sys::nhip_host_free(self.base as *mut std::ffi::c_void);
+        }
     }
 }
 

@@ -314,30 +314,37 @@ def test_large_padded_heights_config5_shape(ctx):
 
 def test_config1_singleproof_gpu(ctx):
     """BASELINE config 1 substitute: one SingleProof-shaped proof at log2 padded
-    height 21 (seed 0xC1; claim input = a kernel MAST hash reversed, output empty) verified
-    through the GPU path: verdict and every Fiat-Shamir sample equal the oracle's; a mutated copy
-    and the un-reversed claim reject on both."""
-    import stark_prover_const as K
+    height 21 (tests/golden/config1.npz, the sparse synthetic prover: every one of the 15 FRI
+    rounds folds non-zero values, last polynomial of degree 122; claim input = a kernel MAST hash
+    reversed, output empty) verified through the GPU path: verdict and every Fiat-Shamir sample
+    equal the oracle transcript stored with the fixture; a mutated copy, a mutated last-round FRI
+    response and the un-reversed claim reject on the GPU as in the C oracle."""
+    import json
+    import coracle as C
     T.use_c_backend()
     NS = _ns()
     params = S.StarkParams()
-    air, recipe = S.synth_air(params, seed=1)
-    rng = np.random.default_rng(0xC1)
-    kernel_mast_hash = [int(x) for x in rng.integers(0, S.P, size=5, dtype=np.uint64)]
-    program_digest = [int(x) for x in rng.integers(0, S.P, size=5, dtype=np.uint64)]
-    claim = (program_digest, 0, kernel_mast_hash[::-1], [])
-    proof, _ = K.prove(params, air, recipe, claim, 21, seed=0xC1)
+    air, _ = S.synth_air(params, seed=1)
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "config1.npz"))
+    m = json.loads(bytes(z["meta"]).decode())
+    claim = (m["digest"], m["version"], m["input"], m["output"])
+    proof = [int(w) for w in z["proof"]]
+    samples = [tuple(int(c) for c in x) for x in z["samples"]]
+    indices = [int(i) for i in z["indices"]]
     mutated = list(proof)
     mutated[len(proof) // 2] = (mutated[len(proof) // 2] + 1) % S.P
-    cases = [(claim, proof), (claim, mutated), ((program_digest, 0, kernel_mast_hash, []), proof)]
+    late_fri = list(proof)
+    late_fri[len(proof) - 1000] = (late_fri[len(proof) - 1000] + 1) % S.P
+    unreversed = (m["digest"], m["version"], m["kernel_mast_hash"], m["output"])
+    cases = [(claim, proof), (claim, mutated), (claim, late_fri), (unreversed, proof)]
     b = NS.Batch(ctx, NS.Air(air.to_words()), NS.Stark.default(), [NS.Claim(*c) for c, _ in cases],
                  [p for _, p in cases])
     v, _ = b.run()
-    want = [S.verify(params, air, c, p) for c, p in cases]
-    assert [bool(x) for x in v] == want == [True, False, False]
-    ok_o, samples, indices = _oracle_samples(params, air, claim, proof)
+    want = [bool(x) for x in C.stark_verify_batch(air.to_words(), params, [c for c, _ in cases], [p for _, p in cases],
+                                                  threads=4)]
+    assert [bool(x) for x in v] == want and want[0] and not any(want[1:])
     xs, idx, fail = b.transcript(0)
-    assert ok_o and fail == 0 and xs == samples and idx == indices
+    assert fail == 0 and xs == samples and idx == indices
     b.close()
 
 
