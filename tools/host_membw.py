@@ -1,7 +1,12 @@
-"""Host DRAM bandwidth of the feed path's copy: T threads each memcpy a private slice of a large
-pageable source into a pinned destination (the staging copy of the pageable path), optionally
-bound to one NUMA node's CPUs.  Prints GB/s of copied bytes (each byte is read once and written
-once, so DRAM traffic is >= 2x that, 3x with write-allocate)."""
+"""Host DRAM bandwidth of the feed path's staging copy, with page placement controlled.
+
+T threads each copy a private slice of a large pageable source (a Vec's words) into pinned memory
+placed on the GPU's NUMA node (nhip_host_alloc_near: the context's staging).  The source pages are
+first-touched by threads bound to the GPU's node ("local") or to another node ("remote"); the copy
+threads run bound to the GPU's node or unbound.  Each byte copied is one DRAM read plus one DRAM
+write (plus a read-for-ownership of the destination for ordinary stores; numpy's copy is memcpy);
+the DMA engine then reads the staging once more.  Prints copied GB/s per case and the page nodes
+actually obtained (nhip_host_page_node), for the 8-GPU budget of DESIGN.md §6."""
 import ctypes
 import json
 import os
@@ -16,50 +21,81 @@ import neptune_hip as nh  # noqa: E402
 import neptune_hip._lib as L  # noqa: E402
 
 
-def run(threads, nbytes, cpus, reps=3):
-    lib = L.load()
-    src = np.ones(nbytes // 8, dtype=np.uint64)
-    h = ctypes.c_void_p()
-    L.check(lib.nhip_host_alloc(nbytes, ctypes.byref(h)), "nhip_host_alloc")
-    dst = np.frombuffer((ctypes.c_uint64 * (nbytes // 8)).from_address(h.value), dtype=np.uint64)
-    dst[:] = 0
-    per = (nbytes // 8) // threads
-    best = 0.0
-    for _ in range(reps):
-        bar = threading.Barrier(threads + 1)
+def node_cpus(n):
+    try:
+        with open(f"/sys/devices/system/node/node{n}/cpulist") as f:
+            lst = f.read().strip()
+    except OSError:
+        return []
+    out = []
+    for part in lst.split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            out += list(range(int(a), int(b) + 1))
+        elif part:
+            out.append(int(part))
+    allowed = os.sched_getaffinity(0)
+    return [c for c in out if c in allowed]
 
-        def work(i):
-            if cpus:
-                os.sched_setaffinity(0, cpus)
-            bar.wait()
-            np.copyto(dst[i * per:(i + 1) * per], src[i * per:(i + 1) * per])
-            bar.wait()
 
-        ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
-        for t in ts:
-            t.start()
+def parallel(threads, cpus, fn):
+    bar = threading.Barrier(threads + 1)
+
+    def work(i):
+        if cpus:
+            os.sched_setaffinity(0, cpus)
         bar.wait()
-        t0 = time.perf_counter()
+        fn(i)
         bar.wait()
-        dt = time.perf_counter() - t0
-        for t in ts:
-            t.join()
-        best = max(best, per * threads * 8 / dt)
-    lib.nhip_host_free(h.value)
-    return best / 1e9
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for t in ts:
+        t.start()
+    bar.wait()
+    t0 = time.perf_counter()
+    bar.wait()
+    dt = time.perf_counter() - t0
+    for t in ts:
+        t.join()
+    return dt
 
 
 def main():
+    lib = L.load()
     ctx = nh.Context(0)
     topo = ctx.numa()
-    ctx.close()
+    gnode = topo["node"]
+    nodes = sorted(int(d[4:]) for d in os.listdir("/sys/devices/system/node") if d.startswith("node") and d[4:].isdigit())
+    other = next((n for n in nodes if n != gnode and node_cpus(n)), None)
     nbytes = int(os.environ.get("MEMBW_BYTES", str(2 << 30)))
-    out = {"gpu_numa_node": topo["node"], "node_cpus": len(topo["cpus"]), "allowed_cpus": len(os.sched_getaffinity(0)),
-           "bytes": nbytes, "GBps_copied": {}}
-    for t in (1, 2, 4, 8, 16):
-        out["GBps_copied"][f"{t}_unbound"] = run(t, nbytes, None)
-        if topo["cpus"]:
-            out["GBps_copied"][f"{t}_bound"] = run(t, nbytes, topo["cpus"])
+    words = nbytes // 8
+    h = ctypes.c_void_p()
+    L.check(lib.nhip_host_alloc_near(ctx.handle, nbytes, ctypes.byref(h)), "nhip_host_alloc_near")
+    dst = np.frombuffer((ctypes.c_uint64 * words).from_address(h.value), dtype=np.uint64)
+    dst[:] = 0
+    out = {"gpu_numa_node": gnode, "numa_nodes": nodes, "gpu_node_cpus": len(topo["cpus"]),
+           "allowed_cpus": len(os.sched_getaffinity(0)), "bytes": nbytes,
+           "staging_page_node": lib.nhip_host_page_node(ctypes.c_void_p(h.value)), "cases": {}}
+    for where, touch_node in (("local", gnode), ("remote", other)):
+        if touch_node is None or touch_node < 0:
+            continue
+        src = np.empty(words, dtype=np.uint64)
+        per_t = words // 16
+        parallel(16, node_cpus(touch_node), lambda i: src[i * per_t:(i + 1) * per_t].fill(i + 1))
+        src_node = lib.nhip_host_page_node(ctypes.c_void_p(src.ctypes.data + nbytes // 2))
+        for threads in (4, 8, 16):
+            per = words // threads
+            for bound in (True, False):
+                cpus = node_cpus(gnode) if bound else None
+                best = 0.0
+                for _ in range(3):
+                    dt = parallel(threads, cpus,
+                                  lambda i: np.copyto(dst[i * per:(i + 1) * per], src[i * per:(i + 1) * per]))
+                    best = max(best, per * threads * 8 / dt / 1e9)
+                out["cases"][f"src_{where}(node {src_node})_{threads}t_{'bound' if bound else 'unbound'}"] = round(best, 1)
+        del src
+    lib.nhip_host_free(ctypes.c_void_p(h.value))
+    ctx.close()
     print(json.dumps(out))
 
 
