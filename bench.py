@@ -277,6 +277,27 @@ def make_batch(pool, collections: int, corrupt_frac: float, seed: int):
     return claims, proofs, np.array(expect, dtype=bool)
 
 
+def pipelined(batches, steps: int, inflight: int, expect):
+    """`steps` launches over resident `batches` (round robin), at most `inflight` in flight, each
+    wait followed at once by the next launch; returns (seconds, every verdict vector == expect)."""
+    ok = True
+    q, launched = [], 0
+    t = time.perf_counter()
+    for i in range(min(inflight, steps, len(batches))):
+        batches[i].launch()
+        q.append(i)
+        launched += 1
+    while q:
+        i = q.pop(0)
+        v, _ = batches[i].wait()
+        if launched < steps:
+            batches[i].launch()
+            q.append(i)
+            launched += 1
+        ok = ok and bool((np.asarray(v, dtype=bool) == expect).all())
+    return time.perf_counter() - t, ok
+
+
 def default_inflight(n: int) -> int:
     """Steps in flight for an n-proof batch per GPU: 8 from 1,024 proofs, 10 below (the N = 1 / 2 / 4
     / 8 shares of config 4; config 5's 8-64 proofs: 10 vs 8 in flight +10-11%, profiles/r03s).
@@ -749,6 +770,10 @@ def main():
     ap.add_argument("--config1-seconds", type=float, default=8.0,
                     help="config-1 single-proof latency leg: CPU-restatement time budget (0 = skip the leg)")
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
+    ap.add_argument("--product-steps", type=int, default=20,
+                    help="steps of the product-depth leg (2 in flight) after the timed region (0 = skip)")
+    ap.add_argument("--share-steps", type=int, default=20,
+                    help="config 4 at N = 1: timed steps of the N = 8 rank's 512-proof share (0 = skip)")
     ap.add_argument("--config5-proofs", type=int, default=64,
                     help="config-5 leg at N = 1: proofs at log2 padded height 23 (0 = skip)")
     ap.add_argument("--stream-batches", type=int, default=6,
@@ -799,6 +824,9 @@ def main():
     R = args.inflight or default_inflight(n)
     # before anything initialises HIP (nothing above has)
     want_q = hw_queues_wanted(R, world > 1)
+    if world == 1 and args.config == 4 and total == 4096 and args.share_steps > 0:
+        # the share_n8 leg runs the N = 8 rank's 512-proof share at its own depth in this process
+        want_q = max(want_q, hw_queues_wanted(default_inflight(total // 8), False))
     if os.environ.get("NHIP_BENCH_HWQ"):  # A/B runs: exactly this many
         os.environ["GPU_MAX_HW_QUEUES"] = os.environ["NHIP_BENCH_HWQ"]
     elif int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < want_q:
@@ -942,6 +970,18 @@ def main():
             for k, x in ring[0].stats().items():
                 acc_iso[k] = acc_iso.get(k, 0.0) + x
         iso_ms = (time.perf_counter() - t_iso) / iso_steps * 1e3
+
+    # the product's own pipeline depth beside the bench's: a queue or a group member keeps two
+    # batches in flight (two slots), with the library's recommended hardware queues enough for it
+    product = None
+    if world == 1 and R > 2 and args.product_steps > 0:
+        ctx.synchronize()
+        dt, ok2 = pipelined(ring, args.product_steps, 2, expect)
+        product = {"value": total * args.product_steps / dt, "unit": "proofs/s", "inflight": 2,
+                   "steps": args.product_steps, "ms_per_step": dt / args.product_steps * 1e3, "verdicts_correct": ok2,
+                   "measured": "the same resident batches, 2 in flight (nhip_queue / nhip_group_stream keep two "
+                               "slots per GPU), right after the timed region"}
+        correct = correct and ok2
 
     if dist is not None:
         import torch
@@ -1120,8 +1160,32 @@ def main():
     if bytes_step:
         res["hbm"].update({"pmc_bytes_per_step": bytes_step, "pmc_GBps": bytes_step / step_s / 1e9,
                            "pmc_frac": bytes_step / step_s / HBM_PEAK, "pmc_profile": bytes_tag})
+    if product is not None:
+        product["vs_value"] = product["value"] / res["value"]
+        res["product_pipeline"] = product
     for b in ring:
         b.close()
+    # the N = 8 rank's share on this GPU (rank 0 of 8's LPT shard of the same 4,096-proof job), in
+    # the same command's shape (its own ring, warm-up, `steps` timed steps): what each GPU of the
+    # driver's 8-GPU run does, measured on one
+    if world == 1 and args.config == 4 and total == 4096 and args.share_steps > 0:
+        sc, sp, se, _, _, _ = make_config4(pool4, total, 0.01, 8, 0)
+        scl, spr = device_form(sc, sp, mont)
+        sn = [NS.Claim(*c) for c in scl]
+        Rs = default_inflight(len(sp))
+        sring = [NS.Batch(ctx, gair, stark, sn, spr) for _ in range(Rs)]
+        pipelined(sring, args.warmup, Rs, se)
+        ctx.synchronize()
+        dt, ok3 = pipelined(sring, args.share_steps, Rs, se)
+        for b in sring:
+            b.close()
+        sh = {"proofs_per_step": len(sp), "inflight": Rs, "steps": args.share_steps, "warmup": args.warmup,
+              "value": len(sp) * args.share_steps / dt, "unit": "proofs/s (one GPU)",
+              "ms_per_step": dt / args.share_steps * 1e3, "verdicts_correct": ok3,
+              "measured": "rank 0 of 8's LPT shard of the 4,096-proof job, resident, the timed region's shape"}
+        sh["vs_value_per_proof"] = sh["value"] / res["value"]
+        res["share_n8"] = sh
+        correct = correct and ok3
     _assert_fracs(res)
     # the PCIe-inclusive leg and the config-2 microbench belong to the one-GPU report (N = 1): with
     # several ranks, rank 0 would run them alone while the others tear down

@@ -133,8 +133,11 @@ __global__ void __launch_bounds__(64) k_decode(const uint64_t* __restrict__ word
 // the two-row "pair" Tip5 (one proof per 32 lanes, PAIR = true: about a quarter fewer dependent
 // instructions per permutation again, at ~1.5x the lane-instructions; used for batches small
 // enough that the sponge replay is on the critical path with most SIMDs idle).  Both rows of a
-// pair hold the same state; only row 0 writes.
-template <bool PAIR, bool MW>
+// pair hold the same state; only row 0 writes.  LAT: the row form with the carry-light arithmetic
+// (mont_mul_lat / mds_reduce_ark_lat: a shorter dependent chain per permutation, more
+// instructions), for batches whose sponge replay sits on the critical path (A/B:
+// NHIP_FS_ROW_LAT_MAX).
+template <bool PAIR, bool MW, bool LAT = false>
 __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restrict__ words,
                                                         const ProofDesc* __restrict__ desc,
                                                         const FsOp* __restrict__ ops, uint32_t n_proofs,
@@ -156,7 +159,7 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
     for (int j = 0; j < 8; ++j) cm[j] = h ? TIP5_MDS[j + 8] : TIP5_MDS[j];
     auto permute = [&](uint64_t st) {
         if constexpr (PAIR) return tip5_permute_pair(st, e, h, rc, cm, lds.lut);
-        else return tip5_permute_wide<false>(st, e, rc, lds.lut);
+        else return tip5_permute_wide<LAT>(st, e, rc, lds.lut);
     };
     const bool writer = h == 0;
     const ProofDesc& d = desc[g];
@@ -1666,6 +1669,16 @@ static bool ood_wide(uint32_t n) {
     return n <= lim;
 }
 
+// row-form batches below this many proofs replay with the carry-light arithmetic (A/B knob
+// NHIP_FS_ROW_LAT_MAX; default 0 = never)
+static uint32_t fs_row_lat_max() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("NHIP_FS_ROW_LAT_MAX");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+    }();
+    return v;
+}
+
 // Fiat-Shamir replay form for an n-proof batch (see k_fs_replay_wide / k_fs_replay_quad):
 // 0 = 16-lane row, 1 = two-row pair, 2 = quad.  A forced form (nhip_set_fs_form: tests and A/B
 // runs; NHIP_FS_FORM=row|pair|quad sets the initial value, read once) overrides the size rule.
@@ -1742,6 +1755,9 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     else if (ff == FS_QUAD)
         hipLaunchKernelGGL(k_fs_replay_quad<MW>, dim3((n * 4 + quad_wg() - 1) / quad_wg()), dim3(quad_wg()), 0, sa, b.words, b.desc, b.ops, n,
                            b.xs, b.idx, b.fail);
+    else if (n < fs_row_lat_max())
+        hipLaunchKernelGGL((k_fs_replay_wide<false, MW, true>), dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words,
+                           b.desc, b.ops, n, b.xs, b.idx, b.fail);
     else
         hipLaunchKernelGGL((k_fs_replay_wide<false, MW>), dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
                            b.ops, n, b.xs, b.idx, b.fail);
