@@ -10,8 +10,6 @@
 // neptune_proof.rs:118-133 empty / all-zero proofs) must come out as `false`.
 #include <hip/hip_runtime.h>
 
-#include <emmintrin.h>
-
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -26,6 +24,7 @@
 
 #include "../../include/neptune_hip.h"
 #include "device_scope.hpp"
+#include "host_copy.hpp"
 #include "host_numa.hpp"
 #include "../../include/nhip_challenge_id.h"
 #include "goldilocks.hpp"
@@ -86,26 +85,6 @@ static bool stage_nt() {
     }();
     return on;
 }
-static void copy_words_nt(uint64_t* dst, const uint64_t* src, size_t words) {
-    if (((uintptr_t)dst & 15u) && words) {
-        *dst++ = *src++;
-        --words;
-    }
-    __m128i* d = (__m128i*)dst;
-    const __m128i* sv = (const __m128i*)src;
-    size_t blocks = words / 8;
-    for (; blocks; --blocks, d += 4, sv += 4) {
-        const __m128i a = _mm_loadu_si128(sv), b = _mm_loadu_si128(sv + 1), c = _mm_loadu_si128(sv + 2),
-                      e = _mm_loadu_si128(sv + 3);
-        _mm_stream_si128(d, a);
-        _mm_stream_si128(d + 1, b);
-        _mm_stream_si128(d + 2, c);
-        _mm_stream_si128(d + 3, e);
-    }
-    const size_t done = words / 8 * 8;
-    for (size_t i = done; i < words; ++i) dst[i] = src[i];
-}
-
 // Host threads for staging copies (NHIP_HOST_THREADS overrides; at most 16, the GPU box's CPU
 // share).
 unsigned host_threads(uint64_t bytes) {

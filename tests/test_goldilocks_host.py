@@ -49,3 +49,20 @@ def test_lazy_xfe_product_and_field_sum_match_integer_arithmetic(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "bad 0" in out.stdout
+
+
+def test_staging_copy_streaming_stores_match_memcpy(tmp_path):
+    """The staging copy's streaming-store word copy (host_copy.hpp) equals memcpy at every 8-byte
+    destination / source alignment and lengths 0-300 and beyond, and writes nothing outside the
+    destination (ASan + UBSan build)."""
+    import shutil
+    gxx = shutil.which("g++")
+    if not gxx:
+        pytest.skip("g++ not available")
+    exe = tmp_path / "copy_check"
+    subprocess.check_call([gxx, "-O2", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                           "-I", os.path.join(ROOT, "neptune-core_amd", "csrc"),
+                           os.path.join(ROOT, "tests", "native", "copy_check.cpp"), "-o", str(exe)])
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "bad 0" in out.stdout
