@@ -695,8 +695,42 @@ def group_stream(devices, air_words, stark, claims, proofs, expect, batches: int
     ncl = [NS.Claim(*c) for c in claims]
     pinned = None
     if pageable:
-        # distinct allocations: config 4 reuses 256 pool proofs, which would stay cache-resident
-        src = [np.array(p, dtype=np.uint64, copy=True) for p in proofs]
+        # distinct allocations: config 4 reuses 256 pool proofs, which would stay cache-resident.
+        # NHIP_BENCH_SRC_NODE=gpu / other (A/B runs): the copies first-touched by a thread on the
+        # first member GPU's NUMA node or on another node (where a node's receive thread may run)
+        where = os.environ.get("NHIP_BENCH_SRC_NODE")
+        src = None
+        if where in ("gpu", "other"):
+            import threading
+            import neptune_hip as nh
+            c0 = nh.Context(devices[0])
+            gnode = c0.numa()["node"]
+            c0.close()
+            nodes = sorted(int(d[4:]) for d in os.listdir("/sys/devices/system/node")
+                           if d.startswith("node") and d[4:].isdigit())
+            want = gnode if where == "gpu" else next((n for n in nodes if n != gnode), gnode)
+            try:
+                with open(f"/sys/devices/system/node/node{want}/cpulist") as f:
+                    cpus = set()
+                    for part in f.read().strip().split(","):
+                        a, _, b = part.partition("-")
+                        cpus.update(range(int(a), int(b or a) + 1))
+                cpus &= os.sched_getaffinity(0)
+            except OSError:
+                cpus = None
+            out = []
+
+            def touch():
+                if cpus:
+                    os.sched_setaffinity(0, cpus)
+                out.extend(np.array(p, dtype=np.uint64, copy=True) for p in proofs)
+
+            th = threading.Thread(target=touch)
+            th.start()
+            th.join()
+            src = out
+        if src is None:
+            src = [np.array(p, dtype=np.uint64, copy=True) for p in proofs]
     else:
         pinned = NS.PinnedProofs(proofs)
         src = pinned.views
@@ -726,6 +760,9 @@ def group_stream(devices, air_words, stark, claims, proofs, expect, batches: int
             "per_batch_ms": {"wall": dt / batches * 1e3, "stage_sum_members": d["ms_stage"],
                              "upload_wait_sum_members": d["ms_upload"], "device_sum_members": d["ms_device"]},
             "verdicts_correct": ok, "source": "pageable (one allocation per proof)" if pageable else "pinned",
+            "source_pages_first_touched": os.environ.get("NHIP_BENCH_SRC_NODE", "by the bench's main thread")
+            if pageable else None,
+            "stage_bind": os.environ.get("NHIP_STAGE_BIND", "auto"),
             "numa": [{"device": d["device"], "node": d["node"], "cpus": len(d["cpus"])} for d in numa],
             "numa_binding": os.environ.get("NHIP_NUMA", "1") != "0",
             "measured": f"{batches} submissions of the whole batch from "

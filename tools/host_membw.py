@@ -85,14 +85,16 @@ def main():
         src_node = lib.nhip_host_page_node(ctypes.c_void_p(src.ctypes.data + nbytes // 2))
         for threads in (4, 8, 16):
             per = words // threads
-            for bound in (True, False):
-                cpus = node_cpus(gnode) if bound else None
+            binds = [("bound", node_cpus(gnode)), ("unbound", None)]
+            if touch_node != gnode:
+                binds.append(("on_src_node", node_cpus(touch_node)))
+            for bname, cpus in binds:
                 best = 0.0
                 for _ in range(3):
                     dt = parallel(threads, cpus,
                                   lambda i: np.copyto(dst[i * per:(i + 1) * per], src[i * per:(i + 1) * per]))
                     best = max(best, per * threads * 8 / dt / 1e9)
-                out["cases"][f"src_{where}(node {src_node})_{threads}t_{'bound' if bound else 'unbound'}"] = round(best, 1)
+                out["cases"][f"src_{where}(node {src_node})_{threads}t_{bname}"] = round(best, 1)
         del src
     lib.nhip_host_free(ctypes.c_void_p(h.value))
     ctx.close()
