@@ -762,7 +762,6 @@ def group_stream(devices, air_words, stark, claims, proofs, expect, batches: int
             "verdicts_correct": ok, "source": "pageable (one allocation per proof)" if pageable else "pinned",
             "source_pages_first_touched": os.environ.get("NHIP_BENCH_SRC_NODE", "by the bench's main thread")
             if pageable else None,
-            "stage_bind": os.environ.get("NHIP_STAGE_BIND", "auto"),
             "numa": [{"device": d["device"], "node": d["node"], "cpus": len(d["cpus"])} for d in numa],
             "numa_binding": os.environ.get("NHIP_NUMA", "1") != "0",
             "measured": f"{batches} submissions of the whole batch from "

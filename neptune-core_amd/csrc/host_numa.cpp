@@ -25,7 +25,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <string>
 #include <vector>
 
@@ -158,47 +157,6 @@ hipError_t host_malloc_on(void** p, size_t bytes, int node, unsigned flags) {
     else (void)sys_set_mempolicy(MPOL_DEFAULT_, nullptr, 0);
     if (e != hipSuccess) e = hipHostMalloc(p, bytes, flags);  // placement is a preference
     return e;
-}
-
-const std::vector<int>& node_cpus(int node) {
-    static std::mutex mu;
-    static std::vector<std::vector<int>> cache;  // per node, read once
-    static std::vector<char> have;
-    static const std::vector<int> none;
-    if (node < 0 || node >= MAX_NODES) return none;
-    std::lock_guard<std::mutex> g(mu);
-    if ((size_t)node >= cache.size()) {
-        cache.resize(node + 1);
-        have.resize(node + 1, 0);
-    }
-    if (!have[node]) {
-        std::string v;
-        std::vector<int> cpus;
-        if (read_small_file("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist", v))
-            (void)parse_cpulist(v.c_str(), cpus);
-        cpu_set_t allowed;
-        CPU_ZERO(&allowed);
-        if (!cpus.empty() && sched_getaffinity(0, sizeof(allowed), &allowed) == 0) {
-            std::vector<int> keep;
-            for (int c : cpus)
-                if (c < CPU_SETSIZE && CPU_ISSET(c, &allowed)) keep.push_back(c);
-            cpus.swap(keep);
-        }
-        cache[node] = std::move(cpus);
-        have[node] = 1;
-    }
-    return cache[node];
-}
-
-StageBind stage_bind() {
-    static const StageBind b = [] {
-        const char* v = std::getenv("NHIP_STAGE_BIND");
-        if (!v || !std::strcmp(v, "auto")) return StageBind::Auto;
-        if (!std::strcmp(v, "gpu")) return StageBind::Gpu;
-        if (!std::strcmp(v, "src")) return StageBind::Src;
-        return StageBind::None;
-    }();
-    return b;
 }
 
 int page_node(const void* p) {

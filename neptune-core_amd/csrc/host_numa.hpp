@@ -27,13 +27,5 @@ bool bind_thread(const std::vector<int>& cpus);
 hipError_t host_malloc_on(void** p, size_t bytes, int node, unsigned flags);
 // the NUMA node holding the page at p (-1 if unknown)
 int page_node(const void* p);
-// node N's CPUs this process may run on (sysfs, read once per node; empty if unknown)
-const std::vector<int>& node_cpus(int node);
-// where the staging copy threads run (NHIP_STAGE_BIND): Auto (default) = on the node holding most
-// of the batch's source pages when that is another node than the GPU's (local reads, streaming
-// writes across), else on the GPU's node; Gpu = always the GPU's node; Src = always the source's;
-// None = unbound.  NHIP_NUMA=0 also leaves them unbound.
-enum class StageBind { Auto, Gpu, Src, None };
-StageBind stage_bind();
 
 }  // namespace nhip

@@ -817,40 +817,15 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
             // at most that node's CPUs, or the count set by nhip_set_host_threads (a group divides a
             // node's CPUs among the members on it)
             const nhip::HostTopo& topo = ctx_topo(ctx);
-            const std::vector<int>* bind = &topo.cpus;
-            static const std::vector<int> unbound;
-            if (!nhip::numa_enabled() || nhip::stage_bind() == nhip::StageBind::None) {
-                bind = &unbound;
-            } else if (nhip::stage_bind() != nhip::StageBind::Gpu && topo.numa_node >= 0 && !todo.empty()) {
-                // the node holding most of the batch's source pages (8 proofs sampled across it):
-                // when it is another node, the copies run there (local reads, streaming writes to
-                // the staging across the socket link) under Auto; always under Src
-                int votes[8] = {0}, nodes[8] = {0}, kinds = 0;
-                for (size_t q = 0; q < 8; ++q) {
-                    const int nd = nhip::page_node(proofs[todo[q * todo.size() / 8]].words);
-                    if (nd < 0) continue;
-                    int k = 0;
-                    while (k < kinds && nodes[k] != nd) ++k;
-                    if (k == kinds) nodes[kinds++] = nd;
-                    ++votes[k];
-                }
-                int best = -1, bv = 0;
-                for (int k = 0; k < kinds; ++k)
-                    if (votes[k] > bv) bv = votes[k], best = nodes[k];
-                if (best >= 0 && (best != topo.numa_node || nhip::stage_bind() == nhip::StageBind::Src)) {
-                    const std::vector<int>& c = nhip::node_cpus(best);
-                    if (!c.empty()) bind = &c;
-                }
-            }
             unsigned threads = host_threads(staged_bytes);
             if (const unsigned set = nhip_internal_host_threads(ctx); set && threads > 1) threads = set;
-            if (!bind->empty()) threads = std::min<unsigned>(threads, (unsigned)bind->size());
+            if (!topo.cpus.empty() && nhip::numa_enabled()) threads = std::min<unsigned>(threads, (unsigned)topo.cpus.size());
             if (threads > 1 && stage != pageable.data()) {
                 pool.reserve(threads);
                 for (unsigned t = 0; t < threads; ++t) {
                     try {
                         pool.emplace_back([&]() {
-                            (void)nhip::bind_thread(*bind);
+                            (void)nhip::bind_thread(topo.cpus);
                             work();
                         });
                     } catch (const std::system_error&) {
