@@ -499,15 +499,17 @@ def config1_latency(ctx, gair, stark, air_words, cpu_seconds: float, reps: int =
                         f"(oracle/stark_oracle.c)"}
 
 
-def config5_leg(ctx, gair, stark, proofs_n: int = 64, steps: int = 20, inflight: int = 4):
+def config5_leg(ctx, gair, stark, proofs_n: int = 64, steps: int = 20, inflight: int = None):
     """BASELINE config 5 beside the headline: `proofs_n` proofs at log2 padded height 23 (FRI domain
     2^26, 16 folding rounds) on one GPU.  The proof is tests/golden/deep_fri.npz's height-23 case
     (the sparse synthetic prover: every FRI codeword non-zero, a non-empty last polynomial), its
-    words copied once per proof; `inflight` resident batches, `steps` steps after 3 warm-up steps.
+    words copied once per proof; `inflight` resident batches (default: the bench's depth for that
+    batch size, 10 below 1,024 proofs), `steps` steps after 3 warm-up steps.
     Beside the rate: one batch alone (phase split; the sequential Fiat-Shamir sponge replay's share
     of that batch's device time) and proof 0's transcript against the oracle's, stored with the
     fixture."""
     import neptune_hip.stark as NS
+    inflight = inflight or default_inflight(proofs_n)
     z = np.load(os.path.join(ROOT, "tests", "golden", "deep_fri.npz"))
     meta = json.loads(bytes(z["meta"]).decode())["cases"]["23"]
     claim = (meta["digest"], meta["version"], meta["input"], meta["output"])
@@ -863,6 +865,8 @@ def main():
     if world == 1 and args.config == 4 and total == 4096 and args.share_steps > 0:
         # the share_n8 leg runs the N = 8 rank's 512-proof share at its own depth in this process
         want_q = max(want_q, hw_queues_wanted(default_inflight(total // 8), False))
+    if world == 1 and args.config5_proofs > 0:  # the config-5 leg at its own depth
+        want_q = max(want_q, hw_queues_wanted(default_inflight(args.config5_proofs), False))
     if os.environ.get("NHIP_BENCH_HWQ"):  # A/B runs: exactly this many
         os.environ["GPU_MAX_HW_QUEUES"] = os.environ["NHIP_BENCH_HWQ"]
     elif int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < want_q:
