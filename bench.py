@@ -565,6 +565,64 @@ def config5_leg(ctx, gair, stark, proofs_n: int = 64, steps: int = 20, inflight:
             "transcript_equals_oracle": transcript_ok, "verdicts_correct": ok}
 
 
+def queue_leg(ctx, gair, stark, claims, proofs, expect, callers: int = 64, rounds: int = 16):
+    """The per-proof call of many concurrent tasks (verifier.rs:60-63 from peer_loop.rs:1342's
+    mempool admission, one tokio task per peer transaction): `callers` threads each verify one proof
+    at a time through the coalescing queue (nhip_queue_verify; closed loop, `rounds` calls each),
+    beside the same calls serialized one proof per nhip_verify_batch.  Proofs/s, per-call latency
+    percentiles and the queue's batch profile."""
+    import threading
+    import neptune_hip.stark as NS
+    from neptune_hip.stark import _Marshal
+    n = len(proofs)
+    ncl = [NS.Claim(*c) for c in claims]
+    NS.verify_batch(ctx, gair, stark, [(ncl[0], proofs[0])])
+    m_ser = 32
+    t = time.perf_counter()
+    ser_ok = all(NS.verify_batch(ctx, gair, stark, [(ncl[i], proofs[i])])[0] == bool(expect[i]) for i in range(m_ser))
+    rate_ser = m_ser / (time.perf_counter() - t)
+    calls = [((j * 37) % n) for j in range(callers * rounds)]
+    marsh = [_Marshal([ncl[i]], [proofs[i]]) for i in calls]
+    lat = [0.0] * len(calls)
+    ok = [True]
+    with NS.Queue(ctx, gair, stark, max_wait_us=200) as q:
+        q.verify(ncl[0], proofs[0])
+        q.profile(reset=True)
+        barrier = threading.Barrier(callers + 1)
+
+        def worker(w):
+            v = np.zeros(1, dtype=np.uint8)
+            barrier.wait()
+            for r in range(rounds):
+                j = w * rounds + r
+                m = marsh[j]
+                t0 = time.perf_counter()
+                rc = ctx.lib.nhip_queue_verify(q.handle, m.claims, m.proofs, 1, v.ctypes.data)
+                lat[j] = time.perf_counter() - t0
+                if rc != 0 or bool(v[0]) != bool(expect[calls[j]]):
+                    ok[0] = False
+
+        ths = [threading.Thread(target=worker, args=(w,)) for w in range(callers)]
+        for th in ths:
+            th.start()
+        barrier.wait()
+        t = time.perf_counter()
+        for th in ths:
+            th.join()
+        dt = time.perf_counter() - t
+        prof = q.profile()
+    lat_ms = np.sort(np.asarray(lat)) * 1e3
+    nb = max(prof.get("batches", 1), 1)
+    return {"callers": callers, "calls": len(calls), "value": len(calls) / dt, "unit": "proofs/s",
+            "serialized_one_proof_calls": rate_ser, "vs_serialized": len(calls) / dt / rate_ser,
+            "latency_ms": {"p50": float(lat_ms[len(lat_ms) // 2]), "p90": float(lat_ms[int(len(lat_ms) * 0.9)]),
+                           "p99": float(lat_ms[int(len(lat_ms) * 0.99)])},
+            "proofs_per_batch": prof.get("proofs", 0) / nb, "batches": prof.get("batches", 0),
+            "verdicts_correct": ok[0] and ser_ok,
+            "measured": f"{callers} threads x {rounds} closed-loop nhip_queue_verify calls of one proof (max wait 200 us), "
+                        f"beside {m_ser} one-proof nhip_verify_batch calls in a row"}
+
+
 # ------------------------------------------------------------------ config 2 Tip5 path microbench
 def tip5_paths(ctx, log2_leaves: int, steps: int):
     """2^log2_leaves depth-log2_leaves Merkle authentication paths (pow.rs:162-180), 1% corrupted;
@@ -812,6 +870,8 @@ def main():
                     help="steps of the product-depth leg (2 in flight) after the timed region (0 = skip)")
     ap.add_argument("--share-steps", type=int, default=20,
                     help="config 4 at N = 1: timed steps of the N = 8 rank's 512-proof share (0 = skip)")
+    ap.add_argument("--queue-callers", type=int, default=64,
+                    help="queue leg at N = 1: concurrent single-proof callers through nhip_queue (0 = skip)")
     ap.add_argument("--config5-proofs", type=int, default=64,
                     help="config-5 leg at N = 1: proofs at log2 padded height 23 (0 = skip)")
     ap.add_argument("--stream-batches", type=int, default=6,
@@ -1233,6 +1293,11 @@ def main():
         res["pcie_inclusive"] = pcie_stream(ctx, gair, stark, dev_claims, dev_proofs, expect, args.stream_batches)
     if world == 1 and args.paths_log2 > 0:
         res["tip5_paths"] = tip5_paths(ctx, args.paths_log2, 5)
+    if world == 1 and args.queue_callers > 0:
+        t = time.time()
+        res["queue"] = queue_leg(ctx, gair, stark, dev_claims, dev_proofs, expect, args.queue_callers)
+        correct = correct and res["queue"]["verdicts_correct"]
+        log(f"[queue] {res['queue']['value']:.0f} proofs/s ({time.time() - t:.1f}s)")
     if world == 1 and args.config5_proofs > 0:
         t = time.time()
         res["config5"] = config5_leg(ctx, gair, stark, args.config5_proofs)

@@ -165,14 +165,16 @@ def _exchange_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_verdict_exchange_one_collective():
-    """shard.VerdictExchange at world size 2 (gloo): one all-gather per step carries the batch verdict
-    (the MIN of every rank's leading byte) and the per-proof verdicts, exchanges posted two at a
-    time complete in posting order, and the answers equal all_ok + gather_verdicts."""
+@pytest.mark.parametrize("world", [2, 8])
+def test_two_rank_verdict_exchange_one_collective(world):
+    """shard.VerdictExchange at world size 2 and 8 (gloo; 8 = the driver's node, every rank's LPT
+    shard of 37 units): one all-gather per step carries the batch verdict (the MIN of every rank's
+    leading byte) and the per-proof verdicts, exchanges posted two at a time complete in posting
+    order, and the answers equal all_ok + gather_verdicts on every rank."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]

@@ -13,7 +13,7 @@ for n in ${SIZES:-4096 512}; do
 for spec in "$@"; do
   IFS='|' read -r name envs extra <<< "$spec"
   f=$OUT/n${n}_${name}_r$rep
-  env $envs timeout -k 10 300 python -u bench.py --no-cpu --config 4 --proofs $n --paths-log2 0 --config5-proofs 0 --product-steps 0 --share-steps 0 --stream-batches 0 \
+  env $envs timeout -k 10 300 python -u bench.py --no-cpu --config 4 --proofs $n --paths-log2 0 --config5-proofs 0 --product-steps 0 --share-steps 0 --queue-callers 0 --stream-batches 0 \
     --config1-seconds 0 --group-batches 0 --steps ${STEPS:-200} $extra > $f.json 2> $f.err || { tail -5 $f.err; exit 1; }
   python3 -c "
 import json, sys

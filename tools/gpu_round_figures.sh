@@ -7,8 +7,8 @@ OUT=$PWD/gpurun_out/figs_${1:-x}; mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 python -u bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || { tail -5 $OUT/bench_default.err; exit 1; }
 timeout -k 10 200 python -u tools/latency.py 20 > $OUT/latency.json 2> $OUT/latency.err || { tail -5 $OUT/latency.err; exit 1; }
-timeout -k 10 200 python -u bench.py --no-cpu --proofs 512 --paths-log2 0 --config5-proofs 0 --product-steps 0 --share-steps 0 --stream-batches 0 > $OUT/bench_512.json 2> $OUT/bench_512.err || { tail -5 $OUT/bench_512.err; exit 1; }
-timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_LDS SQ_INSTS_SALU -d $OUT/pmc512 -o pmc_valu --output-format csv -- python3 bench.py --no-cpu --proofs 512 --paths-log2 0 --config5-proofs 0 --product-steps 0 --share-steps 0 --stream-batches 0 --group-batches 0 --config1-seconds 0 > $OUT/bench_512_pmc.json 2> $OUT/pmc512.err || exit 1
+timeout -k 10 200 python -u bench.py --no-cpu --proofs 512 --paths-log2 0 --config5-proofs 0 --product-steps 0 --share-steps 0 --queue-callers 0 --stream-batches 0 > $OUT/bench_512.json 2> $OUT/bench_512.err || { tail -5 $OUT/bench_512.err; exit 1; }
+timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_LDS SQ_INSTS_SALU -d $OUT/pmc512 -o pmc_valu --output-format csv -- python3 bench.py --no-cpu --proofs 512 --paths-log2 0 --config5-proofs 0 --product-steps 0 --share-steps 0 --queue-callers 0 --stream-batches 0 --group-batches 0 --config1-seconds 0 > $OUT/bench_512_pmc.json 2> $OUT/pmc512.err || exit 1
 python3 - $OUT <<'PY'
 import json, sys
 o = sys.argv[1]

@@ -6,7 +6,7 @@
 set -o pipefail
 TAG=${1:-r02}
 shift || true
-ARGS=${*:-"--steps 20 --warmup 5 --no-cpu --paths-log2 0 --config5-proofs 0 --product-steps 0 --share-steps 0 --stream-batches 0 --config1-seconds 0 --group-batches 0"}
+ARGS=${*:-"--steps 20 --warmup 5 --no-cpu --paths-log2 0 --config5-proofs 0 --product-steps 0 --share-steps 0 --queue-callers 0 --stream-batches 0 --config1-seconds 0 --group-batches 0"}
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
