@@ -3,7 +3,9 @@ share of batch k staged and uploaded while its share of batch k - 1 runs, as boo
 (state/mod.rs:2226-2272) and block batches (peer_loop.rs:315-323) verify one batch after another.
 Here the members are several contexts on GPU 0.  Every batch's verdicts arrive one submit later (the
 last at finish), in the caller's order, equal to the expected ones, in both input forms; empty
-batches, a batch smaller than the member count and a single-member group stream too."""
+batches, a batch smaller than the member count, a single-member group stream, and eight members
+(the driver's node: eight member threads, each with its share of the node's CPUs for its copy
+threads) too."""
 import numpy as np
 import pytest
 
@@ -26,7 +28,7 @@ def batches():
     return pool4["air"], out
 
 
-@pytest.mark.parametrize("members,mont", [(2, False), (3, True), (1, True)])
+@pytest.mark.parametrize("members,mont", [(2, False), (3, True), (1, True), (8, True)])
 def test_group_stream_verdicts(batches, members, mont):
     import neptune_hip.stark as NS
     air_words, bs = batches
