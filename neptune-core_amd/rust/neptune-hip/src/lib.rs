@@ -282,25 +282,10 @@ impl GpuNode {
     }
 
     /// The batch's proofs from a [`ProofArena`] (pinned receive memory): DMA'd as they lie, no
-    /// staging copy.  `claims[i]` belongs to `arena.proof(i)`.
+    /// staging copy, split over every GPU (`nhip_group_verify_batch`).  `claims[i]` belongs to
+    /// `arena.proof(i)`.
     pub fn verify_arena(&self, claims: &[Claim], arena: &ProofArena) -> Result<(Vec<bool>, bool), GpuFault> {
-        if claims.len() != arena.len() {
-            return Err(GpuFault(sys::NHIP_ERR_ARG));
-        }
-        let mut cs = Vec::with_capacity(claims.len());
-        let mut ps = Vec::with_capacity(claims.len());
-        for (i, c) in claims.iter().enumerate() {
-            cs.push(sys::nhip_claim {
-                program_digest: raw_digest(&c.program_digest),
-                version: c.version,
-                input: raw_words(&c.input),
-                input_len: c.input.len(),
-                output: raw_words(&c.output),
-                output_len: c.output.len(),
-            });
-            let p = arena.proof(i);
-            ps.push(sys::nhip_proof { words: raw_words(p), len: p.len() });
-        }
+        let (cs, ps) = arena_marshal(claims, arena)?;
         let mut v = vec![0u8; claims.len()];
         let mut all = 0u8;
         ok(unsafe {
@@ -309,12 +294,83 @@ impl GpuNode {
         })?;
         Ok((v.into_iter().map(|b| b == 1).collect(), all == 1))
     }
+
+    /// One arena per GPU, each on its GPU's NUMA node ([`GpuNode::arenas`]): member `m` verifies the
+    /// proofs of `batches[m]` itself (no re-sharding, so no proof crosses the socket link), all
+    /// members concurrently.  Returns each member's verdicts and the AND over all of them (the
+    /// block / ProofCollection verdict, `proof_collection.rs:388`).
+    pub fn verify_arenas(&self, batches: &[(&[Claim], &ProofArena)]) -> Result<(Vec<Vec<bool>>, bool), GpuFault> {
+        if batches.len() > self.gpus() {
+            return Err(GpuFault(sys::NHIP_ERR_ARG));
+        }
+        // the C structs hold raw pointers into the arenas and claims, which outlive the scope below
+        struct Shard(Vec<sys::nhip_claim>, Vec<sys::nhip_proof>);
+        unsafe impl Sync for Shard {}
+        let mut marshalled = Vec::with_capacity(batches.len());
+        for (claims, arena) in batches {
+            let (cs, ps) = arena_marshal(claims, arena)?;
+            marshalled.push(Shard(cs, ps));
+        }
+        let results: Vec<Result<Vec<u8>, GpuFault>> = std::thread::scope(|scope| {
+            let handles: Vec<_> = marshalled
+                .iter()
+                .enumerate()
+                .map(|(m, Shard(cs, ps))| {
+                    let ctx = unsafe { sys::nhip_group_member(self.group, m) } as usize;
+                    let (air, params) = (self.air.0 as usize, &self.params);
+                    scope.spawn(move || {
+                        let mut v = vec![0u8; cs.len()];
+                        ok(unsafe {
+                            sys::nhip_verify_batch(ctx as *mut sys::nhip_ctx, air as *mut sys::nhip_air, params, cs.as_ptr(),
+                                                   ps.as_ptr(), cs.len(), v.as_mut_ptr(), ptr::null_mut())
+                        })
+                        .map(|_| v)
+                    })
+                })
+                .collect();
+            handles.into_iter().map(|h| h.join().unwrap_or(Err(GpuFault(sys::NHIP_ERR_HIP)))).collect()
+        });
+        let mut out = Vec::with_capacity(results.len());
+        let mut all = true;
+        for r in results {
+            let v: Vec<bool> = r?.into_iter().map(|b| b == 1).collect();  // any member's fault: unknown
+            all &= v.iter().all(|&x| x);
+            out.push(v);
+        }
+        Ok((out, all))
+    }
+
+    /// One [`ProofArena`] of `cap_words` words per GPU, each on that GPU's NUMA node.
+    pub fn arenas(&self, cap_words: usize) -> Result<Vec<ProofArena>, GpuFault> {
+        (0..self.gpus()).map(|m| ProofArena::new(self, m, cap_words)).collect()
+    }
 }
 
 impl Drop for GpuNode {
     fn drop(&mut self) {
         unsafe { sys::nhip_group_destroy(self.group) }
     }
+}
+
+fn arena_marshal(claims: &[Claim], arena: &ProofArena) -> Result<(Vec<sys::nhip_claim>, Vec<sys::nhip_proof>), GpuFault> {
+    if claims.len() != arena.len() {
+        return Err(GpuFault(sys::NHIP_ERR_ARG));
+    }
+    let mut cs = Vec::with_capacity(claims.len());
+    let mut ps = Vec::with_capacity(claims.len());
+    for (i, c) in claims.iter().enumerate() {
+        cs.push(sys::nhip_claim {
+            program_digest: raw_digest(&c.program_digest),
+            version: c.version,
+            input: raw_words(&c.input),
+            input_len: c.input.len(),
+            output: raw_words(&c.output),
+            output_len: c.output.len(),
+        });
+        let p = arena.proof(i);
+        ps.push(sys::nhip_proof { words: raw_words(p), len: p.len() });
+    }
+    Ok((cs, ps))
 }
 
 /// Pinned receive memory for proofs, on the NUMA node of one GPU (`nhip_host_alloc_near`): the node
