@@ -80,6 +80,7 @@ bool parse_cpulist(const char* s, std::vector<int>& out) {
         long stride = 1;
         if (*p == ':') {  // "a-b:stride" (kernel cpulist syntax)
             ++p;
+            if (!std::isdigit((unsigned char)*p)) return false;  // strtol would skip whitespace
             stride = std::strtol(p, &e, 10);
             p = e;
             if (stride <= 0) return false;

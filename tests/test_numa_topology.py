@@ -104,3 +104,51 @@ def test_page_node_of_host_memory():
     buf[0] = 1  # touched: the page exists
     node = lib.nhip_host_page_node(ctypes.addressof(buf))
     assert node in (-1, 0) or node >= 0
+
+
+def _py_cpulist(text):
+    """The kernel's cpulist syntax (lib/bitmap.c bitmap_parselist): "a", "a-b" or "a-b:stride"
+    groups, separated by commas (the library also takes whitespace between groups); None when
+    malformed."""
+    import re
+    out = set()
+    for part in re.split(r"[,\s]+", text):
+        if not part:
+            continue
+        rng, colon, stride = part.partition(":")
+        a, dash, b = rng.partition("-")
+        if not a.isdigit() or (dash and not b.isdigit()) or (colon and not stride.isdigit()):
+            return None
+        lo, hi = int(a), int(b) if dash else int(a)
+        st = int(stride) if stride else 1
+        if hi < lo or st <= 0 or hi > (1 << 20):
+            return None
+        out.update(range(lo, hi + 1, st))
+    return sorted(out)
+
+
+def test_cpulist_parse_matches_reference_grammar():
+    """nhip_cpulist_parse on generated lists (single CPUs, ranges, strided ranges, overlaps, spaces)
+    equals the grammar above; random byte strings never crash it and are either refused or parsed
+    as the grammar parses them."""
+    import random
+    lib = _lib()
+    rng = random.Random(0x5A)
+    for _ in range(2000):
+        parts = []
+        for _ in range(rng.randint(1, 6)):
+            a = rng.randint(0, 300)
+            kind = rng.random()
+            if kind < 0.4:
+                parts.append(str(a))
+            elif kind < 0.8:
+                parts.append(f"{a}-{a + rng.randint(0, 64)}")
+            else:
+                parts.append(f"{a}-{a + rng.randint(0, 64)}:{rng.randint(1, 9)}")
+        text = ",".join(parts) + rng.choice(["", "\n", " "])
+        assert _parse(lib, text) == _py_cpulist(text), text
+    alphabet = "0123456789,-: \nx"
+    for _ in range(2000):
+        text = "".join(rng.choice(alphabet) for _ in range(rng.randint(0, 24)))
+        got, want = _parse(lib, text), _py_cpulist(text)
+        assert got is None or got == want, text
