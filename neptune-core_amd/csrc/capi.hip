@@ -245,7 +245,6 @@ void* nhip_internal_staging(nhip_ctx* c, size_t bytes) {
 
 const void* nhip_internal_topo(nhip_ctx* c) { return &c->topo; }  // a const nhip::HostTopo*
 unsigned nhip_internal_host_threads(nhip_ctx* c) { return c->host_threads; }
-void nhip_internal_set_host_threads(nhip_ctx* c, unsigned n) { c->host_threads = n; }
 
 int nhip_device_numa(nhip_ctx* c, int* numa_node, int* cpus, size_t cpu_cap, size_t* n_cpus) {
     if (!c || !numa_node) return NHIP_ERR_ARG;

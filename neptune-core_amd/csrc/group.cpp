@@ -280,9 +280,12 @@ struct nhip_group_stream {
         ms.in_flight[s] = false;
         StreamBatch& B = sb[s];
         const size_t cnt = B.idx[mm].size();
-        if (ms.v[s].size() < cnt) return NHIP_ERR_ARG;  // sized at submit; never written past
-        const int rc = nhip_batch_wait(g->members[mm], ms.b[s], ms.v[s].data(), nullptr);
+        // sized at submit, so never short; if it were, the batch is still waited for (the slot must
+        // be idle before it is refilled or destroyed) and its verdicts are not read
+        const bool fits = ms.v[s].size() >= cnt;
+        const int rc = nhip_batch_wait(g->members[mm], ms.b[s], fits ? ms.v[s].data() : nullptr, nullptr);
         if (rc) return rc;
+        if (!fits) return NHIP_ERR_ARG;
         for (size_t q = 0; q < cnt; ++q) B.verdicts[B.idx[mm][q]] = ms.v[s][q];
         nhip_stats st{};
         nhip_batch_stats(ms.b[s], &st);

@@ -75,7 +75,7 @@ void encode_claim(const nhip_claim& claim, bool mont, uint64_t* c) {
 // stores: the staging is written once and read only by the DMA engine, so ordinary stores would
 // first read every destination line into the cache (a read-for-ownership) and then evict it: one
 // more host-DRAM pass per proof byte.  The feed path's host bandwidth is what an 8-GPU node runs
-// out of first (DESIGN.md §6), so the copy streams: 8-byte head to 16-byte alignment, 64-byte
+// out of first (DESIGN.md §6a), so the copy streams: 8-byte head to 16-byte alignment, 64-byte
 // blocks of four 16-byte streaming stores, then the tail.  The caller fences (_mm_sfence) before
 // the DMA of the chunk is issued.  NHIP_STAGE_NT=0: plain memcpy (A/B).
 static bool stage_nt() {
@@ -1120,10 +1120,14 @@ static int launch_resources(nhip_batch* b) {
                     for (uint32_t j = 0; j < 2 * MAX_HASH_LAUNCHES; ++j) b->tm.lev[j] = nullptr;
                     break;  // untimed hash launches: a fault of the timing only
                 }
-            if (NHIP_HASH_LAUNCH_EVENTS && (hipEventCreate(&b->tm.rev[0]) != hipSuccess ||
-                                            hipEventCreate(&b->tm.rev[1]) != hipSuccess)) {
-                if (b->tm.rev[0]) (void)hipEventDestroy(b->tm.rev[0]);
-                b->tm.rev[0] = b->tm.rev[1] = nullptr;  // an untimed row launch
+            if (NHIP_HASH_LAUNCH_EVENTS) {
+                hipEvent_t r0 = nullptr, r1 = nullptr;
+                if (hipEventCreate(&r0) == hipSuccess && hipEventCreate(&r1) == hipSuccess) {
+                    b->tm.rev[0] = r0;
+                    b->tm.rev[1] = r1;
+                } else if (r0) {
+                    (void)hipEventDestroy(r0);  // an untimed row launch: a fault of the timing only
+                }
             }
             if (hipStreamCreateWithFlags(&b->main, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
             if (hipStreamCreateWithFlags(&b->aux, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
