@@ -190,6 +190,24 @@ def pmc_mp_valu_per_launch(config: int, proofs: int):
         return None, None
 
 
+def pmc_rows_valu_per_launch(config: int, proofs: int):
+    """Wave-level VALU instructions of one row-hashing launch (k_hash_rows, one per step) from the
+    latest committed PMC pass; None when absent."""
+    import csv
+    tag = latest_profile(config, proofs)
+    if tag is None:
+        return None, None
+    try:
+        tot, n = 0.0, 0
+        for r in csv.DictReader(open(os.path.join(ROOT, "profiles", tag, "pmc_valu_counter_collection.csv"))):
+            if r["Counter_Name"] == "SQ_INSTS_VALU" and "k_hash_rows" in r["Kernel_Name"]:
+                tot += float(r["Counter_Value"])
+                n += 1
+        return (tot / n, tag) if n else (None, None)
+    except (OSError, KeyError):
+        return None, None
+
+
 def under_profiler() -> bool:
     """rocprofv3 runs this process with its tool library preloaded (it initialises the GPU before
     bench.py starts): no child process may then be started from here."""
@@ -1232,6 +1250,15 @@ def main():
                 "frac_of_measured_ceiling": ach / (VALU_ISSUE_CEILING * 64),
                 "row_bytes_per_launch": n * stark.num_collinearity_checks * sum(widths) * 8,
                 "measured": f"the same {iso_steps} isolated steps; hipExtLaunchKernel start/stop of the row launch"}
+            rv, rv_tag = pmc_rows_valu_per_launch(args.config, len(proofs))
+            if rv:
+                # a row permutation skips its capacity-only / digest-only last-round outputs, so it
+                # executes fewer than the fixed 7,520: the executed count (committed PMC pass of this
+                # library) against the measured issue ceiling is the kernel's own issue fraction
+                ex = rv * 64 / rows_perms
+                res["roofline"]["rows_kernel"].update({
+                    "valu_ops_per_perm_executed": ex, "executed_profile": rv_tag,
+                    "executed_frac_of_measured_ceiling": rows_perms * ex / (rows_ms / 1e3) / (VALU_ISSUE_CEILING * 64)})
         res["roofline"]["inflight"] = {k: inflight[k] for k in ("achieved", "frac", "kernel_avg_ms",
                                                                  "kernel_avg_ms_events", "launches_per_step",
                                                                  "perms_per_launch", "launches_x_avg_ms", "step_ms",
