@@ -55,3 +55,23 @@ def test_pageable_views_at_odd_offsets(ctx, batch, mont):
     assert [bool(x) for x in v] == want and ok == all(want)
     b.close()
     del big
+
+
+def test_receive_buffer_on_the_gpus_numa_node(ctx, batch):
+    """nhip_host_alloc_near places the pinned receive buffer on the NUMA node of the context's GPU
+    (when the platform reports one), and proofs received into it verify as they lie."""
+    import ctypes
+    import neptune_hip.stark as NS
+    air_words, claims, proofs, expect = batch
+    topo = ctx.numa()
+    pinned = NS.PinnedProofs(proofs[:64], near=ctx)
+    try:
+        node = ctx.lib.nhip_host_page_node(ctypes.c_void_p(pinned.ptr))
+        if topo["node"] >= 0 and node >= 0:
+            assert node == topo["node"]
+        air = NS.Air([int(w) for w in air_words])
+        got = NS.verify_batch(ctx, air, NS.Stark.default(), list(zip([NS.Claim(*c) for c in claims[:64]],
+                                                                      pinned.views)))
+        assert got == [bool(x) for x in expect[:64]]
+    finally:
+        pinned.close()
