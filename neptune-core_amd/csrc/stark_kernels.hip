@@ -997,7 +997,8 @@ __global__ void __launch_bounds__(MP_CLIMB_THREADS) k_mp_climb(const uint64_t* _
                                                                const uint64_t* __restrict__ dig, MpPlan plan,
                                                                uint32_t trees_per_proof,
                                                                const ProofDesc* __restrict__ desc, uint32_t n_proofs,
-                                                               const uint32_t* __restrict__ fail, LcwTree lcw) {
+                                                               const uint32_t* __restrict__ fail, LcwTree lcw,
+                                                               uint32_t start_lvl) {
     latency_priority();
     __shared__ Tip5Lds t5;
     tip5_lds_init(t5);
@@ -1012,7 +1013,7 @@ __global__ void __launch_bounds__(MP_CLIMB_THREADS) k_mp_climb(const uint64_t* _
         const ProofDesc& d = desc[p];
         const uint32_t L = d.last_cw_n;
         uint64_t* mine = lcw.nodes + (uint64_t)p * lcw.max_len * 5;
-        for (uint32_t lvl = 0; (L >> (lvl + 1)) > 0; ++lvl) {
+        for (uint32_t lvl = start_lvl; (L >> (lvl + 1)) > 0; ++lvl) {
             const uint32_t cnt = L >> (lvl + 1);
             for (uint32_t row = row0; row < cnt; row += ROWS) {  // uniform within the 16-lane row
                 const uint32_t v = cnt + row;
@@ -1029,7 +1030,7 @@ __global__ void __launch_bounds__(MP_CLIMB_THREADS) k_mp_climb(const uint64_t* _
     const uint32_t grp = y < 4 ? 0u : y - 3u, sub = y < 4 ? y : 0u;
     const uint64_t grp_id = (uint64_t)p * (trees_per_proof - 3) + grp;
     const uint32_t nl = plan.lvl_n[grp_id];
-    for (uint32_t lvl = 0; lvl < nl; ++lvl) {
+    for (uint32_t lvl = start_lvl; lvl < nl; ++lvl) {
         const uint64_t g0 = plan.lvl_g0[grp_id * plan.levels + lvl];
         const uint32_t cnt = plan.lvl_cnt[grp_id * plan.levels + lvl];
         for (uint32_t row = row0; row < cnt; row += ROWS) {  // uniform within the 16-lane row
@@ -1669,6 +1670,24 @@ static bool ood_wide(uint32_t n) {
     return n <= lim;
 }
 
+// Level-synchronous batches of deep trees (>= CLIMB_FROM_MIN_LEVELS hash levels: BASELINE config 5's
+// height-23 proofs have 26) hand the rest of their trees to one per-tree climb launch (k_mp_climb
+// from a start level) at the first level with at most climb_from_ops() hash ops: the top levels of a
+// deep tree are launch-bound, not VALU-bound.  Measured (profiles/r05z/ab/climb_from_ab_r05q.txt):
+// config 5's 64 proofs +3-6% at 4,096 ops; config 4's trees (<= 19 levels) are not affected (at
+// 4,096 ops without the depth gate: 512 proofs -2 to -4%, 4,096 equal; 16K / 64K ops: worse).
+// NHIP_CLIMB_FROM_OPS overrides the threshold for every depth (0 = never).
+static constexpr uint32_t CLIMB_FROM_MIN_LEVELS = 24;
+static constexpr uint64_t CLIMB_FROM_OPS_DEFAULT = 4096;
+static uint64_t climb_from_ops(uint32_t hash_levels) {
+    static const int64_t v = [] {
+        const char* e = std::getenv("NHIP_CLIMB_FROM_OPS");
+        return e ? (int64_t)std::strtoull(e, nullptr, 10) : (int64_t)-1;
+    }();
+    if (v >= 0) return (uint64_t)v;
+    return hash_levels >= CLIMB_FROM_MIN_LEVELS ? CLIMB_FROM_OPS_DEFAULT : 0ull;
+}
+
 // row-form batches below this many proofs replay with the carry-light arithmetic (A/B knob
 // NHIP_FS_ROW_LAT_MAX; default 0 = never)
 static uint32_t fs_row_lat_max() {
@@ -1833,7 +1852,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
         const bool timed = tm->lev[0] != nullptr;
         hipExtLaunchKernelGGL(k_mp_climb<MW>, dim3(n, tpp + 1), dim3(MP_CLIMB_THREADS), 0, st,
                               timed ? tm->lev[0] : nullptr, timed ? tm->lev[1] : nullptr, 0, b.words, b.dig, b.mp,
-                              tpp, b.desc, n, (const uint32_t*)b.fail, LcwTree{b.lcw, b.max_lcw});
+                              tpp, b.desc, n, (const uint32_t*)b.fail, LcwTree{b.lcw, b.max_lcw}, 0u);
         launches = 1;
     }
     const LcwTree lcw{b.lcw, b.max_lcw};
@@ -1859,6 +1878,18 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
         }
         const bool timed = launches < MAX_HASH_LAUNCHES && tm->lev[0] != nullptr;
         hipEvent_t e0 = timed ? tm->lev[2 * launches] : nullptr, e1 = timed ? tm->lev[2 * launches + 1] : nullptr;
+        {
+            // the rest of every tree climbed per (proof, tree group) in one launch once a level is small
+            // (deep trees: climb_from_ops above)
+            const uint64_t ops_l = (l < b.mp.levels ? b.mp_cap_host[l] : 0) + (uint64_t)(b.max_lcw >> (l + 1)) * n;
+            const uint64_t cf = climb_from_ops(hash_levels);
+            if (cf && ops_l <= cf && hash_levels - l >= 3) {
+                hipExtLaunchKernelGGL(k_mp_climb<MW>, dim3(n, tpp + 1), dim3(MP_CLIMB_THREADS), 0, st, e0, e1, 0, b.words,
+                                      b.dig, b.mp, tpp, b.desc, n, (const uint32_t*)b.fail, lcw, l);
+                ++launches;
+                break;
+            }
+        }
         if (l == tail0) {
             TailCaps caps{};
             for (uint32_t t = l; t < hash_levels; ++t) caps.cap[t - l] = t < b.mp.levels ? (uint32_t)b.mp_cap_host[t] : 0u;
