@@ -1017,8 +1017,14 @@ def main():
     exch = shard.VerdictExchange(shards, total, dist) if (dist is not None and shards is not None) else None
     exchanged = []  # (batch verdict, job verdict vector) of every completed exchange
 
+    # NHIP_BENCH_TIMELINE=<file>: host times of every launch and wait return of the timed region
+    # (a diagnostic of the pipeline's fill and drain; the kernel tracer stretches small steps)
+    timeline = [] if os.environ.get("NHIP_BENCH_TIMELINE") else None
+
     def launch_one():
         ring[next_slot[0]].launch()
+        if timeline is not None:
+            timeline.append(("L", time.perf_counter()))
         launched.append(next_slot[0])
         next_slot[0] = (next_slot[0] + 1) % R
         to_launch[0] -= 1
@@ -1031,6 +1037,8 @@ def main():
             launch_one()
         b = ring[launched.pop(0)]
         v, ok = b.wait()
+        if timeline is not None:
+            timeline.append(("W", time.perf_counter()))
         st = b.stats()
         if to_launch[0]:
             launch_one()
@@ -1064,6 +1072,8 @@ def main():
     correct = True
     t_start = time.perf_counter()
     to_launch[0] = args.steps  # every timed step is launched and waited inside the timed region
+    if timeline is not None:
+        timeline.clear()
     for _ in range(args.steps):
         st, v, batch_ok = step()
         correct = correct and bool((np.asarray(v, dtype=bool) == expect).all())
@@ -1072,6 +1082,10 @@ def main():
     drain_exchange()  # the last step's exchange completes inside the timed region
     barrier_sync()
     elapsed = time.perf_counter() - t_start
+    if timeline is not None and rank == 0:
+        with open(os.environ["NHIP_BENCH_TIMELINE"], "w") as f:
+            json.dump({"t_start": t_start, "elapsed": elapsed, "inflight": R,
+                       "events": [(k, t - t_start) for k, t in timeline]}, f)
     if exch is not None:
         correct = correct and len(exchanged) == args.steps
         for ok_all, full in exchanged:
