@@ -34,8 +34,12 @@ Beside `value` (HBM-resident input, the contract):
   roofline: the dominant kernel, the per-level Merkle hash launches (k_mp_hash), as Tip5 VALU
     lane-ops/s against the gfx950 VALU peak, from its launches in steps run one at a time right
     after the timed region (the kernel's own rate: launches x average <= step time).
-    roofline.inflight: the same launches inside the timed region, where launches of the steps in
-    flight overlap each other and the other kernels (labelled, not the kernel's rate).
+    roofline.inflight: the same launches in the timed region's shape (R steps in flight, up to 50
+    steps) run again right after it, where launches of the steps in flight overlap each other and
+    the other kernels (labelled, not the kernel's rate).  The kernel timing (per-dispatch begin / end
+    timestamps, nhip_batch_set_launch_timing) is on in these two passes only: the timed region runs
+    the product's configuration, without it (it costs a 512-proof share ~4.5%; the pass's own rate
+    stands beside the timed region's in roofline.inflight).
   pcie_inclusive: the same batch arriving from host memory (pinned, DMA'd per refill, two batches
     alternating) with the host-to-device link's measured ceiling; never `value`.
   group_stream: the same batches through the in-process multi-GPU form neptune-core uses
@@ -293,6 +297,15 @@ def make_batch(pool, collections: int, corrupt_frac: float, seed: int):
             proofs.append(proof)
             expect.append(ok)
     return claims, proofs, np.array(expect, dtype=bool)
+
+
+def kernel_timing(batches, on: bool = True):
+    """Per-dispatch timestamps on the Merkle hash and row launches (nhip_batch_set_launch_timing),
+    for the kernel-timing passes only: every batch runs without them otherwise, as the product's
+    batches do (they cost a 512-proof share ~4.5% of its rate)."""
+    for b in batches:
+        if hasattr(b.ctx.lib, "nhip_batch_set_launch_timing"):  # older libraries (NHIP_LIB A/B) always time
+            b.set_launch_timing(on)
 
 
 def pipelined(batches, steps: int, inflight: int, expect):
@@ -1061,6 +1074,10 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
+    # NHIP_BENCH_REGION_TIMING=1 (A/B of their cost): the timed region and the share leg with the
+    # per-dispatch timestamps on, as bench.py ran them before round 5
+    region_timing = os.environ.get("NHIP_BENCH_REGION_TIMING", "0") == "1"
+    kernel_timing(ring, region_timing)
     to_launch[0] = args.warmup
     for _ in range(args.warmup):
         step()
@@ -1091,7 +1108,30 @@ def main():
         for ok_all, full in exchanged:
             correct = correct and bool((full.astype(bool) == expect_all).all())
             batch_ok = ok_all
-    # the same steps one at a time (nothing else on the device): the kernel's own roofline
+    # the kernel-timing passes, right after the timed region (which ran the product's configuration,
+    # without per-dispatch timestamps): the same R-in-flight shape again with them
+    # (roofline.inflight), then the same steps one at a time (roofline, the kernel's own rate)
+    kernel_timing(ring, True)
+    acc_if, if_steps = {}, max(1, min(args.steps, 50))
+    ctx.synchronize()
+    t_if = time.perf_counter()
+    q_if, launched_if, ok_if = [], 0, True
+    for i in range(min(R, if_steps)):
+        ring[i].launch()
+        q_if.append(i)
+        launched_if += 1
+    while q_if:
+        i = q_if.pop(0)
+        v_if, _ = ring[i].wait()
+        for k, x in ring[i].stats().items():  # before the relaunch re-records the events
+            acc_if[k] = acc_if.get(k, 0.0) + x
+        if launched_if < if_steps:
+            ring[i].launch()
+            q_if.append(i)
+            launched_if += 1
+        ok_if = ok_if and bool((np.asarray(v_if, dtype=bool) == expect).all())
+    if_ms = (time.perf_counter() - t_if) / if_steps * 1e3
+    correct = correct and ok_if
     acc_iso, iso_ms = {}, 0.0
     iso_steps = args.iso_steps
     if R > 1 and iso_steps:
@@ -1102,6 +1142,7 @@ def main():
             for k, x in ring[0].stats().items():
                 acc_iso[k] = acc_iso.get(k, 0.0) + x
         iso_ms = (time.perf_counter() - t_iso) / iso_steps * 1e3
+    kernel_timing(ring, False)
 
     # the product's own pipeline depth beside the bench's: a queue or a group member keeps two
     # batches in flight (two slots), with the library's recommended hardware queues enough for it
@@ -1242,8 +1283,13 @@ def main():
         "inflight": R,
         "iso_steps": iso_steps if acc_iso else 0,
     }
-    inflight = roofline(acc, K, step_ms, R, f"timed region, {R} step(s) in flight (launches of different steps "
-                                            f"overlap); per-launch HIP events (hipExtLaunchKernel start/stop)")
+    inflight = roofline(acc_if, if_steps, if_ms, R,
+                        f"{if_steps} steps right after the timed region, {R} in flight as there (launches of "
+                        f"different steps overlap); per-launch HIP events (hipExtLaunchKernel start/stop)")
+    # that pass's own rate beside the timed region's: the cost of the per-dispatch timestamps
+    inflight["proofs_per_s_gpu_timed_region"] = n * K / elapsed
+    inflight["proofs_per_s_gpu_with_dispatch_timestamps"] = n / (if_ms / 1e3)
+    inflight["pass_steps"] = if_steps
     if acc_iso:
         res["roofline"] = roofline(acc_iso, iso_steps, iso_ms, 1,
                                    f"the kernel's own rate: {iso_steps} steps one at a time right after the timed "
@@ -1276,7 +1322,9 @@ def main():
         res["roofline"]["inflight"] = {k: inflight[k] for k in ("achieved", "frac", "kernel_avg_ms",
                                                                  "kernel_avg_ms_events", "launches_per_step",
                                                                  "perms_per_launch", "launches_x_avg_ms", "step_ms",
-                                                                 "measured")}
+                                                                 "measured", "proofs_per_s_gpu_timed_region",
+                                                                 "proofs_per_s_gpu_with_dispatch_timestamps",
+                                                                 "pass_steps")}
     else:
         res["roofline"] = inflight
     valu_step, valu_tag = pmc_valu_per_step(args.config, len(proofs))
@@ -1315,6 +1363,7 @@ def main():
         sn = [NS.Claim(*c) for c in scl]
         Rs = default_inflight(len(sp))
         sring = [NS.Batch(ctx, gair, stark, sn, spr) for _ in range(Rs)]
+        kernel_timing(sring, region_timing)
         pipelined(sring, args.warmup, Rs, se)
         ctx.synchronize()
         dt, ok3 = pipelined(sring, args.share_steps, Rs, se)

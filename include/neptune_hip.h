@@ -244,6 +244,10 @@ int nhip_batch_run(nhip_ctx *ctx, nhip_batch *batch, uint8_t *verdicts, uint8_t 
 int nhip_batch_launch(nhip_ctx *ctx, nhip_batch *batch);
 int nhip_batch_wait(nhip_ctx *ctx, nhip_batch *batch, uint8_t *verdicts, uint8_t *all_ok);
 int nhip_batch_stats(const nhip_batch *batch, nhip_stats *stats);
+/* Per-dispatch begin / end timestamps on the batch's Merkle hash launches and its row-hashing
+ * launch, read back as nhip_stats.ms_mp_hash_exec / ms_row_hash_exec (0 when off).  Off by
+ * default; a benchmark's kernel timing turns it on.  NHIP_ERR_ARG while the batch is in flight. */
+int nhip_batch_set_launch_timing(nhip_batch *batch, int on);
 /* Fiat-Shamir replay form of later launches, process-wide (tests and A/B runs): -1 = chosen by the
  * batch size (default), 0 = 16-lane row, 1 = two-row pair, 2 = quad.  NHIP_ERR_ARG otherwise. */
 int nhip_set_fs_form(int form);

@@ -150,6 +150,7 @@ struct StarkPhaseTimer {
     hipEvent_t ev[STARK_EVENTS];
     hipEvent_t lev[2 * MAX_HASH_LAUNCHES];  // per hash launch: dispatch begin / end (nullptr = untimed)
     hipEvent_t rev[2] = {nullptr, nullptr};  // the row-hashing launch: dispatch begin / end (nullptr = untimed)
+    bool launch_events = false;  // use lev / rev on this launch (nhip_batch_set_launch_timing)
     uint32_t mp_hash_launches;
     uint32_t aux_after_level = 0;  // hash levels launched before the OOD/FRI/DEEP chain is released
 };

@@ -1050,11 +1050,6 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     }
 
 static int launch_resources(nhip_batch* b);
-// start / stop events on every Merkle hash launch of a resident batch (the bench's roofline timing);
-// 0 builds a variant without them (A/B of their cost)
-#ifndef NHIP_HASH_LAUNCH_EVENTS
-#define NHIP_HASH_LAUNCH_EVENTS 1
-#endif
 
 // A resident batch: prepared, and its launch resources made now rather than at its first launch (a
 // failure there is left to the launch to report)
@@ -1114,13 +1109,13 @@ static int launch_resources(nhip_batch* b) {
         } else {
             for (int i = 0; i < STARK_EVENTS; ++i)
                 if (hipEventCreate(&b->tm.ev[i]) != hipSuccess) return NHIP_ERR_HIP;
-            for (uint32_t i = 0; i < (NHIP_HASH_LAUNCH_EVENTS ? 2 * MAX_HASH_LAUNCHES : 0); ++i)  // per hash launch
+            for (uint32_t i = 0; i < 2 * MAX_HASH_LAUNCHES; ++i)  // per hash launch
                 if (hipEventCreate(&b->tm.lev[i]) != hipSuccess) {
                     for (uint32_t j = 0; j < i; ++j) (void)hipEventDestroy(b->tm.lev[j]);
                     for (uint32_t j = 0; j < 2 * MAX_HASH_LAUNCHES; ++j) b->tm.lev[j] = nullptr;
                     break;  // untimed hash launches: a fault of the timing only
                 }
-            if (NHIP_HASH_LAUNCH_EVENTS) {
+            {
                 hipEvent_t r0 = nullptr, r1 = nullptr;
                 if (hipEventCreate(&r0) == hipSuccess && hipEventCreate(&r1) == hipSuccess) {
                     b->tm.rev[0] = r0;
@@ -1173,6 +1168,15 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
     return NHIP_OK;
 }
 
+// Dispatch begin / end timestamps on the batch's Merkle hash launches and its row launch (the
+// bench's kernel timing: nhip_stats.ms_mp_hash_exec / ms_row_hash_exec); off by default, since
+// they cost a small batch ~2% of its rate and the product paths do not read them.
+int nhip_batch_set_launch_timing(nhip_batch* b, int on) {
+    if (!b || b->in_flight) return NHIP_ERR_ARG;
+    b->tm.launch_events = on != 0;
+    return NHIP_OK;
+}
+
 // Internal (queue.cpp): has every phase of a launched batch completed?  Its last packets (the verdict
 // copy) are on the main stream, which joins the aux chain before them.
 bool nhip_internal_batch_done(nhip_batch* b) {
@@ -1201,16 +1205,18 @@ int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* al
         std::memcpy(&c, b->h_out + OUT_HDR + 4 * i, 4);
         reserved += c;
     }
-    {  // the hash launches' own durations (dispatch begin / end timestamps)
+    {  // the hash launches' own durations (dispatch begin / end timestamps; launch timing on)
         double exec = 0;
-        const uint32_t nl = std::min<uint32_t>(b->tm.mp_hash_launches, MAX_HASH_LAUNCHES);
+        const bool ev = b->tm.launch_events;
+        const uint32_t nl = ev ? std::min<uint32_t>(b->tm.mp_hash_launches, MAX_HASH_LAUNCHES) : 0u;
         for (uint32_t i = 0; i < nl && b->tm.lev[0]; ++i) {
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, b->tm.lev[2 * i], b->tm.lev[2 * i + 1]) == hipSuccess) exec += ms;
         }
         b->mp_hash_exec_ms = exec;
         float rms = 0.f;
-        b->row_hash_exec_ms = b->tm.rev[0] && hipEventElapsedTime(&rms, b->tm.rev[0], b->tm.rev[1]) == hipSuccess ? rms : 0.0;
+        b->row_hash_exec_ms =
+            ev && b->tm.rev[0] && hipEventElapsedTime(&rms, b->tm.rev[0], b->tm.rev[1]) == hipSuccess ? rms : 0.0;
     }
     b->H.perms_static = cnt[CNT_PERMS_STATIC];
     b->H.perms_lcw = cnt[CNT_PERMS_LCW];

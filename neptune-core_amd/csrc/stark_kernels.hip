@@ -1798,12 +1798,13 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
             return v && std::strtoul(v, nullptr, 10) != 0;
         }();
         // dispatch begin / end events (the row kernel's own duration, as the kernel trace has it)
+        hipEvent_t r0 = tm->launch_events ? tm->rev[0] : nullptr, r1 = tm->launch_events ? tm->rev[1] : nullptr;
         if (rows_lds)
-            hipExtLaunchKernelGGL(k_hash_rows_lds<MW>, dim3(gx, 3), dim3(256), 0, st, tm->rev[0], tm->rev[1], 0, b.words,
-                                  b.desc, n, k, b.dims, b.dig, b.fail);
+            hipExtLaunchKernelGGL(k_hash_rows_lds<MW>, dim3(gx, 3), dim3(256), 0, st, r0, r1, 0, b.words, b.desc, n, k,
+                                  b.dims, b.dig, b.fail);
         else
-            hipExtLaunchKernelGGL(k_hash_rows<MW>, dim3(gx, 3), dim3(256), 0, st, tm->rev[0], tm->rev[1], 0, b.words,
-                                  b.desc, n, k, b.dims, b.dig, b.fail);
+            hipExtLaunchKernelGGL(k_hash_rows<MW>, dim3(gx, 3), dim3(256), 0, st, r0, r1, 0, b.words, b.desc, n, k,
+                                  b.dims, b.dig, b.fail);
     }
     mark(2, st);
     if (small) {
@@ -1849,7 +1850,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     if (small) {  // every tree climbed by its own workgroup, one launch
         launch_aux_chain();
         aux_started = true;
-        const bool timed = tm->lev[0] != nullptr;
+        const bool timed = tm->launch_events && tm->lev[0] != nullptr;
         hipExtLaunchKernelGGL(k_mp_climb<MW>, dim3(n, tpp + 1), dim3(MP_CLIMB_THREADS), 0, st,
                               timed ? tm->lev[0] : nullptr, timed ? tm->lev[1] : nullptr, 0, b.words, b.dig, b.mp,
                               tpp, b.desc, n, (const uint32_t*)b.fail, LcwTree{b.lcw, b.max_lcw}, 0u);
@@ -1876,7 +1877,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
             launch_aux_chain();
             aux_started = true;
         }
-        const bool timed = launches < MAX_HASH_LAUNCHES && tm->lev[0] != nullptr;
+        const bool timed = tm->launch_events && launches < MAX_HASH_LAUNCHES && tm->lev[0] != nullptr;
         hipEvent_t e0 = timed ? tm->lev[2 * launches] : nullptr, e1 = timed ? tm->lev[2 * launches + 1] : nullptr;
         {
             // the rest of every tree climbed per (proof, tree group) in one launch once a level is small

@@ -209,6 +209,12 @@ class Batch:
         check(self.ctx.lib.nhip_batch_wait(self.ctx.handle, self.handle, v, ctypes.byref(ok)), "nhip_batch_wait")
         return v[:self.n], bool(ok.value)
 
+    def set_launch_timing(self, on: bool = True) -> "Batch":
+        """Per-dispatch timestamps on the Merkle hash and row launches (stats ms_mp_hash_exec /
+        ms_row_hash_exec); off by default (nhip_batch_set_launch_timing)."""
+        check(self.ctx.lib.nhip_batch_set_launch_timing(self.handle, 1 if on else 0), "nhip_batch_set_launch_timing")
+        return self
+
     def stats(self) -> dict:
         s = _lib.Stats()
         check(self.ctx.lib.nhip_batch_stats(self.handle, ctypes.byref(s)), "nhip_batch_stats")

@@ -273,6 +273,33 @@ def test_async_launch_wait_matches_run(ctx):
     b2.close()
 
 
+def test_launch_timing_switch(ctx):
+    """Per-dispatch timestamps are off by default (the product path: exec times read 0) and on after
+    nhip_batch_set_launch_timing (the bench's kernel timing); the verdicts are the same either way,
+    and the switch is refused while the batch is in flight."""
+    NS = _ns()
+    air_w, pool = _pool()
+    gair = NS.Air([int(w) for w in air_w])
+    b = NS.Batch(ctx, gair, NS.Stark.default(), [NS.Claim(*c) for c, _, _ in pool], [p for _, p, _ in pool])
+    v0, ok0 = b.run()
+    s0 = b.stats()
+    assert s0["ms_mp_hash_exec"] == 0.0 and s0["ms_row_hash_exec"] == 0.0
+    b.set_launch_timing(True)
+    v1, ok1 = b.run()
+    s1 = b.stats()
+    assert s1["ms_mp_hash_exec"] > 0.0 and s1["ms_row_hash_exec"] > 0.0
+    assert list(v0) == list(v1) == [1] * len(pool) and ok0 and ok1
+    b.launch()
+    with pytest.raises(Exception):
+        b.set_launch_timing(False)
+    v2, _ = b.wait()
+    assert list(v2) == list(v1)
+    b.set_launch_timing(False)
+    b.run()
+    assert b.stats()["ms_mp_hash_exec"] == 0.0
+    b.close()
+
+
 def test_empty_and_single_malformed_batches(ctx):
     NS = _ns()
     air_w, pool = _pool()

@@ -5,6 +5,8 @@
 set -o pipefail
 TAG=${1:-r05z}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
+# the box's clocks, power and temperature before anything runs (box-to-box spread of the rates)
+rocm-smi --showclocks --showpower --showtemp --showmaxpower > $OUT/smi_idle.txt 2>&1 || true
 bash tools/gpu_tests.sh $TAG && \
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && tail -1 $OUT/smoke.log && \
 bash tools/profile_round.sh $TAG && \

@@ -70,7 +70,9 @@ if trace and b and b.get("roofline"):
     else:
         ri, rf = b.get("roofline_isolated"), b["roofline"]
     per_step = int(round(rf["launches_per_step"]))
-    timed = b["steps"] * per_step
+    # round 5: roofline.inflight is a pass of `pass_steps` in-flight steps right after the timed
+    # region (which runs without per-dispatch timestamps), before the isolated steps
+    timed = rf.get("pass_steps", b["steps"]) * per_step
     iso = b.get("iso_steps", 5) * per_step if ri else 0
     if iso and len(mh) >= iso:
         i_ = mh[-iso:]
@@ -81,7 +83,7 @@ if trace and b and b.get("roofline"):
     if len(mh) >= timed + iso:
         t = mh[len(mh) - iso - timed:len(mh) - iso]
         avg_ms = sum(t) / len(t) / 1e6
-        print(f"\nMerkle hash launches of the timed steps: {len(t)} calls, trace average {avg_ms:.4f} ms; "
+        print(f"\nMerkle hash launches of the in-flight steps (the timing pass after the timed region; before round 5 the timed steps): {len(t)} calls, trace average {avg_ms:.4f} ms; "
               f"bench kernel_avg_ms (HIP start/stop events per launch) {rf['kernel_avg_ms']:.4f} ms "
               f"({(rf['kernel_avg_ms'] / avg_ms - 1) * 100:+.1f}%), HIP-event span / launches "
               f"{rf.get('kernel_avg_ms_events', float('nan')):.4f} ms")
