@@ -62,6 +62,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config {3,4,5}]
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -299,6 +300,11 @@ def make_batch(pool, collections: int, corrupt_frac: float, seed: int):
     return claims, proofs, np.array(expect, dtype=bool)
 
 
+# exchanges posted before the oldest is completed (shard.VerdictExchange ring; 2 = complete the
+# previous step's right after posting this one's)
+EXCHANGE_DEPTH = 4
+
+
 def kernel_timing(batches, on: bool = True):
     """Per-dispatch timestamps on the Merkle hash and row launches (nhip_batch_set_launch_timing),
     for the kernel-timing passes only: every batch runs without them otherwise, as the product's
@@ -329,27 +335,32 @@ def pipelined(batches, steps: int, inflight: int, expect):
     return time.perf_counter() - t, ok
 
 
-def default_inflight(n: int) -> int:
-    """Steps in flight for an n-proof batch per GPU: 8 from 1,024 proofs, 10 below (the N = 1 / 2 / 4
-    / 8 shares of config 4; config 5's 8-64 proofs: 10 vs 8 in flight +10-11%, profiles/r03s).
-    Round 4, the driver's command (20 timed steps after 5 warm-up steps; `gpurun_out/ab_r04q`):
-    4,096 proofs 461.6-462.0k at 8 in flight vs 453.7-455.9k at 2; 512 proofs 393.7-396.4k at 10,
-    367.6-377.9k at 6, 340.4-345.5k at 4; 200 steps: 4,096 at 8 461.5-463.7k vs 450.1-451.6k at 2
-    (`ab_r04n`, `ab_r04o`).  (Before the library made a batch's streams, events and pinned readback
-    at its preparation, a resident batch whose first launch fell inside the timed region stalled the
-    others: with 5 warm-up steps, 512 proofs ran at 91-93k with 10 in flight.)  More than 11 in
-    flight would take more than the 24 hardware queues below."""
-    return 8 if n >= 1024 else 10
+def default_inflight(n: int, multi_rank: bool = False) -> int:
+    """Steps in flight for an n-proof batch per GPU: 8 from 1,024 proofs, 10 below (9 for a rank of
+    a multi-rank run, whose process also holds torch's and RCCL's streams: see hw_queues_wanted).
+    The N = 1 / 2 / 4 / 8 shares of config 4; config 5's 8-64 proofs: 10 vs 8 in flight +10-11%,
+    profiles/r03s.  Round 4, the driver's command (20 timed steps after 5 warm-up steps;
+    `gpurun_out/ab_r04q`): 4,096 proofs 461.6-462.0k at 8 in flight vs 453.7-455.9k at 2; 512 proofs
+    393.7-396.4k at 10, 367.6-377.9k at 6, 340.4-345.5k at 4; 200 steps: 4,096 at 8 461.5-463.7k vs
+    450.1-451.6k at 2 (`ab_r04n`, `ab_r04o`).  (Before the library made a batch's streams, events
+    and pinned readback at its preparation, a resident batch whose first launch fell inside the
+    timed region stalled the others: with 5 warm-up steps, 512 proofs ran at 91-93k with 10 in
+    flight.)  More in flight would need more than the 22 hardware queues below."""
+    if n >= 1024:
+        return 8
+    return 9 if multi_rank else 10
 
 
 def hw_queues_wanted(inflight: int, multi_rank: bool) -> int:
     """GPU_MAX_HW_QUEUES for R steps in flight: R resident batches x 2 streams + the context stream
     need their own hardware queues (streams sharing a queue serialize; the GPU boxes export HIP's
     default of 4); with several ranks two more for torch's stream and RCCL's, so that no batch stream
-    queues behind a collective waiting for the other ranks.  At least 8, at most 24 (past that the
-    device's queues are time-sliced: profiles/r03j)."""
-    return min(24, max(8, 2 * inflight + 2 + (2 if multi_rank else 0)))
-
+    queues behind a collective waiting for the other ranks.  At least 8, at most 22: a process whose
+    streams occupy more than ~22 hardware queues collapses (round 5, `profiles/r05z/ab/
+    hw_queue_budget_r05.txt`: 11 steps in flight = 23 queues in use, 512 proofs 82k instead of
+    406-416k; one rank of the multi-rank path at 512 proofs, 10 in flight with 24 queues 173-178k,
+    22 queues 367-372k, 9 in flight 377-380k)."""
+    return min(22, max(8, 2 * inflight + 2 + (2 if multi_rank else 0)))
 
 
 def load_pool4():
@@ -950,9 +961,12 @@ def main():
         air_words = np.asarray(S.bloat_air(S.AirCircuit.from_words([int(w) for w in air_words]), 24000).to_words(),
                                dtype=np.uint64)
     n = len(proofs)
-    R = args.inflight or default_inflight(n)
+    # NHIP_BENCH_FORCE_DIST=1 (rehearsal on one GPU): one rank through the multi-rank path (process
+    # group, per-step verdict exchange, its hardware-queue budget), as each rank of an N-GPU run
+    multi = world > 1 or os.environ.get("NHIP_BENCH_FORCE_DIST") == "1"
+    R = args.inflight or default_inflight(n, multi)
     # before anything initialises HIP (nothing above has)
-    want_q = hw_queues_wanted(R, world > 1)
+    want_q = hw_queues_wanted(R, multi)
     if world == 1 and args.config == 4 and total == 4096 and args.share_steps > 0:
         # the share_n8 leg runs the N = 8 rank's 512-proof share at its own depth in this process
         want_q = max(want_q, hw_queues_wanted(default_inflight(total // 8), False))
@@ -991,7 +1005,7 @@ def main():
 
     dist = None
     dev_index = local_rank
-    if world > 1:
+    if multi:
         import torch
         import torch.distributed as dist
         # NHIP_DIST_BACKEND=gloo rehearses the multi-rank logic with several ranks on one GPU
@@ -1001,6 +1015,14 @@ def main():
             dev_index = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(dev_index)
         dist.init_process_group(backend)
+        flags = ctypes.c_uint(0)
+        try:
+            ctypes.CDLL("libamdhip64.so").hipGetDeviceFlags(ctypes.byref(flags))
+        except OSError:
+            pass
+        log(f"[rank {rank}] {backend} process group: {len(os.sched_getaffinity(0))} CPUs in affinity, "
+            f"{len(os.listdir('/proc/self/task'))} threads, HIP device flags {flags.value:#x}, "
+            f"env {sorted(k for k in os.environ if k.startswith(('HIP_', 'HSA_', 'GPU_', 'AMD_', 'ROC')))}")
     import neptune_hip as nh
     import neptune_hip.stark as NS
     from neptune_hip import shard
@@ -1027,7 +1049,10 @@ def main():
     # configs 4 / 5 with several ranks: one all-gather per step carries every rank's batch verdict
     # and per-proof verdicts (shard.VerdictExchange), posted without waiting and completed one step
     # later; config 3 (no per-proof exchange): the all-reduce(MIN) of the batch verdict
-    exch = shard.VerdictExchange(shards, total, dist) if (dist is not None and shards is not None) else None
+    exch = (shard.VerdictExchange(shards, total, dist, depth=EXCHANGE_DEPTH)
+            if (dist is not None and shards is not None) else None)
+    if os.environ.get("NHIP_BENCH_NO_EXCHANGE") == "1":  # A/B only: the multi-rank path without its exchange
+        exch = None
     exchanged = []  # (batch verdict, job verdict vector) of every completed exchange
 
     # NHIP_BENCH_TIMELINE=<file>: host times of every launch and wait return of the timed region
@@ -1057,7 +1082,7 @@ def main():
             launch_one()
         if exch is not None:  # block validation: every rank gets every proof's verdict
             exch.post(ok, v)
-            if len(exch.pending) > 1:
+            if len(exch.pending) >= exch.depth:  # complete step k - depth + 1
                 exchanged.append(exch.complete())
         elif dist is not None:
             ok = shard.all_ok(ok, dist)  # RCCL all-reduce(MIN) of the batch verdict
@@ -1072,7 +1097,8 @@ def main():
         if dist is not None:
             import torch
             torch.cuda.synchronize()
-            dist.barrier()
+            if os.environ.get("NHIP_BENCH_NO_BARRIER") != "1":  # A/B only (one rank): no collective before the region
+                dist.barrier()
 
     # NHIP_BENCH_REGION_TIMING=1 (A/B of their cost): the timed region and the share leg with the
     # per-dispatch timestamps on, as bench.py ran them before round 5

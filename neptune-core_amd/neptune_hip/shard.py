@@ -79,47 +79,71 @@ class VerdictExchange:
     Every rank all-gathers ``[local_ok, verdict bytes of its shard (padded to the widest shard)]``;
     the batch verdict is the MIN of the leading bytes (what ``all_ok``'s all-reduce(MIN) gives) and
     the job's verdict vector is scattered from the rest (what ``gather_verdicts`` gives), so one
-    collective replaces the pair.  ``post`` enqueues the all-gather (``async_op``) on preallocated
-    double buffers and returns at once; ``complete`` waits for the oldest posted exchange and
-    returns ``(batch_ok, verdicts)``.  A caller keeps at most two exchanges posted (post step k,
-    complete step k - 1), so a slow collective never stalls the launch of the next GPU step.
+    collective replaces the pair.  ``post`` enqueues the exchange on a ring of ``depth``
+    preallocated buffers and returns at once; ``complete`` returns the oldest posted exchange's
+    ``(batch_ok, verdicts)``.  A caller keeps at most ``depth`` exchanges posted (bench.py: post step
+    k, complete step k - depth + 1), so a slow collective never stalls the launch of the next GPU
+    step.
+
+    RCCL ("nccl") form: the verdict bytes go through pinned host buffers; post enqueues the copy in,
+    the all_gather_into_tensor, the stream's wait for it and the copy out on torch's current stream
+    and records an event, all without blocking the host; complete waits on that event only.  (Round
+    5: the blocking pageable copies of the first form cost a 512-proof rank ~5% of its rate, the
+    host stalling on each step's exchange instead of relaunching the GPU's next step.)
     """
 
-    def __init__(self, shards: List[List[int]], n: int, dist):
+    def __init__(self, shards: List[List[int]], n: int, dist, depth: int = 2):
         import torch
         self.dist = dist
         self.n = n
+        self.depth = max(2, int(depth))
         self.dev = _device_for(dist)
         self.world = dist.get_world_size()
         self.width = 1 + (max(len(s) for s in shards) if shards else 0)
         self.index = [np.asarray(s, dtype=np.int64) for s in shards]
         # gloo has no all_gather_into_tensor: per-rank views of the flat receive buffer instead
         self.flat = self.dev.type == "cuda"
-        self.send = [torch.zeros(self.width, dtype=torch.uint8, device=self.dev) for _ in range(2)]
-        self.recv = [torch.zeros(self.world * self.width, dtype=torch.uint8, device=self.dev) for _ in range(2)]
+        self.send = [torch.zeros(self.width, dtype=torch.uint8, device=self.dev) for _ in range(self.depth)]
+        self.recv = [torch.zeros(self.world * self.width, dtype=torch.uint8, device=self.dev)
+                     for _ in range(self.depth)]
+        if self.flat:
+            self.send_host = [torch.zeros(self.width, dtype=torch.uint8).pin_memory() for _ in range(self.depth)]
+            self.recv_host = [torch.zeros(self.world * self.width, dtype=torch.uint8).pin_memory()
+                              for _ in range(self.depth)]
+            self.done = [torch.cuda.Event() for _ in range(self.depth)]
         self.pending: List[tuple] = []
         self.slot = 0
 
     def post(self, local_ok: bool, local: np.ndarray) -> None:
         import torch
-        if len(self.pending) >= 2:
-            raise RuntimeError("VerdictExchange: complete() the oldest exchange before posting a third")
+        if len(self.pending) >= self.depth:
+            raise RuntimeError(f"VerdictExchange: complete() the oldest exchange before posting a {self.depth + 1}th")
         s = self.slot
-        self.slot ^= 1
-        host = np.zeros(self.width, dtype=np.uint8)
+        self.slot = (s + 1) % self.depth
+        host = self.send_host[s].numpy() if self.flat else np.zeros(self.width, dtype=np.uint8)
+        host[:] = 0
         host[0] = 1 if local_ok else 0
         host[1:1 + len(local)] = np.asarray(local, dtype=np.uint8)
-        self.send[s].copy_(torch.from_numpy(host))
         if self.flat:
+            self.send[s].copy_(self.send_host[s], non_blocking=True)
             work = self.dist.all_gather_into_tensor(self.recv[s], self.send[s], async_op=True)
+            work.wait()  # the current stream waits for the collective; the host does not
+            self.recv_host[s].copy_(self.recv[s], non_blocking=True)
+            self.done[s].record()
+            self.pending.append((s, None))
         else:
+            self.send[s].copy_(torch.from_numpy(host))
             work = self.dist.all_gather(list(self.recv[s].view(self.world, self.width)), self.send[s], async_op=True)
-        self.pending.append((s, work))
+            self.pending.append((s, work))
 
     def complete(self):
         s, work = self.pending.pop(0)
-        work.wait()
-        got = self.recv[s].view(self.world, self.width).cpu().numpy()
+        if self.flat:
+            self.done[s].synchronize()
+            got = self.recv_host[s].numpy().reshape(self.world, self.width).copy()
+        else:
+            work.wait()
+            got = self.recv[s].view(self.world, self.width).numpy().copy()
         full = np.zeros(self.n, dtype=np.uint8)
         for r, idx in enumerate(self.index):
             if len(idx):

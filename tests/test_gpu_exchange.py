@@ -25,25 +25,26 @@ torch.cuda.set_device(0)
 dist.init_process_group("nccl", init_method="tcp://127.0.0.1:" + sys.argv[2], rank=0, world_size=1)
 n = 300
 shards = [list(range(n))]
-ex = shard.VerdictExchange(shards, n, dist)
-assert ex.flat and ex.dev.type == "cuda"
 steps = []
-for k in range(5):
+for k in range(9):
     v = np.ones(n, dtype=np.uint8)
     v[(17 * k) % n] = 0
     if k == 4:
         v[:] = 1
     steps.append(v)
-got = []
-for v in steps:
-    ex.post(bool(v.all()), v)
-    if len(ex.pending) > 1:
+for depth in (2, 4):  # bench.py posts 4 deep (pinned staging, on-stream copies, one event per slot)
+    ex = shard.VerdictExchange(shards, n, dist, depth=depth)
+    assert ex.flat and ex.dev.type == "cuda"
+    got = []
+    for v in steps:
+        ex.post(bool(v.all()), v)
+        if len(ex.pending) >= depth:
+            got.append(ex.complete())
+    while ex.pending:
         got.append(ex.complete())
-while ex.pending:
-    got.append(ex.complete())
-assert len(got) == len(steps)
-for (ok, full), v in zip(got, steps):
-    assert ok == bool(v.all()) and (full == v).all()
+    assert len(got) == len(steps)
+    for (ok, full), v in zip(got, steps):
+        assert ok == bool(v.all()) and (full == v).all()
 dist.destroy_process_group()
 print("exchange ok")
 '''

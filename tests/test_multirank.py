@@ -125,7 +125,7 @@ def test_two_rank_config4_stark_sharding():
         assert ok is False and all(matches) and sum(sizes) == 48 and gathered_ok
 
 
-def _exchange_worker(rank, world, port, q):
+def _exchange_worker(rank, world, port, q, depth=2):
     sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
@@ -143,16 +143,16 @@ def _exchange_worker(rank, world, port, q):
         if k == 3:
             full[:] = 1
         steps.append(full)
-    ex = shard.VerdictExchange(shards, n, dist)
+    ex = shard.VerdictExchange(shards, n, dist, depth=depth)
     got = []
     for k, full in enumerate(steps):
         v = full[mine]
         ex.post(bool(v.all()), v)
-        if len(ex.pending) > 1:
+        if len(ex.pending) >= depth:
             got.append(ex.complete())
     try:
         ex.post(True, steps[0][mine])
-        ex.post(True, steps[0][mine])  # a third posted exchange is refused
+        ex.post(True, steps[0][mine])  # one posted exchange past the ring's depth is refused
         third = False
     except RuntimeError:
         third = True
@@ -165,16 +165,16 @@ def _exchange_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 8])
-def test_two_rank_verdict_exchange_one_collective(world):
+@pytest.mark.parametrize("world,depth", [(2, 2), (8, 2), (2, 4), (8, 4)])
+def test_two_rank_verdict_exchange_one_collective(world, depth):
     """shard.VerdictExchange at world size 2 and 8 (gloo; 8 = the driver's node, every rank's LPT
     shard of 37 units): one all-gather per step carries the batch verdict (the MIN of every rank's
-    leading byte) and the per-proof verdicts, exchanges posted two at a time complete in posting
+    leading byte) and the per-proof verdicts, exchanges posted two or four deep complete in posting
     order, and the answers equal all_ok + gather_verdicts on every rank."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q, depth)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
