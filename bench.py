@@ -969,7 +969,7 @@ def main():
     want_q = hw_queues_wanted(R, multi)
     if world == 1 and args.config == 4 and total == 4096 and args.share_steps > 0:
         # the share_n8 leg runs the N = 8 rank's 512-proof share at its own depth in this process
-        want_q = max(want_q, hw_queues_wanted(default_inflight(total // 8), False))
+        want_q = max(want_q, hw_queues_wanted(default_inflight(total // 8, True), True))
     if world == 1 and args.config5_proofs > 0:  # the config-5 leg at its own depth
         want_q = max(want_q, hw_queues_wanted(default_inflight(args.config5_proofs), False))
     if os.environ.get("NHIP_BENCH_HWQ"):  # A/B runs: exactly this many
@@ -1387,7 +1387,7 @@ def main():
         sc, sp, se, _, _, _ = make_config4(pool4, total, 0.01, 8, 0)
         scl, spr = device_form(sc, sp, mont)
         sn = [NS.Claim(*c) for c in scl]
-        Rs = default_inflight(len(sp))
+        Rs = default_inflight(len(sp), multi_rank=True)  # the rank's own depth (its process also holds RCCL's streams)
         sring = [NS.Batch(ctx, gair, stark, sn, spr) for _ in range(Rs)]
         kernel_timing(sring, region_timing)
         pipelined(sring, args.warmup, Rs, se)
@@ -1398,7 +1398,9 @@ def main():
         sh = {"proofs_per_step": len(sp), "inflight": Rs, "steps": args.share_steps, "warmup": args.warmup,
               "value": len(sp) * args.share_steps / dt, "unit": "proofs/s (one GPU)",
               "ms_per_step": dt / args.share_steps * 1e3, "verdicts_correct": ok3,
-              "measured": "rank 0 of 8's LPT shard of the 4,096-proof job, resident, the timed region's shape"}
+              "measured": "rank 0 of 8's LPT shard of the 4,096-proof job, resident, the timed region's shape at "
+                          "the rank's depth; without the rank's process group and verdict exchange (their cost "
+                          "at this size: DESIGN.md section 6)"}
         sh["vs_value_per_proof"] = sh["value"] / res["value"]
         res["share_n8"] = sh
         correct = correct and ok3
