@@ -13,10 +13,13 @@ One step = whole verification of the rank's batch from its raw proof words in HB
 decode on the device (k_decode: ProofStream::try_from + the dequeue order of Stark::verify, every
 step again), Fiat-Shamir replay, row hashing, Merkle multiproofs, OOD AIR evaluation, FRI, DEEP, the
 verdict copy back (nhip_batch_launch / nhip_batch_wait) and, for N > 1, the verdict exchange: configs
-4 / 5 one RCCL all-gather per step of [batch verdict byte, per-proof verdict bytes] (the batch
-verdict is the MIN of the leading bytes; block validation needs every transaction's verdict:
-SURVEY.md §8e), posted without waiting and completed one step later, the last one inside the timed
-region (shard.VerdictExchange); config 3 one all-reduce(MIN) of the batch verdict.  Steps are pipelined as a node verifying a stream
+4 / 5 one all-gather per step of [batch verdict byte, per-proof verdict bytes] over the host (gloo:
+the verdicts are host bytes; the batch verdict is the MIN of the leading bytes; block validation
+needs every transaction's verdict: SURVEY.md §8e), posted without waiting and completed three steps
+later, the last ones inside the timed region (shard.VerdictExchange); config 3 one all-reduce(MIN)
+of the batch verdict per step.  After the timed region ONE RCCL all-reduce over xGMI carries the
+job's verdict AND and the max over ranks of the region's time (an RCCL communicator alive during
+the region costs a 512-proof rank ~6%: DESIGN.md §6).  Steps are pipelined as a node verifying a stream
 of batches runs them (--inflight; 8 from 1,024 proofs per GPU, 10 below): resident copies rotate, step k+1 is launched before step k
 is waited on, so one step's latency-bound phases overlap the other's VALU-bound hashing; every timed
 step is launched and waited inside the timed region.  Two copies x 2 streams need more than HIP's
@@ -1008,10 +1011,16 @@ def main():
     if multi:
         import torch
         import torch.distributed as dist
-        # NHIP_DIST_BACKEND=gloo rehearses the multi-rank logic with several ranks on one GPU
-        # (collectives on host tensors); the default is RCCL ("nccl") over xGMI
-        backend = os.environ.get("NHIP_DIST_BACKEND", "nccl")
-        if backend != "nccl":
+        # The per-step verdict exchange runs on the host (gloo): the verdicts are host bytes after
+        # every step's wait, and an RCCL communicator alive in the process costs a 512-proof rank ~6%
+        # of its rate with no collective running.  The job's verdict AND (with the
+        # timing's max over ranks) is ONE RCCL all-reduce over xGMI after the timed region, on a group
+        # made there.  NHIP_DIST_BACKEND=nccl runs the per-step exchange on RCCL device buffers
+        # instead; NHIP_FINAL_BACKEND=gloo keeps the final all-reduce on the host (several ranks on
+        # one GPU: RCCL refuses two ranks on one device).
+        backend = os.environ.get("NHIP_DIST_BACKEND", "gloo")
+        final_backend = os.environ.get("NHIP_FINAL_BACKEND", "nccl")
+        if backend != "nccl" and final_backend != "nccl":
             dev_index = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(dev_index)
         dist.init_process_group(backend)
@@ -1184,10 +1193,21 @@ def main():
 
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed, 0.0 if correct else 1.0], dtype=torch.float64, device=shard._device_for(dist))
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, any_bad = float(t[0].item()), float(t[1].item())
+        # ONE all-reduce(MAX) over [elapsed, any rank wrong, NOT the job's verdict] = the max over
+        # ranks of the timed region and the job's logical AND: RCCL over xGMI (a group made here,
+        # after every timed region of the run), or on the exchange's group when that is RCCL already
+        if final_backend == "nccl" and backend != "nccl":
+            grp, fdev = dist.new_group(backend="nccl"), torch.device("cuda", dev_index)
+        else:
+            grp, fdev = None, shard._device_for(dist)
+        t = torch.tensor([elapsed, 0.0 if correct else 1.0, 0.0 if batch_ok else 1.0], dtype=torch.float64,
+                         device=fdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=grp)
+        elapsed, any_bad, not_ok = float(t[0].item()), float(t[1].item()), float(t[2].item())
         correct = any_bad == 0.0
+        batch_ok = not_ok == 0.0
+        final_collective = {"backend": "nccl" if grp is not None else dist.get_backend(),
+                            "op": "all_reduce(MAX) of [elapsed, any rank wrong, NOT job verdict]"}
     perms_rank = (acc.get("tip5_perms_static", 0.0) + acc.get("tip5_perms_merkle", 0.0)) / max(args.steps, 1)
     perms_job = perms_rank
     if dist is not None:
@@ -1288,7 +1308,12 @@ def main():
                    "input": "HBM-resident raw proof words (uploaded before the timed region; decoded on the "
                             "device every step)",
                    "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
-                   "lib_sha256": lib_sha256()[:16]},
+                   "lib_sha256": lib_sha256()[:16],
+                   "verdict_exchange": (None if dist is None else
+                                        {"per_step": f"{dist.get_backend()} all-gather of [batch verdict, "
+                                                     f"per-proof verdicts] (shard.VerdictExchange, "
+                                                     f"{EXCHANGE_DEPTH} deep)",
+                                         "final": final_collective})},
         # what one step is: the raw proof words are resident in HBM when the step starts; the step
         # decodes every proof stream on the device (k_decode) and runs every verifier phase
         "step": "device proof-stream decode + Fiat-Shamir replay + row hashing + Merkle multiproofs + OOD AIR + "
