@@ -1023,6 +1023,9 @@ def main():
         if backend != "nccl" and final_backend != "nccl":
             dev_index = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(dev_index)
+        if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
+            # one node: gloo over the loopback device (the container's hostname may not resolve)
+            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         dist.init_process_group(backend)
         flags = ctypes.c_uint(0)
         try:
