@@ -338,6 +338,16 @@ def pipelined(batches, steps: int, inflight: int, expect):
     return time.perf_counter() - t, ok
 
 
+# batches of at most this many proofs run every phase on one stream (nhip_batch_set_streams) at
+# twice the depth: config 5's 8 / 64 proofs +17% / +13%; config 4's 512-4,096 lose 10-23% that way
+# (profiles/r05z/ab/single_stream_ab_r05l.txt)
+SINGLE_STREAM_MAX_PROOFS = 64
+
+
+def streams_for(n: int) -> int:
+    return 1 if n <= SINGLE_STREAM_MAX_PROOFS else 2
+
+
 def default_inflight(n: int, multi_rank: bool = False) -> int:
     """Steps in flight for an n-proof batch per GPU: 8 from 1,024 proofs, 10 below (9 for a rank of
     a multi-rank run, whose process also holds torch's and RCCL's streams: see hw_queues_wanted).
@@ -351,10 +361,12 @@ def default_inflight(n: int, multi_rank: bool = False) -> int:
     flight.)  More in flight would need more than the 22 hardware queues below."""
     if n >= 1024:
         return 8
+    if streams_for(n) == 1:  # one stream per batch: twice the depth in the same hardware queues
+        return 18 if multi_rank else 20
     return 9 if multi_rank else 10
 
 
-def hw_queues_wanted(inflight: int, multi_rank: bool) -> int:
+def hw_queues_wanted(inflight: int, multi_rank: bool, streams: int = 2) -> int:
     """GPU_MAX_HW_QUEUES for R steps in flight: R resident batches x 2 streams + the context stream
     need their own hardware queues (streams sharing a queue serialize; the GPU boxes export HIP's
     default of 4); with several ranks two more for torch's stream and RCCL's, so that no batch stream
@@ -363,7 +375,7 @@ def hw_queues_wanted(inflight: int, multi_rank: bool) -> int:
     hw_queue_budget_r05.txt`: 11 steps in flight = 23 queues in use, 512 proofs 82k instead of
     406-416k; one rank of the multi-rank path at 512 proofs, 10 in flight with 24 queues 173-178k,
     22 queues 367-372k, 9 in flight 377-380k)."""
-    return min(22, max(8, 2 * inflight + 2 + (2 if multi_rank else 0)))
+    return min(22, max(8, streams * inflight + 2 + (2 if multi_rank else 0)))
 
 
 def load_pool4():
@@ -564,7 +576,8 @@ def config5_leg(ctx, gair, stark, proofs_n: int = 64, steps: int = 20, inflight:
     dcl, dpr = device_form([claim], [proof], stark.input_form == 1)
     ncl = [NS.Claim(*dcl[0])] * proofs_n
     prs = [np.array(dpr[0], dtype=np.uint64, copy=True) for _ in range(proofs_n)]
-    ring = [NS.Batch(ctx, gair, stark, ncl, prs) for _ in range(inflight)]
+    nstreams = int(os.environ.get("NHIP_BENCH_C5_STREAMS", "0")) or streams_for(proofs_n)  # A/B: 2 = two streams
+    ring = [NS.Batch(ctx, gair, stark, ncl, prs).set_streams(nstreams) for _ in range(inflight)]
     ok = True
     # alone: phase split and the transcript
     v, _ = ring[0].run()
@@ -603,6 +616,7 @@ def config5_leg(ctx, gair, stark, proofs_n: int = 64, steps: int = 20, inflight:
             "proof": "tests/golden/deep_fri.npz height 23 (sparse synthetic prover: non-zero FRI codewords)",
             "proof_words": int(proof.size), "value": proofs_n * steps / dt, "unit": "proofs/s",
             "ms_per_step": dt / steps * 1e3, "steps": steps, "inflight": inflight,
+            "streams_per_batch": nstreams,
             "alone_ms": {k[3:]: round(alone[k], 4) for k in ("ms_device_decode", "ms_fiat_shamir", "ms_row_hash",
                                                                "ms_merkle", "ms_ood_air", "ms_fri", "ms_deep",
                                                                "ms_device_total")},
@@ -917,6 +931,8 @@ def main():
                     help="config 4 at N = 1: timed steps of the N = 8 rank's 512-proof share (0 = skip)")
     ap.add_argument("--queue-callers", type=int, default=64,
                     help="queue leg at N = 1: concurrent single-proof callers through nhip_queue (0 = skip)")
+    ap.add_argument("--config5-inflight", type=int, default=None,
+                    help="steps in flight of the config-5 leg (default: the bench's depth for its size)")
     ap.add_argument("--config5-proofs", type=int, default=64,
                     help="config-5 leg at N = 1: proofs at log2 padded height 23 (0 = skip)")
     ap.add_argument("--stream-batches", type=int, default=6,
@@ -969,12 +985,13 @@ def main():
     multi = world > 1 or os.environ.get("NHIP_BENCH_FORCE_DIST") == "1"
     R = args.inflight or default_inflight(n, multi)
     # before anything initialises HIP (nothing above has)
-    want_q = hw_queues_wanted(R, multi)
+    want_q = hw_queues_wanted(R, multi, streams_for(n))
     if world == 1 and args.config == 4 and total == 4096 and args.share_steps > 0:
         # the share_n8 leg runs the N = 8 rank's 512-proof share at its own depth in this process
         want_q = max(want_q, hw_queues_wanted(default_inflight(total // 8, True), True))
     if world == 1 and args.config5_proofs > 0:  # the config-5 leg at its own depth
-        want_q = max(want_q, hw_queues_wanted(default_inflight(args.config5_proofs), False))
+        want_q = max(want_q, hw_queues_wanted(default_inflight(args.config5_proofs), False,
+                                              streams_for(args.config5_proofs)))
     if os.environ.get("NHIP_BENCH_HWQ"):  # A/B runs: exactly this many
         os.environ["GPU_MAX_HW_QUEUES"] = os.environ["NHIP_BENCH_HWQ"]
     elif int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < want_q:
@@ -1049,7 +1066,7 @@ def main():
     stark = NS.Stark.default().montgomery() if mont else NS.Stark.default()
     ncl = [NS.Claim(*c) for c in dev_claims]
     # R resident copies of the raw proof words (each step decodes them on the device again)
-    ring = [NS.Batch(ctx, gair, stark, ncl, dev_proofs) for _ in range(R)]
+    ring = [NS.Batch(ctx, gair, stark, ncl, dev_proofs).set_streams(streams_for(n)) for _ in range(R)]
     prep_s = time.time() - t0
     st0 = ring[0].stats()
     log(f"[rank {rank}] batch ready: {n} proofs x {R} resident copies, {st0['proof_words']} words, "
@@ -1446,7 +1463,7 @@ def main():
         log(f"[queue] {res['queue']['value']:.0f} proofs/s ({time.time() - t:.1f}s)")
     if world == 1 and args.config5_proofs > 0:
         t = time.time()
-        res["config5"] = config5_leg(ctx, gair, stark, args.config5_proofs)
+        res["config5"] = config5_leg(ctx, gair, stark, args.config5_proofs, inflight=args.config5_inflight)
         correct = correct and res["config5"]["verdicts_correct"]
         log(f"[config5] {res['config5']['value']:.0f} proofs/s ({time.time() - t:.1f}s)")
     if world == 1 and args.config1_seconds > 0 and not args.no_cpu:

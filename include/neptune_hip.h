@@ -248,6 +248,10 @@ int nhip_batch_stats(const nhip_batch *batch, nhip_stats *stats);
  * launch, read back as nhip_stats.ms_mp_hash_exec / ms_row_hash_exec (0 when off).  Off by
  * default; a benchmark's kernel timing turns it on.  NHIP_ERR_ARG while the batch is in flight. */
 int nhip_batch_set_launch_timing(nhip_batch *batch, int on);
+/* 2 (default): the batch's latency-bound chain and its hashing run on two streams and overlap; 1:
+ * every phase in order on one stream (one hardware queue), so twice as many batches fit in flight —
+ * for many tiny batches at once (e.g. 8-64 proofs each).  NHIP_ERR_ARG while in flight. */
+int nhip_batch_set_streams(nhip_batch *batch, int streams);
 /* Fiat-Shamir replay form of later launches, process-wide (tests and A/B runs): -1 = chosen by the
  * batch size (default), 0 = 16-lane row, 1 = two-row pair, 2 = quad.  NHIP_ERR_ARG otherwise. */
 int nhip_set_fs_form(int form);

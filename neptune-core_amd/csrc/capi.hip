@@ -143,7 +143,7 @@ extern "C" {
 // 2100: nhip_stats.ms_row_hash_exec (the struct grew), the NUMA entry points (nhip_host_alloc_near,
 // nhip_device_numa, nhip_numa_from_sysfs, nhip_cpulist_parse, nhip_host_page_node,
 // nhip_set_host_threads)
-// 2200: nhip_batch_set_launch_timing (per-dispatch timestamps off by default)
+// 2200: nhip_batch_set_launch_timing (per-dispatch timestamps off by default), nhip_batch_set_streams
 int nhip_abi_version(void) { return 2200; }
 
 int nhip_set_fs_form(int form) { return nhip::set_fs_form(form) == 0 ? NHIP_OK : NHIP_ERR_ARG; }

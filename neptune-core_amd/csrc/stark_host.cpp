@@ -1050,7 +1050,6 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
     }
 
 static int launch_resources(nhip_batch* b);
-
 // A resident batch: prepared, and its launch resources made now rather than at its first launch (a
 // failure there is left to the launch to report)
 static int prepare_resident(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
@@ -1174,6 +1173,28 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
 int nhip_batch_set_launch_timing(nhip_batch* b, int on) {
     if (!b || b->in_flight) return NHIP_ERR_ARG;
     b->tm.launch_events = on != 0;
+    return NHIP_OK;
+}
+
+// One stream or two for a resident batch.  Two (the default): the latency-bound chain (decode,
+// Fiat-Shamir replay, plan, OOD / FRI / DEEP) and the VALU-bound hashing overlap within the batch.
+// One: every phase in order on the main stream, one hardware queue per batch, so a caller can keep
+// twice as many batches in flight — the better trade for tiny batches run many at a time
+// (BASELINE config 5's 8-64 proofs per GPU: +12-18% at twice the depth), the worse one from a few
+// hundred proofs on (config 4 at 512-4,096 proofs: -10 to -23%).
+int nhip_batch_set_streams(nhip_batch* b, int streams) {
+    if (!b || b->in_flight || b->scratch || (streams != 1 && streams != 2)) return NHIP_ERR_ARG;
+    const DeviceScope device_scope(b->device);
+    if (int rc = launch_resources(b)) return rc;
+    if (streams == 1 && b->aux != b->main) {
+        (void)hipStreamSynchronize(b->aux);
+        (void)hipStreamDestroy(b->aux);
+        b->aux = b->main;
+    } else if (streams == 2 && b->aux == b->main) {
+        hipStream_t s2 = nullptr;
+        if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
+        b->aux = s2;
+    }
     return NHIP_OK;
 }
 
@@ -1328,8 +1349,8 @@ void nhip_batch_destroy(nhip_batch* b) {
         for (hipEvent_t e : b->tm.rev)
             if (e) (void)hipEventDestroy(e);
     }
+    if (b->aux && b->aux != b->main) (void)hipStreamDestroy(b->aux);
     if (b->main) (void)hipStreamDestroy(b->main);
-    if (b->aux) (void)hipStreamDestroy(b->aux);
     if (b->h_out) (void)hipHostFree(b->h_out);
     if (b->dmem) (void)hipFree(b->dmem);
     if (b->dwords) (void)hipFree(b->dwords);

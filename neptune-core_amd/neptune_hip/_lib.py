@@ -189,6 +189,7 @@ SIGNATURES = {
     "nhip_batch_stats": ([_vp, ctypes.POINTER(Stats)], ctypes.c_int),
     "nhip_set_fs_form": ([ctypes.c_int], ctypes.c_int),
     "nhip_batch_set_launch_timing": ([_vp, ctypes.c_int], ctypes.c_int),
+    "nhip_batch_set_streams": ([_vp, ctypes.c_int], ctypes.c_int),
     "nhip_batch_transcript": ([_vp, _vp, _sz, _u64p, _sz, ctypes.POINTER(ctypes.c_uint32), _sz,
                                ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "nhip_batch_destroy": ([_vp], None),

@@ -215,6 +215,13 @@ class Batch:
         check(self.ctx.lib.nhip_batch_set_launch_timing(self.handle, 1 if on else 0), "nhip_batch_set_launch_timing")
         return self
 
+    def set_streams(self, streams: int) -> "Batch":
+        """2 (default): the latency-bound chain and the hashing overlap on two streams; 1: every
+        phase in order on one stream, so twice as many tiny batches fit in flight
+        (nhip_batch_set_streams)."""
+        check(self.ctx.lib.nhip_batch_set_streams(self.handle, int(streams)), "nhip_batch_set_streams")
+        return self
+
     def stats(self) -> dict:
         s = _lib.Stats()
         check(self.ctx.lib.nhip_batch_stats(self.handle, ctypes.byref(s)), "nhip_batch_stats")

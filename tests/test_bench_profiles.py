@@ -119,12 +119,14 @@ def test_inflight_defaults_and_queue_budget():
     stream keeps its own queue, and no process asks for more than the 22 past which the device
     collapses (a rank of a multi-rank run also holds torch's and RCCL's streams: 9 in flight at
     512 proofs instead of 10)."""
-    assert [bench.default_inflight(n) for n in (4096, 2048, 1024, 512, 64, 8)] == [8, 8, 8, 10, 10, 10]
-    assert [bench.default_inflight(n, True) for n in (4096, 2048, 1024, 512, 64, 8)] == [8, 8, 8, 9, 9, 9]
+    assert [bench.default_inflight(n) for n in (4096, 2048, 1024, 512, 64, 8)] == [8, 8, 8, 10, 20, 20]
+    assert [bench.default_inflight(n, True) for n in (4096, 2048, 1024, 512, 64, 8)] == [8, 8, 8, 9, 18, 18]
+    assert [bench.streams_for(n) for n in (4096, 512, 65, 64, 8)] == [2, 2, 2, 1, 1]
     for n in (4096, 2048, 1024, 512, 64, 8):
         for multi in (False, True):
             r = bench.default_inflight(n, multi)
-            q = bench.hw_queues_wanted(r, multi)
-            streams = 2 * r + 1 + (2 if multi else 0)  # batch streams, the context's, torch + RCCL
+            k = bench.streams_for(n)  # one stream per batch for the tiny ones
+            q = bench.hw_queues_wanted(r, multi, k)
+            streams = k * r + 1 + (2 if multi else 0)  # batch streams, the context's, torch + RCCL
             assert 8 <= q <= 22 and q >= streams, (n, multi, q, streams)
     assert bench.hw_queues_wanted(16, True) == 22

@@ -300,6 +300,40 @@ def test_launch_timing_switch(ctx):
     b.close()
 
 
+def test_one_stream_batches(ctx):
+    """nhip_batch_set_streams: every phase on one stream gives the two-stream verdicts and
+    Fiat-Shamir transcripts (mutated proofs included), one-stream batches run concurrently, and the
+    switch back to two streams and the refusal while in flight hold."""
+    NS = _ns()
+    air_w, pool = _pool()
+    gair = NS.Air([int(w) for w in air_w])
+    stark = NS.Stark.default()
+    claims = [NS.Claim(*c) for c, _, _ in pool]
+    proofs = [p for _, p, _ in pool]
+    bad = []
+    for _, p, (lo, hi) in pool:
+        m = p.copy()
+        m[(lo + hi) // 2] = np.uint64((int(m[(lo + hi) // 2]) + 7) % S.P)
+        bad.append(m)
+    two = NS.Batch(ctx, gair, stark, claims + claims, proofs + bad)
+    v2, _ = two.run()
+    ones = [NS.Batch(ctx, gair, stark, claims + claims, proofs + bad).set_streams(1) for _ in range(3)]
+    for b in ones:
+        b.launch()
+    with pytest.raises(Exception):
+        ones[0].set_streams(2)
+    for b in ones:
+        v1, _ = b.wait()
+        assert list(v1) == list(v2) == [1] * len(pool) + [0] * len(pool)
+    for i in range(len(pool)):
+        assert ones[1].transcript(i) == two.transcript(i)
+    ones[2].set_streams(2)
+    v3, _ = ones[2].run()
+    assert list(v3) == list(v2)
+    for b in ones + [two]:
+        b.close()
+
+
 def test_empty_and_single_malformed_batches(ctx):
     NS = _ns()
     air_w, pool = _pool()
