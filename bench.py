@@ -349,8 +349,10 @@ def streams_for(n: int) -> int:
 
 
 def default_inflight(n: int, multi_rank: bool = False) -> int:
-    """Steps in flight for an n-proof batch per GPU: 8 from 1,024 proofs, 10 below (9 for a rank of
-    a multi-rank run, whose process also holds torch's and RCCL's streams: see hw_queues_wanted).
+    """Steps in flight for an n-proof batch per GPU: 8 from 1,024 proofs, 10 below (9 for a rank
+    whose per-step exchange runs on RCCL, NHIP_DIST_BACKEND=nccl: its process then also holds
+    torch's and RCCL's streams during the timed region, see hw_queues_wanted; `multi_rank` means
+    that case; the default host exchange holds none).
     The N = 1 / 2 / 4 / 8 shares of config 4; config 5's 8-64 proofs: 10 vs 8 in flight +10-11%,
     profiles/r03s.  Round 4, the driver's command (20 timed steps after 5 warm-up steps;
     `gpurun_out/ab_r04q`): 4,096 proofs 461.6-462.0k at 8 in flight vs 453.7-455.9k at 2; 512 proofs
@@ -983,12 +985,15 @@ def main():
     # NHIP_BENCH_FORCE_DIST=1 (rehearsal on one GPU): one rank through the multi-rank path (process
     # group, per-step verdict exchange, its hardware-queue budget), as each rank of an N-GPU run
     multi = world > 1 or os.environ.get("NHIP_BENCH_FORCE_DIST") == "1"
-    R = args.inflight or default_inflight(n, multi)
+    # torch's and RCCL's streams live in the process during the timed region only when the per-step
+    # exchange runs on RCCL (NHIP_DIST_BACKEND=nccl); the default host exchange adds none
+    gpu_exchange = multi and os.environ.get("NHIP_DIST_BACKEND", "gloo") == "nccl"
+    R = args.inflight or default_inflight(n, gpu_exchange)
     # before anything initialises HIP (nothing above has)
-    want_q = hw_queues_wanted(R, multi, streams_for(n))
+    want_q = hw_queues_wanted(R, gpu_exchange, streams_for(n))
     if world == 1 and args.config == 4 and total == 4096 and args.share_steps > 0:
         # the share_n8 leg runs the N = 8 rank's 512-proof share at its own depth in this process
-        want_q = max(want_q, hw_queues_wanted(default_inflight(total // 8, True), True))
+        want_q = max(want_q, hw_queues_wanted(default_inflight(total // 8), False))
     if world == 1 and args.config5_proofs > 0:  # the config-5 leg at its own depth
         want_q = max(want_q, hw_queues_wanted(default_inflight(args.config5_proofs), False,
                                               streams_for(args.config5_proofs)))
@@ -1432,7 +1437,7 @@ def main():
         sc, sp, se, _, _, _ = make_config4(pool4, total, 0.01, 8, 0)
         scl, spr = device_form(sc, sp, mont)
         sn = [NS.Claim(*c) for c in scl]
-        Rs = default_inflight(len(sp), multi_rank=True)  # the rank's own depth (its process also holds RCCL's streams)
+        Rs = default_inflight(len(sp))  # the rank's own depth (its default host exchange holds no GPU streams)
         sring = [NS.Batch(ctx, gair, stark, sn, spr) for _ in range(Rs)]
         kernel_timing(sring, region_timing)
         pipelined(sring, args.warmup, Rs, se)
