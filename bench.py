@@ -1030,6 +1030,7 @@ def main():
 
     dist = None
     dev_index = local_rank
+    gpu_shared = False  # several ranks on one GPU (the gloo rehearsals)
     if multi:
         import torch
         import torch.distributed as dist
@@ -1044,6 +1045,7 @@ def main():
         final_backend = os.environ.get("NHIP_FINAL_BACKEND", "nccl")
         if backend != "nccl" and final_backend != "nccl":
             dev_index = local_rank % max(1, torch.cuda.device_count())
+            gpu_shared = world > max(1, torch.cuda.device_count())
         torch.cuda.set_device(dev_index)
         if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
             # one node: gloo over the loopback device (the container's hostname may not resolve)
@@ -1370,7 +1372,10 @@ def main():
         res["roofline"] = roofline(acc_iso, iso_steps, iso_ms, 1,
                                    f"the kernel's own rate: {iso_steps} steps one at a time right after the timed "
                                    f"region; per-launch HIP events (hipExtLaunchKernel start/stop)")
-        assert res["roofline"]["launches_x_avg_ms"] <= step_ms, (res["roofline"], step_ms)
+        if gpu_shared:  # ranks time-sharing one GPU (a rehearsal): the other ranks' steps stretch these
+            res["roofline"]["gpu_shared_by_ranks"] = world
+        else:
+            assert res["roofline"]["launches_x_avg_ms"] <= step_ms, (res["roofline"], step_ms)
         # the row-hashing launch of the same isolated steps (k_hash_rows: one lane per revealed row,
         # every main / aux / quotient row's hash_varlen; dispatch begin / end events), beside the
         # Merkle launches: permutations per launch = proofs x checks x sum over the three trees of
