@@ -933,6 +933,8 @@ def main():
                     help="config 4 at N = 1: timed steps of the N = 8 rank's 512-proof share (0 = skip)")
     ap.add_argument("--queue-callers", type=int, default=64,
                     help="queue leg at N = 1: concurrent single-proof callers through nhip_queue (0 = skip)")
+    ap.add_argument("--no-rank-path", dest="rank_path", action="store_false",
+                    help="skip share_n8.rank_path (the share size through the multi-rank path in a child)")
     ap.add_argument("--config5-inflight", type=int, default=None,
                     help="steps in flight of the config-5 leg (default: the bench's depth for its size)")
     ap.add_argument("--config5-proofs", type=int, default=64,
@@ -1022,6 +1024,37 @@ def main():
                 "gpu_max_hw_queues": h["config"]["gpu_max_hw_queues"], "verdicts_correct": h["verdicts_correct"],
                 "measured": "child process before this one initialised HIP, same workload, NHIP_BENCH_HWQ=4"}
         log(f"[hwq4] {h['value']:.0f} proofs/s at 4 hardware queues ({time.time() - t:.1f}s)")
+    rank_path = None
+    if (world == 1 and args.config == 4 and total == 4096 and args.share_steps > 0 and args.rank_path
+            and not os.environ.get("NHIP_BENCH_FORCE_DIST")):
+        # the N = 8 rank's share size through the multi-rank path itself (process group, host
+        # exchange, one RCCL all-reduce after the region) at world size 1: a child under
+        # torch.distributed.run, started before this process touches the GPU
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__),
+               "--gpus", "1", "--proofs", str(total // 8), "--steps", str(args.share_steps), "--warmup",
+               str(args.warmup), "--no-cpu", "--paths-log2", "0", "--stream-batches", "0", "--group-batches", "0",
+               "--config1-seconds", "0", "--product-steps", "0", "--share-steps", "0", "--queue-callers", "0",
+               "--config5-proofs", "0", "--air", args.air, "--input-form", args.input_form]
+        t = time.time()
+        try:
+            out = subprocess.run(cmd, env=dict(os.environ, NHIP_BENCH_FORCE_DIST="1"), stdout=subprocess.PIPE,
+                                 stderr=subprocess.DEVNULL, timeout=600, check=True)
+            h = json.loads(out.stdout.decode().strip().splitlines()[-1])
+            rank_path = {"value": h["value"], "ms_per_step": h["ms_per_step"], "steps": h["steps"],
+                         "inflight": h["inflight"], "verdicts_correct": h["verdicts_correct"],
+                         "verdict_exchange": h["config"].get("verdict_exchange"),
+                         "measured": f"a {total // 8}-proof config-4 job (the N = 8 rank's share size) in a child "
+                                     "under torch.distributed.run at world size 1 with NHIP_BENCH_FORCE_DIST=1: "
+                                     "the rank's process group, per-step exchange and final all-reduce"}
+            log(f"[rank path] {h['value']:.0f} proofs/s ({time.time() - t:.1f}s)")
+        except (subprocess.SubprocessError, ValueError, KeyError, IndexError) as e:
+            rank_path = {"error": f"{type(e).__name__}: {e}"[:300]}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         t = time.time()
@@ -1457,6 +1490,11 @@ def main():
                           "the rank's depth; without the rank's process group and verdict exchange (their cost "
                           "at this size: DESIGN.md section 6)"}
         sh["vs_value_per_proof"] = sh["value"] / res["value"]
+        if rank_path is not None:
+            if "value" in rank_path:
+                rank_path["vs_value_per_proof"] = rank_path["value"] / res["value"]
+                correct = correct and rank_path["verdicts_correct"]
+            sh["rank_path"] = rank_path
         res["share_n8"] = sh
         correct = correct and ok3
     _assert_fracs(res)
