@@ -1079,7 +1079,8 @@ def main():
         if backend != "nccl" and final_backend != "nccl":
             dev_index = local_rank % max(1, torch.cuda.device_count())
             gpu_shared = world > max(1, torch.cuda.device_count())
-        torch.cuda.set_device(dev_index)
+        if os.environ.get("NHIP_BENCH_NO_SET_DEVICE") != "1":  # A/B only (one rank, host collectives only)
+            torch.cuda.set_device(dev_index)
         if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
             # one node: gloo over the loopback device (the container's hostname may not resolve)
             os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
@@ -1120,7 +1121,8 @@ def main():
     # later; config 3 (no per-proof exchange): the all-reduce(MIN) of the batch verdict
     exch = (shard.VerdictExchange(shards, total, dist, depth=EXCHANGE_DEPTH)
             if (dist is not None and shards is not None) else None)
-    if os.environ.get("NHIP_BENCH_NO_EXCHANGE") == "1":  # A/B only: the multi-rank path without its exchange
+    no_exchange = os.environ.get("NHIP_BENCH_NO_EXCHANGE", "0")  # A/B only (one rank): 1 = all_ok per step, 2 = nothing
+    if no_exchange != "0":
         exch = None
     exchanged = []  # (batch verdict, job verdict vector) of every completed exchange
 
@@ -1153,8 +1155,8 @@ def main():
             exch.post(ok, v)
             if len(exch.pending) >= exch.depth:  # complete step k - depth + 1
                 exchanged.append(exch.complete())
-        elif dist is not None:
-            ok = shard.all_ok(ok, dist)  # RCCL all-reduce(MIN) of the batch verdict
+        elif dist is not None and no_exchange != "2":
+            ok = shard.all_ok(ok, dist)  # all-reduce(MIN) of the batch verdict
         return st, v, ok
 
     def drain_exchange():
