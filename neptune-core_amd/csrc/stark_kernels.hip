@@ -31,6 +31,33 @@ namespace nhip {
 __device__ __forceinline__ void latency_priority() {
     if constexpr (NHIP_LAT_PRIO > 0) __builtin_amdgcn_s_setprio(NHIP_LAT_PRIO);
 }
+// Oldest-first wave priority: the AGE_PRIO_OLDEST oldest batch launches in flight on the device run
+// their sponge replay, row hashing and Merkle levels one priority level above their kernel's base,
+// so the in-flight steps drift apart (the oldest finishes first) instead of moving through their
+// phases in lockstep.  Measured (profiles/r05z/ab/age_prio_ab_r05w.txt, 3
+// repetitions x 2 runs): config 4 at 4,096 proofs in the driver's 20 steps +0.9-1.2%, 1,024 / 2,048
+// equal, 512 -1 to -2%, so from AGE_PRIO_MIN_PROOFS on.  g_batches_done counts the device's
+// finished batch launches (k_verdicts); a launch's seq is its place in the device's launch order.
+static constexpr uint32_t AGE_PRIO_OLDEST = 2;
+static constexpr uint32_t AGE_PRIO_MIN_PROOFS = 4096;
+__device__ uint32_t g_batches_done;
+struct AgePrio {
+    uint32_t seq, k;
+};
+__device__ __forceinline__ void age_priority(AgePrio a, int base) {
+    bool old = false;
+    if (a.k) {  // uniform: a kernel argument
+        const uint32_t done = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&g_batches_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        old = (int32_t)(a.seq - done) < (int32_t)a.k;
+    }
+    switch (base + (old ? 1 : 0)) {
+        case 0: break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
 // wave priority of the lane-per-op Merkle level kernel (the level chain is each step's critical
 // path once its sponge replay is done; the row hashing has slack)
 #ifndef NHIP_MP_PRIO
@@ -142,8 +169,8 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
                                                         const ProofDesc* __restrict__ desc,
                                                         const FsOp* __restrict__ ops, uint32_t n_proofs,
                                                         uint64_t* __restrict__ xs, uint32_t* __restrict__ idx_out,
-                                                        const uint32_t* __restrict__ fail) {
-    latency_priority();
+                                                        const uint32_t* __restrict__ fail, AgePrio age) {
+    age_priority(age, NHIP_LAT_PRIO);
     __shared__ Tip5Lds lds;
     tip5_lds_init(lds);
     constexpr uint32_t LANES = PAIR ? 32u : 16u;
@@ -226,8 +253,8 @@ __global__ void __launch_bounds__(1024) k_fs_replay_quad(const uint64_t* __restr
                                                        const ProofDesc* __restrict__ desc,
                                                        const FsOp* __restrict__ ops, uint32_t n_proofs,
                                                        uint64_t* __restrict__ xs, uint32_t* __restrict__ idx_out,
-                                                       const uint32_t* __restrict__ fail) {
-    if constexpr (NHIP_QUAD_PRIO > 0) __builtin_amdgcn_s_setprio(NHIP_QUAD_PRIO);
+                                                       const uint32_t* __restrict__ fail, AgePrio age) {
+    age_priority(age, NHIP_QUAD_PRIO);
     __shared__ Tip5Lds lds;
     __shared__ uint64_t rck[80];
     for (int i = threadIdx.x; i < 80; i += blockDim.x) rck[i] = c_tip5_rck_raw[i];
@@ -310,7 +337,9 @@ __global__ void __launch_bounds__(1024) k_fs_replay_quad(const uint64_t* __restr
 template <bool MW>
 __global__ void __launch_bounds__(256, NHIP_ROWS_WAVES) k_hash_rows(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
                                                    uint32_t n_proofs, uint32_t k, StarkDims dims,
-                                                   uint64_t* __restrict__ dig, const uint32_t* __restrict__ fail) {
+                                                   uint64_t* __restrict__ dig, const uint32_t* __restrict__ fail,
+                                                   AgePrio age) {
+    age_priority(age, 0);
     __shared__ Tip5Lds lds;
     tip5_lds_init(lds);
     const uint32_t tree = blockIdx.y;
@@ -773,11 +802,11 @@ template <int WAVES, bool MW>
 __global__ void __launch_bounds__(256, WAVES) k_mp_hash(const uint64_t* __restrict__ words, const uint64_t* __restrict__ dig,
                                                  MpPlan plan, uint32_t lvl, uint32_t mp_blocks,
                                                  const ProofDesc* __restrict__ desc, uint32_t n_proofs,
-                                                 const uint32_t* __restrict__ fail, LcwTree lcw) {
+                                                 const uint32_t* __restrict__ fail, LcwTree lcw, AgePrio age) {
     __shared__ Tip5Lds t5;
     __shared__ uint64_t s_base[MP_SHARDS + 1];
     __shared__ uint32_t s_cnt[MP_SHARDS];
-    if constexpr (NHIP_MP_PRIO > 0) __builtin_amdgcn_s_setprio(NHIP_MP_PRIO);
+    age_priority(age, NHIP_MP_PRIO);
     const bool is_lcw = blockIdx.x >= mp_blocks;  // uniform per block
     if (!is_lcw) {
         if (threadIdx.x < MP_SHARDS) {
@@ -1657,6 +1686,7 @@ __global__ void __launch_bounds__(256, NHIP_DEEP_WAVES) k_deep_rows8(const uint6
 __global__ void k_verdicts(const uint32_t* __restrict__ fail, uint32_t n, uint8_t* __restrict__ v) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = fail[i] == 0 ? 1 : 0;
+    if (i == 0) atomicAdd(&g_batches_done, 1u);  // the batch's last kernel: one more finished launch
 }
 
 // ------------------------------------------------------------------ launchers
@@ -1750,6 +1780,18 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     // DEEP (which needs both) waits for it.  With the climb that short, OOD -> FRI -> DEEP in a row
     // would be the critical path.
     const bool small = n <= climb_max_proofs();
+    // this launch's place in the device's launch order, for the oldest-first priority: the 2 oldest
+    // batches in flight one level up, for batches of at least AGE_PRIO_MIN_PROOFS (NHIP_AGE_PRIO=k
+    // sets k for every size, 0 = off)
+    static const int64_t age_env = [] {
+        const char* e = std::getenv("NHIP_AGE_PRIO");
+        return e ? (int64_t)std::strtoul(e, nullptr, 10) : (int64_t)-1;
+    }();
+    const uint32_t age_k = age_env >= 0 ? (uint32_t)age_env : (n >= AGE_PRIO_MIN_PROOFS ? AGE_PRIO_OLDEST : 0u);
+    static std::atomic<uint32_t> seq_ctr[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const AgePrio age{seq_ctr[(uint32_t)dev & 63u].fetch_add(1u, std::memory_order_relaxed), age_k};
     // fork: the aux stream starts after everything already queued on st (counter resets)
     mark(12, st);
     (void)hipStreamWaitEvent(sa, tm->ev[12], 0);
@@ -1770,16 +1812,16 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     const FsForm ff = fs_form(n);
     if (ff == FS_PAIR)
         hipLaunchKernelGGL((k_fs_replay_wide<true, MW>), dim3((n * 32 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
-                           b.ops, n, b.xs, b.idx, b.fail);
+                           b.ops, n, b.xs, b.idx, b.fail, age);
     else if (ff == FS_QUAD)
         hipLaunchKernelGGL(k_fs_replay_quad<MW>, dim3((n * 4 + quad_wg() - 1) / quad_wg()), dim3(quad_wg()), 0, sa, b.words, b.desc, b.ops, n,
-                           b.xs, b.idx, b.fail);
+                           b.xs, b.idx, b.fail, age);
     else if (n < fs_row_lat_max())
         hipLaunchKernelGGL((k_fs_replay_wide<false, MW, true>), dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words,
-                           b.desc, b.ops, n, b.xs, b.idx, b.fail);
+                           b.desc, b.ops, n, b.xs, b.idx, b.fail, age);
     else
         hipLaunchKernelGGL((k_fs_replay_wide<false, MW>), dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
-                           b.ops, n, b.xs, b.idx, b.fail);
+                           b.ops, n, b.xs, b.idx, b.fail, age);
     mark(1, sa);
     if (k <= 128)
         hipLaunchKernelGGL(k_mp_plan<128>, dim3(n, 1 + b.max_R), dim3(128), 0, sa, b.words, b.desc, n, k, tpp, b.dig,
@@ -1804,7 +1846,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
                                   b.dims, b.dig, b.fail);
         else
             hipExtLaunchKernelGGL(k_hash_rows<MW>, dim3(gx, 3), dim3(256), 0, st, r0, r1, 0, b.words, b.desc, n, k,
-                                  b.dims, b.dig, b.fail);
+                                  b.dims, b.dig, b.fail, age);
     }
     mark(2, st);
     if (small) {
@@ -1913,10 +1955,10 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
                                   st, e0, e1, 0, b.words, b.dig, b.mp, l, cap, b.desc, n, (const uint32_t*)b.fail, lcw);
         else if (n < mp_small_max)
             hipExtLaunchKernelGGL((k_mp_hash<NHIP_MP_WAVES_SMALL, MW>), dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0,
-                                  e1, 0, b.words, b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw);
+                                  e1, 0, b.words, b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw, age);
         else
             hipExtLaunchKernelGGL((k_mp_hash<NHIP_MP_WAVES, MW>), dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0, e1, 0,
-                                  b.words, b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw);
+                                  b.words, b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw, age);
         ++launches;
     }
     if (!aux_started) launch_aux_chain();
