@@ -32,14 +32,16 @@ __device__ __forceinline__ void latency_priority() {
     if constexpr (NHIP_LAT_PRIO > 0) __builtin_amdgcn_s_setprio(NHIP_LAT_PRIO);
 }
 // Oldest-first wave priority: the AGE_PRIO_OLDEST oldest batch launches in flight on the device run
-// their sponge replay, row hashing and Merkle levels one priority level above their kernel's base,
-// so the in-flight steps drift apart (the oldest finishes first) instead of moving through their
-// phases in lockstep.  Measured (profiles/r05z/ab/age_prio_ab_r05w.txt, 3
-// repetitions x 2 runs): config 4 at 4,096 proofs in the driver's 20 steps +0.9-1.2%, 1,024 / 2,048
-// equal, 512 -1 to -2%, so from AGE_PRIO_MIN_PROOFS on.  g_batches_done counts the device's
-// finished batch launches (k_verdicts); a launch's seq is its place in the device's launch order.
+// their row hashing and Merkle levels one priority level above their kernel's base (the sponge
+// replay keeps its own), so the in-flight steps drift apart (the oldest finishes first) instead of
+// moving through their phases in lockstep.  Measured
+// (profiles/r05z/ab/age_prio_ab_r05w.txt, 3 alternating repetitions per run): config 4 in the
+// driver's 20 steps at 4,096 proofs +1.4%, 2,048 +0.9%, 1,024 and 512 equal (raising the sponge too:
+// 4,096 +1.2-1.5%, 512 -1 to -2%), so from AGE_PRIO_MIN_PROOFS on.  g_batches_done counts the
+// device's finished batch launches (k_verdicts); a launch's seq is its place in the device's launch
+// order.
 static constexpr uint32_t AGE_PRIO_OLDEST = 2;
-static constexpr uint32_t AGE_PRIO_MIN_PROOFS = 4096;
+static constexpr uint32_t AGE_PRIO_MIN_PROOFS = 2048;
 __device__ uint32_t g_batches_done;
 struct AgePrio {
     uint32_t seq, k;
@@ -1781,8 +1783,8 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     // would be the critical path.
     const bool small = n <= climb_max_proofs();
     // this launch's place in the device's launch order, for the oldest-first priority: the 2 oldest
-    // batches in flight one level up, for batches of at least AGE_PRIO_MIN_PROOFS (NHIP_AGE_PRIO=k
-    // sets k for every size, 0 = off)
+    // batches in flight one level up, for batches of at least AGE_PRIO_MIN_PROOFS (A/B knobs:
+    // NHIP_AGE_PRIO=k sets k for every size, 0 = off; NHIP_AGE_PRIO_FS=1 raises the sponge too)
     static const int64_t age_env = [] {
         const char* e = std::getenv("NHIP_AGE_PRIO");
         return e ? (int64_t)std::strtoul(e, nullptr, 10) : (int64_t)-1;
@@ -1792,6 +1794,11 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     int dev = 0;
     (void)hipGetDevice(&dev);
     const AgePrio age{seq_ctr[(uint32_t)dev & 63u].fetch_add(1u, std::memory_order_relaxed), age_k};
+    static const bool age_fs = [] {  // NHIP_AGE_PRIO_FS=1 (A/B): the sponge replay raised as well
+        const char* e = std::getenv("NHIP_AGE_PRIO_FS");
+        return e && e[0] == '1';
+    }();
+    const AgePrio age_sponge{age.seq, age_fs ? age.k : 0u};
     // fork: the aux stream starts after everything already queued on st (counter resets)
     mark(12, st);
     (void)hipStreamWaitEvent(sa, tm->ev[12], 0);
@@ -1812,16 +1819,16 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     const FsForm ff = fs_form(n);
     if (ff == FS_PAIR)
         hipLaunchKernelGGL((k_fs_replay_wide<true, MW>), dim3((n * 32 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
-                           b.ops, n, b.xs, b.idx, b.fail, age);
+                           b.ops, n, b.xs, b.idx, b.fail, age_sponge);
     else if (ff == FS_QUAD)
         hipLaunchKernelGGL(k_fs_replay_quad<MW>, dim3((n * 4 + quad_wg() - 1) / quad_wg()), dim3(quad_wg()), 0, sa, b.words, b.desc, b.ops, n,
                            b.xs, b.idx, b.fail, age);
     else if (n < fs_row_lat_max())
         hipLaunchKernelGGL((k_fs_replay_wide<false, MW, true>), dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words,
-                           b.desc, b.ops, n, b.xs, b.idx, b.fail, age);
+                           b.desc, b.ops, n, b.xs, b.idx, b.fail, age_sponge);
     else
         hipLaunchKernelGGL((k_fs_replay_wide<false, MW>), dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
-                           b.ops, n, b.xs, b.idx, b.fail, age);
+                           b.ops, n, b.xs, b.idx, b.fail, age_sponge);
     mark(1, sa);
     if (k <= 128)
         hipLaunchKernelGGL(k_mp_plan<128>, dim3(n, 1 + b.max_R), dim3(128), 0, sa, b.words, b.desc, n, k, tpp, b.dig,
