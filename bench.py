@@ -20,12 +20,13 @@ later, the last ones inside the timed region (shard.VerdictExchange); config 3 o
 of the batch verdict per step.  After the timed region ONE RCCL all-reduce over xGMI carries the
 job's verdict AND and the max over ranks of the region's time (an RCCL communicator alive during
 the region costs a 512-proof rank ~6%: DESIGN.md §6).  Steps are pipelined as a node verifying a stream
-of batches runs them (--inflight; 8 from 1,024 proofs per GPU, 10 below): resident copies rotate, step k+1 is launched before step k
-is waited on, so one step's latency-bound phases overlap the other's VALU-bound hashing; every timed
-step is launched and waited inside the timed region.  Two copies x 2 streams need more than HIP's
-default 4 hardware queues per process, so GPU_MAX_HW_QUEUES is raised here before HIP starts (to
-2 x in-flight + 2, at least 8, at most 24); the library's nhip_init provisions 8 when the variable is
-unset.
+of batches runs them (--inflight; 8 from 1,024 proofs per GPU, 10 below, 20 on one stream each up to
+64 proofs): resident copies rotate, step k+1 is launched before step k is waited on, so one step's
+latency-bound phases overlap the other's VALU-bound hashing; every timed step is launched and waited
+inside the timed region.  The copies' streams need more than HIP's default 4 hardware queues per
+process, so GPU_MAX_HW_QUEUES is raised here before HIP starts (to streams x in-flight + 2, at least
+8, at most 22: past that a process collapses); the library's nhip_init provisions 8 when the
+variable is unset.
 The default timed region is 200 steps (~2 s of sustained load).
 
 Defaults (round 4): the AIR is the synthetic constraints bloated to triton-air's size class
