@@ -1259,18 +1259,27 @@ def main():
         # ONE all-reduce(MAX) over [elapsed, any rank wrong, NOT the job's verdict] = the max over
         # ranks of the timed region and the job's logical AND: RCCL over xGMI (a group made here,
         # after every timed region of the run), or on the exchange's group when that is RCCL already
+        vals = [elapsed, 0.0 if correct else 1.0, 0.0 if batch_ok else 1.0]
+        grp, final_error = None, None
         if final_backend == "nccl" and backend != "nccl":
-            grp, fdev = dist.new_group(backend="nccl"), torch.device("cuda", dev_index)
-        else:
-            grp, fdev = None, shard._device_for(dist)
-        t = torch.tensor([elapsed, 0.0 if correct else 1.0, 0.0 if batch_ok else 1.0], dtype=torch.float64,
-                         device=fdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=grp)
+            try:
+                import datetime
+                grp = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=180))
+                t = torch.tensor(vals, dtype=torch.float64, device=torch.device("cuda", dev_index))
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=grp)
+            except Exception as e:  # noqa: BLE001 - the timing must survive an RCCL fault
+                grp, final_error = None, f"{type(e).__name__}: {e}"[:300]
+                log(f"[rank {rank}] RCCL all-reduce failed ({final_error}); reducing on the host group")
+        if grp is None:
+            t = torch.tensor(vals, dtype=torch.float64, device=shard._device_for(dist))
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, any_bad, not_ok = float(t[0].item()), float(t[1].item()), float(t[2].item())
         correct = any_bad == 0.0
         batch_ok = not_ok == 0.0
         final_collective = {"backend": "nccl" if grp is not None else dist.get_backend(),
                             "op": "all_reduce(MAX) of [elapsed, any rank wrong, NOT job verdict]"}
+        if final_error:
+            final_collective["rccl_error"] = final_error
     perms_rank = (acc.get("tip5_perms_static", 0.0) + acc.get("tip5_perms_merkle", 0.0)) / max(args.steps, 1)
     perms_job = perms_rank
     if dist is not None:
