@@ -179,6 +179,15 @@ typedef struct nhip_batch nhip_batch;
 
 void nhip_stark_params_default(nhip_stark_params *out);
 int nhip_air_create(const uint64_t *words, size_t n_words, nhip_air **out);
+/* The OOD program compiler's options (0 = the default for each): LDS-held value slots (fewer puts the
+ * rest in the per-proof global area), instructions per program step, working-slot budget.  Tests of
+ * the compiler and of k_ood_air's global-slot path; nhip_air_create(w, n, out) = _ex(w, n, NULL, out). */
+typedef struct {
+    uint32_t lds_slots;
+    uint32_t step_width;   /* 16 .. 65536 */
+    uint32_t slot_budget;  /* >= 64 */
+} nhip_air_options;
+int nhip_air_create_ex(const uint64_t *words, size_t n_words, const nhip_air_options *options, nhip_air **out);
 void nhip_air_destroy(nhip_air *air);
 int nhip_air_info(const nhip_air *air, uint32_t *num_nodes, uint32_t *num_levels, uint32_t *num_constraints);
 /* The OOD evaluator's value slots (liveness-allocated): those in LDS, and those past the LDS budget
@@ -255,6 +264,10 @@ int nhip_batch_set_streams(nhip_batch *batch, int streams);
 /* Fiat-Shamir replay form of later launches, process-wide (tests and A/B runs): -1 = chosen by the
  * batch size (default), 0 = 16-lane row, 1 = two-row pair, 2 = quad.  NHIP_ERR_ARG otherwise. */
 int nhip_set_fs_form(int form);
+/* Merkle climb-from threshold of later launches, process-wide (tests): -1 = the default (trees of
+ * at least 24 hash levels hand their remaining levels to one per-tree climb launch at the first level
+ * with at most 4,096 hash ops), 0 = never, k > 0 = at k ops for every depth. */
+int nhip_set_climb_from_ops(int64_t ops);
 /* Samples squeezed for proof `proof` in squeeze order (challenges, quotient weights, z, linear-
  * combination weights, FRI folding challenges, last-round indeterminate) as canonical XFE
  * triples, the FRI indices, and the proof's failure bits (0 = accepted). */
@@ -296,6 +309,10 @@ typedef struct {
                                 from there without a staging copy on the worker) */
 } nhip_queue_profile;
 int nhip_queue_profile_read(const nhip_queue *queue, nhip_queue_profile *out, int reset);
+/* Per-request latency in microseconds (a caller's arrival in nhip_queue_verify -> its verdicts
+ * delivered), the last 65,536 requests oldest first: *n = how many are held; up to cap written.
+ * reset != 0 forgets them. */
+int nhip_queue_latencies(const nhip_queue *queue, float *us_out, size_t cap, size_t *n, int reset);
 /* Drains the pending requests, then stops the worker. */
 void nhip_queue_destroy(nhip_queue *queue);
 
@@ -337,6 +354,12 @@ int nhip_group_stream_create(nhip_group *group, nhip_air *air, const nhip_stark_
                              nhip_group_stream **out);
 int nhip_group_stream_submit(nhip_group_stream *stream, const nhip_claim *claims, const nhip_proof *proofs,
                              size_t n, uint8_t *verdicts, uint8_t *all_ok);
+/* nhip_group_stream_submit with the caller's placement: proof i goes to member member_of[i] (< the
+ * group's size) instead of nhip_group_shard's.  For proofs decoded into a member's arena
+ * (nhip_arena_ingest_*, which return that placement): each member's share then lies adjacent in
+ * pinned memory on its GPU's node and is DMA'd as it lies. */
+int nhip_group_stream_submit_placed(nhip_group_stream *stream, const nhip_claim *claims, const nhip_proof *proofs,
+                                    const uint32_t *member_of, size_t n, uint8_t *verdicts, uint8_t *all_ok);
 /* Waits for the last submitted batch and writes its verdicts. */
 int nhip_group_stream_finish(nhip_group_stream *stream);
 /* Host / device milliseconds of the stream's batches so far (summed over members: stage = host
@@ -413,6 +436,44 @@ int nhip_tx_scan(const uint8_t *bytes, size_t n_bytes, nhip_tx *tx);
  * type_script_hashes, kernel_mast_hash, salted_inputs_hash, salted_outputs_hash, merge_bit_mast_path. */
 int nhip_tx_parts(const uint8_t *bytes, size_t n_bytes, const nhip_tx *tx, uint64_t *seq_words,
                   uint64_t seq_offsets[9], uint64_t *proof_spans, uint64_t *digests);
+
+/* ---- per-member proof arenas: wire bytes decoded straight into pinned memory per GPU (§8f row 2)
+ * The receive side of the feed path.  An arena set holds, for every member of a group, bytes_per_member
+ * of pinned host memory on that member GPU's NUMA node (nhip_host_alloc_near).  The ingest functions
+ * scan bincode bytes (blk files: import_blocks_from_files.rs:100-115; peer TransferTransactions:
+ * transfer_transaction.rs:31-47), give each proof to the least-loaded member with room (by words) and
+ * decode its words (8-byte little-endian, reduced mod p: nhip_le_words, i.e. canonical values ->
+ * nhip_stark_params.input_form NHIP_INPUT_CANONICAL) straight into that member's arena, on copy
+ * threads bound to the member's node (NHIP_HOST_THREADS, else the group's share per member).  They
+ * return nhip_proof records pointing into the arenas and each proof's member, ready for
+ * nhip_group_stream_submit_placed.  The arena's proofs stay valid until nhip_arena_reset; reset only
+ * after the submit of the batch holding them has returned (its words are then on the devices).
+ * Double-buffer with two arena sets to decode batch k + 1 while batch k uploads. */
+typedef struct nhip_arena nhip_arena;
+int nhip_arena_create(nhip_group *group, size_t bytes_per_member, nhip_arena **out);
+void nhip_arena_destroy(nhip_arena *arena);
+int nhip_arena_reset(nhip_arena *arena);
+/* words placed since the last reset, capacity in words, and the NUMA node of the member's pages
+ * (-1: unknown); each output nullable */
+int nhip_arena_member_info(const nhip_arena *arena, size_t member, uint64_t *used_words, uint64_t *cap_words,
+                           int *page_node);
+/* Proofs given as n (byte offset, word count) pairs `spans` of bytes[n_bytes].  NHIP_ERR_OOM when an
+ * arena cannot take a proof (the ones before it are placed and decoded). */
+int nhip_arena_ingest_spans(nhip_arena *arena, const uint8_t *bytes, size_t n_bytes, const uint64_t *spans, size_t n,
+                            nhip_proof *proofs, uint32_t *member_of);
+/* Back-to-back TransferTransactions: up to max_txs of them, every proof (a SingleProof's one, a
+ * ProofCollection's in field order) in stream order.  Stops early with NHIP_OK, before the
+ * transaction that does not fit, when proof_cap or the arenas are full (*consumed < n_bytes: submit,
+ * reset, continue from there); NHIP_ERR_DECODE at a malformed transaction (those before it are placed
+ * and counted).  *n_txs, *n_proofs, *consumed nullable. */
+int nhip_arena_ingest_txs(nhip_arena *arena, const uint8_t *bytes, size_t n_bytes, size_t max_txs, nhip_proof *proofs,
+                          uint32_t *member_of, size_t proof_cap, size_t *n_txs, size_t *n_proofs, size_t *consumed);
+/* A blk file's bytes: the SingleProof block proof of every block (block_of[i] = its block's index;
+ * nullable).  A malformed block fails the whole file (NHIP_ERR_DECODE, nothing placed); NHIP_ERR_ARG
+ * when proof_cap is short of the file's SingleProof blocks, NHIP_ERR_OOM when the arenas are. */
+int nhip_arena_ingest_blocks(nhip_arena *arena, const uint8_t *bytes, size_t n_bytes, uint32_t pow_tree_height,
+                             nhip_proof *proofs, uint32_t *member_of, uint64_t *block_of, size_t proof_cap,
+                             size_t *n_proofs, size_t *n_blocks);
 
 /* ---- proof of work (neptune-core/src/protocol/consensus/block/pow.rs) ---
  * PowMastPaths (pow.rs:202-207): MAST authentication paths of the pow field (BlockHeader, 3),

@@ -512,3 +512,20 @@ int nhip_tx_parts(const uint8_t* bytes, size_t n_bytes, const nhip_tx* tx, uint6
 }
 
 }  // extern "C"
+
+namespace nhip {
+// The proof spans of the TransferTransaction at the start of bytes[0, n) (arena.cpp): (byte offset
+// from `bytes`, words) per proof in ProofCollection field order, appended to `spans`, and its size.
+bool tx_proof_spans(const uint8_t* bytes, size_t n, std::vector<uint64_t>& spans, uint64_t& size) {
+    size_t ends[8];
+    nhip_tx t;
+    Rd probe{bytes, n, 0};
+    if (!parse_tx(probe, &t, nullptr, ends, nullptr, nullptr)) return false;  // sizes first
+    const size_t base = spans.size();
+    spans.resize(base + 2ull * t.n_proofs);
+    Rd r{bytes, n, 0};
+    if (!parse_tx(r, &t, nullptr, ends, spans.data() + base, nullptr)) return false;
+    size = t.size;
+    return true;
+}
+}  // namespace nhip

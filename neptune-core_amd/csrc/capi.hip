@@ -144,9 +144,12 @@ extern "C" {
 // nhip_device_numa, nhip_numa_from_sysfs, nhip_cpulist_parse, nhip_host_page_node,
 // nhip_set_host_threads)
 // 2200: nhip_batch_set_launch_timing (per-dispatch timestamps off by default), nhip_batch_set_streams
-int nhip_abi_version(void) { return 2200; }
+// 2300: nhip_air_create_ex (compiler options instead of environment variables), nhip_set_climb_from_ops,
+// the per-member proof arenas (nhip_arena_*, nhip_group_stream_submit_placed)
+int nhip_abi_version(void) { return 2300; }
 
 int nhip_set_fs_form(int form) { return nhip::set_fs_form(form) == 0 ? NHIP_OK : NHIP_ERR_ARG; }
+int nhip_set_climb_from_ops(int64_t ops) { return nhip::set_climb_from_ops(ops) == 0 ? NHIP_OK : NHIP_ERR_ARG; }
 
 const char* nhip_strerror(int code) {
     switch (code) {

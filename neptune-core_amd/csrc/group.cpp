@@ -24,12 +24,9 @@
 #include <vector>
 
 #include "../../include/neptune_hip.h"
+#include "group.hpp"
 #include "host_numa.hpp"
 
-struct nhip_group {
-    std::vector<nhip_ctx*> members;
-    std::vector<std::vector<int>> cpus;  // per member: its GPU's NUMA-node CPUs (empty: unknown)
-};
 
 // Each member's host work on its GPU's NUMA node: the member threads a group starts are bound to
 // the node's CPUs, and the node's CPUs are divided among the members on it for their staging copy
@@ -38,6 +35,7 @@ struct nhip_group {
 static void place_members(nhip_group* g) {
     const size_t M = g->members.size();
     g->cpus.assign(M, {});
+    if (!nhip::numa_enabled()) return;  // NHIP_NUMA=0: no binding and the default copy threads
     std::vector<int> node(M, -1);
     for (size_t m = 0; m < M; ++m) {
         size_t n = 0;
@@ -343,11 +341,14 @@ int nhip_group_stream_create(nhip_group* g, nhip_air* air, const nhip_stark_para
     return NHIP_OK;
 }
 
-int nhip_group_stream_submit(nhip_group_stream* st, const nhip_claim* claims, const nhip_proof* proofs, size_t n,
-                             uint8_t* verdicts, uint8_t* all_ok) {
+static int stream_submit(nhip_group_stream* st, const nhip_claim* claims, const nhip_proof* proofs,
+                         const uint32_t* placed, size_t n, uint8_t* verdicts, uint8_t* all_ok) {
     if (!st) return NHIP_ERR_ARG;
     if (n && (!claims || !proofs || !verdicts)) return NHIP_ERR_ARG;
     const size_t M = st->m.size();
+    if (placed)
+        for (size_t i = 0; i < n; ++i)
+            if (placed[i] >= M) return NHIP_ERR_ARG;
     const int s = (int)(st->next & 1u), sp = s ^ 1;
     try {
         StreamBatch& B = st->sb[s];
@@ -355,7 +356,9 @@ int nhip_group_stream_submit(nhip_group_stream* st, const nhip_claim* claims, co
         B.all_ok = all_ok;
         B.n = n;
         std::vector<uint32_t> member_of(n);
-        int rc = nhip_group_shard(proofs, n, M, member_of.data());
+        int rc = NHIP_OK;
+        if (placed) std::copy(placed, placed + n, member_of.begin());  // the caller's placement (arenas)
+        else rc = nhip_group_shard(proofs, n, M, member_of.data());
         if (rc) return rc;
         for (auto& v : B.idx) v.clear();
         for (size_t i = 0; i < n; ++i) B.idx[member_of[i]].push_back(i);
@@ -412,6 +415,17 @@ int nhip_group_stream_submit(nhip_group_stream* st, const nhip_claim* claims, co
         return NHIP_ERR_OOM;
     }
     return NHIP_OK;
+}
+
+int nhip_group_stream_submit(nhip_group_stream* st, const nhip_claim* claims, const nhip_proof* proofs, size_t n,
+                             uint8_t* verdicts, uint8_t* all_ok) {
+    return stream_submit(st, claims, proofs, nullptr, n, verdicts, all_ok);
+}
+
+int nhip_group_stream_submit_placed(nhip_group_stream* st, const nhip_claim* claims, const nhip_proof* proofs,
+                                    const uint32_t* member_of, size_t n, uint8_t* verdicts, uint8_t* all_ok) {
+    if (n && !member_of) return NHIP_ERR_ARG;
+    return stream_submit(st, claims, proofs, member_of, n, verdicts, all_ok);
 }
 
 int nhip_group_stream_finish(nhip_group_stream* st) {

@@ -46,7 +46,7 @@ bool read_small_file(const std::string& path, std::string& out) {
     return true;
 }
 
-constexpr int MPOL_DEFAULT_ = 0, MPOL_BIND_ = 2;
+constexpr int MPOL_DEFAULT_ = 0, MPOL_PREFERRED_ = 1;
 constexpr int MAX_NODES = 1024;
 
 long sys_get_mempolicy(int* mode, unsigned long* mask, unsigned long maxnode, void* addr, unsigned long flags) {
@@ -109,6 +109,14 @@ HostTopo topo_from_sysfs(const char* root, const char* bus_id) {
     return t;
 }
 
+unsigned host_threads_env() {
+    static const unsigned v = [] {
+        const char* e = std::getenv("NHIP_HOST_THREADS");
+        return e ? (unsigned)std::strtoul(e, nullptr, 10) : 0u;
+    }();
+    return v;
+}
+
 bool numa_enabled() {
     static const bool on = [] {
         const char* v = std::getenv("NHIP_NUMA");
@@ -152,11 +160,14 @@ hipError_t host_malloc_on(void** p, size_t bytes, int node, unsigned flags) {
     const bool have_old = sys_get_mempolicy(&old_mode, old_mask, MAX_NODES, nullptr, 0) == 0;
     unsigned long mask[MAX_NODES / (8 * sizeof(unsigned long))] = {0};
     mask[node / (8 * sizeof(unsigned long))] |= 1ul << (node % (8 * sizeof(unsigned long)));
-    if (sys_set_mempolicy(MPOL_BIND_, mask, MAX_NODES) != 0) return hipHostMalloc(p, bytes, flags);
+    // preferred, not bound: the pages land on the GPU's node while it has free memory and on another
+    // node otherwise (a strict bind of locked pages on a full node would wake the OOM killer instead
+    // of failing the allocation)
+    if (sys_set_mempolicy(MPOL_PREFERRED_, mask, MAX_NODES) != 0) return hipHostMalloc(p, bytes, flags);
     hipError_t e = hipHostMalloc(p, bytes, flags | hipHostMallocNumaUser);
     if (have_old) (void)sys_set_mempolicy(old_mode, old_mode == MPOL_DEFAULT_ ? nullptr : old_mask, MAX_NODES);
     else (void)sys_set_mempolicy(MPOL_DEFAULT_, nullptr, 0);
-    if (e != hipSuccess) e = hipHostMalloc(p, bytes, flags);  // placement is a preference
+    if (e != hipSuccess) e = hipHostMalloc(p, bytes, flags);
     return e;
 }
 

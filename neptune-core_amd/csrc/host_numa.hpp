@@ -21,6 +21,9 @@ HostTopo topo_from_sysfs(const char* root, const char* bus_id);
 HostTopo device_topo(int device);
 // NHIP_NUMA unset or non-zero
 bool numa_enabled();
+// the operator's NHIP_HOST_THREADS (0 = unset): host copy threads per upload / ingest, taking
+// precedence over the count a group sets per member (nhip_set_host_threads)
+unsigned host_threads_env();
 // bind the calling thread to `cpus` (no-op when empty or disabled); true if bound
 bool bind_thread(const std::vector<int>& cpus);
 // pinned host memory (hipHostMalloc `flags`) with its pages on `node` (< 0 or disabled: no placement)

@@ -5,6 +5,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "ab_env.hpp"
 #include "proof_codec.hpp"
 #include "stark.hpp"
 #include "xfe.hpp"
@@ -49,7 +50,7 @@ static constexpr uint32_t MP_TAIL_LEVELS_MAX = 32;
 static constexpr uint32_t MP_CLIMB_MAX_PROOFS = 32;
 inline uint32_t climb_max_proofs() {  // NHIP_CLIMB_MAX overrides (A/B runs)
     static const uint32_t v = [] {
-        const char* e = std::getenv("NHIP_CLIMB_MAX");
+        const char* e = nhip::ab_env("NHIP_CLIMB_MAX");
         return e ? (uint32_t)std::strtoul(e, nullptr, 10) : MP_CLIMB_MAX_PROOFS;
     }();
     return v;
@@ -161,6 +162,8 @@ hipError_t launch_stark_phases(const StarkBatchDev& b, hipStream_t st, hipStream
 hipError_t stark_set_kernel_attributes();
 // nhip_set_fs_form: -1 = by batch size (default), 0 row, 1 pair, 2 quad; -1 return = bad form
 int set_fs_form(int form);
+// nhip_set_climb_from_ops: -1 = default, 0 = never, k = at k hash ops; -1 return = bad value
+int set_climb_from_ops(int64_t ops);
 
 // k_deep_rows8's carry-free accumulation (stark_kernels.hip): a row has M + 3A < DEEP_ROW_WORDS_MAX
 // words (dims_from), a lane takes at most ceil(M / 8) + ceil(3A / 8) <= DEEP_LANE_TERMS_MAX of them,

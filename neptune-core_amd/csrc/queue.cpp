@@ -96,7 +96,21 @@ struct nhip_queue {
         return std::chrono::duration<double, std::milli>(t1 - t0).count();
     }
 
+    // per-request latency (arrival in nhip_queue_verify -> verdicts delivered), microseconds, the
+    // last LAT_CAP requests (nhip_queue_latencies); guarded by prof_mu
+    static constexpr size_t LAT_CAP = 1u << 16;
+    std::vector<float> lat_us;
+    uint64_t lat_n = 0;
+
     void deliver(std::vector<Req*>& reqs, int rc, const uint8_t* v) {
+        const Clock::time_point now = Clock::now();
+        {
+            std::lock_guard<std::mutex> g(prof_mu);
+            for (Req* r : reqs) {
+                if (lat_us.size() < LAT_CAP) lat_us.push_back(0.f);
+                lat_us[lat_n++ % LAT_CAP] = (float)(ms_since(r->arrived, now) * 1e3);
+            }
+        }
         std::lock_guard<std::mutex> g(mu);
         size_t off = 0;
         for (Req* r : reqs) {
@@ -338,6 +352,22 @@ int nhip_queue_profile_read(const nhip_queue* q, nhip_queue_profile* out, int re
     std::lock_guard<std::mutex> g(q->prof_mu);
     *out = q->prof;
     if (reset) const_cast<nhip_queue*>(q)->prof = nhip_queue_profile{};
+    return NHIP_OK;
+}
+
+int nhip_queue_latencies(const nhip_queue* q, float* us_out, size_t cap, size_t* n, int reset) {
+    if (!q || (cap && !us_out)) return NHIP_ERR_ARG;
+    auto* m = const_cast<nhip_queue*>(q);
+    std::lock_guard<std::mutex> g(m->prof_mu);
+    const size_t have = m->lat_us.size();
+    if (n) *n = have;
+    // oldest first: the ring's next write position is the oldest entry once it has wrapped
+    const size_t start = m->lat_n > have ? (size_t)(m->lat_n % have) : 0;
+    for (size_t i = 0; i < std::min(cap, have); ++i) us_out[i] = m->lat_us[(start + i) % have];
+    if (reset) {
+        m->lat_us.clear();
+        m->lat_n = 0;
+    }
     return NHIP_OK;
 }
 

@@ -80,16 +80,14 @@ void encode_claim(const nhip_claim& claim, bool mont, uint64_t* c) {
 // the DMA of the chunk is issued.  NHIP_STAGE_NT=0: plain memcpy (A/B).
 static bool stage_nt() {
     static const bool on = [] {
-        const char* v = std::getenv("NHIP_STAGE_NT");
+        const char* v = nhip::ab_env("NHIP_STAGE_NT");
         return !v || std::strtol(v, nullptr, 10) != 0;
     }();
     return on;
 }
-// Host threads for staging copies (NHIP_HOST_THREADS overrides; at most 16, the GPU box's CPU
-// share).
+// Host threads for staging copies (at most 16, the GPU box's CPU share).
 unsigned host_threads(uint64_t bytes) {
-    unsigned t = std::thread::hardware_concurrency();
-    if (const char* e = std::getenv("NHIP_HOST_THREADS")) t = (unsigned)std::strtoul(e, nullptr, 10);
+    unsigned t = nhip::host_threads_env() ? nhip::host_threads_env() : std::thread::hardware_concurrency();
     t = std::max(1u, std::min(t, 16u));
     return bytes < (8ull << 20) ? 1u : t;
 }
@@ -134,7 +132,7 @@ struct nhip_air {
     // latency per proof, for smaller batches); a batch takes one by its size (ood_program_for)
     OodProgram progs[2];
     // slots held in LDS (the rest in the per-proof global area): AIR_LDS_SLOTS_MAX, or less when
-    // NHIP_OOD_LDS_SLOTS asks for it at creation (tests of the global-slot path)
+    // nhip_air_options.lds_slots asks for it at creation (tests of the global-slot path)
     uint32_t lds_cap = AIR_LDS_SLOTS_MAX;
     // device copies, one per GPU that has used this AIR (read-only, so every context on that GPU
     // shares it; a group drives several contexts from one process, possibly concurrently);
@@ -294,14 +292,9 @@ int air_upload(nhip_ctx* ctx, nhip_air* a, nhip_air::Dev* out) {
     return NHIP_OK;
 }
 
-// Instructions per step of the compiled AIR program (NHIP_OOD_STEP_WIDTH overrides, A/B runs):
-// two per thread of k_ood_air's 256-thread workgroups.
-// Read at every nhip_air_create (rare: once per AIR at startup).
-uint32_t ood_step_width() {
-    const char* e = std::getenv("NHIP_OOD_STEP_WIDTH");
-    const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 10) : 512u;
-    return v >= 16 && v <= (1u << 16) ? v : 512u;
-}
+// Instructions per step of the compiled AIR program: two per thread of k_ood_air's 256-thread
+// workgroups (nhip_air_options.step_width sets another, tests of the compiler).
+static constexpr uint32_t OOD_STEP_WIDTH = 512;
 
 // The program a batch of n proofs runs: the wide-step one up to NHIP_OOD_WIDE_PROG_MAX proofs (default
 // 1,024), where one proof's evaluation latency matters more than proofs per CU.  Config 4 per-GPU
@@ -310,7 +303,7 @@ uint32_t ood_step_width() {
 // bottleneck there), 4,096: 425k vs 436-437k.
 int ood_program_for(uint32_t n) {
     static const uint32_t lim = [] {
-        const char* e = std::getenv("NHIP_OOD_WIDE_PROG_MAX");
+        const char* e = nhip::ab_env("NHIP_OOD_WIDE_PROG_MAX");
         return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1024u;
     }();
     return n <= lim ? 1 : 0;
@@ -332,7 +325,8 @@ int ood_program_for(uint32_t n) {
 // its handful of constraints.  Within a step the instructions are grouped by kind (copies, products,
 // sums, differences): a wave then runs one kind of XFE operation instead of the divergent union of
 // several.
-void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t width, OodProgram& pg) {
+void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t width, uint32_t slot_budget,
+                 OodProgram& pg) {
     pg = OodProgram{};
     pg.width = width;
     const size_t NN = a->nodes.size();
@@ -395,10 +389,9 @@ void air_compile(const nhip_air* a, const std::vector<uint32_t>& cons, uint32_t 
     for (size_t i = 0; i < NN; ++i)
         if (slotted[i] && deps[i] == 0) ready.push_back((uint32_t)i);
     // working slots; the C constraint slots above them take their share of the LDS first
-    // (NHIP_OOD_SLOT_BUDGET lowers it, A/B runs)
+    // (nhip_air_options.slot_budget lowers it: tests of the compiler)
     uint32_t budget = AIR_LDS_SLOTS_MAX > cons.size() + 256 ? AIR_LDS_SLOTS_MAX - (uint32_t)cons.size() : 256u;
-    if (const char* e = std::getenv("NHIP_OOD_SLOT_BUDGET"))
-        budget = std::min<uint32_t>(budget, (uint32_t)std::max(64ul, std::strtoul(e, nullptr, 10)));
+    if (slot_budget) budget = std::min<uint32_t>(budget, std::max<uint32_t>(64u, slot_budget));
     std::vector<uint32_t> free_slots, to_free;
     uint32_t next_slot = 0, live = 0;
     std::vector<OodIns> cur, acc_next;
@@ -503,9 +496,14 @@ void nhip_stark_params_default(nhip_stark_params* out) {
     out->input_form = NHIP_INPUT_CANONICAL;
 }
 
-int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
+int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) { return nhip_air_create_ex(w, n, nullptr, out); }
+
+int nhip_air_create_ex(const uint64_t* w, size_t n, const nhip_air_options* opt, nhip_air** out) {
     if (!w || !out || n < 9) return NHIP_ERR_ARG;
     *out = nullptr;
+    const nhip_air_options o = opt ? *opt : nhip_air_options{0, 0, 0};
+    const uint32_t width = o.step_width ? o.step_width : OOD_STEP_WIDTH;
+    if (width < 16 || width > (1u << 16)) return NHIP_ERR_ARG;
     if (w[0] != 0x41495231ull) return NHIP_ERR_ARG;
     const uint64_t M = w[1], A = w[2], K = w[3], NN = w[4];
     const uint64_t nc[4] = {w[5], w[6], w[7], w[8]};
@@ -568,10 +566,9 @@ int nhip_air_create(const uint64_t* w, size_t n, nhip_air** out) {
         cons[i] = (uint32_t)cw[i];
     }
     a->cons_off = make_uint4((uint32_t)nc[0], (uint32_t)(nc[0] + nc[1]), (uint32_t)(nc[0] + nc[1] + nc[2]), (uint32_t)C);
-    air_compile(a, cons, ood_step_width(), a->progs[0]);
-    air_compile(a, cons, 2 * ood_step_width(), a->progs[1]);
-    if (const char* e = std::getenv("NHIP_OOD_LDS_SLOTS"))
-        a->lds_cap = std::min<uint32_t>(AIR_LDS_SLOTS_MAX, (uint32_t)std::strtoul(e, nullptr, 10));
+    air_compile(a, cons, width, o.slot_budget, a->progs[0]);
+    air_compile(a, cons, 2 * width, o.slot_budget, a->progs[1]);
+    if (o.lds_slots) a->lds_cap = std::min<uint32_t>(AIR_LDS_SLOTS_MAX, o.lds_slots);
     *out = a;
     return NHIP_OK;
 }
@@ -818,7 +815,8 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
             // node's CPUs among the members on it)
             const nhip::HostTopo& topo = ctx_topo(ctx);
             unsigned threads = host_threads(staged_bytes);
-            if (const unsigned set = nhip_internal_host_threads(ctx); set && threads > 1) threads = set;
+            if (const unsigned set = nhip_internal_host_threads(ctx); set && threads > 1 && !nhip::host_threads_env())
+                threads = set;
             if (!topo.cpus.empty() && nhip::numa_enabled()) threads = std::min<unsigned>(threads, (unsigned)topo.cpus.size());
             if (threads > 1 && stage != pageable.data()) {
                 pool.reserve(threads);
@@ -1082,7 +1080,7 @@ int nhip_batch_refill(nhip_ctx* ctx, nhip_batch* b, nhip_air* air, const nhip_st
 // quarter of its rate).
 static int launch_resources(nhip_batch* b) {
     if (!b->timed) {
-        const char* al = std::getenv("NHIP_AUX_AFTER_LEVEL");
+        const char* al = nhip::ab_env("NHIP_AUX_AFTER_LEVEL");
         b->tm.aux_after_level = al ? (uint32_t)std::strtoul(al, nullptr, 10) : AUX_AFTER_LEVEL_DEFAULT;
         const size_t out_bytes = OUT_HDR + (size_t)b->dev.mp.levels * MP_SHARDS * 4 + b->dev.n_proofs + 16;
         if (VerifyScratch* sc = b->scratch) {

@@ -386,110 +386,6 @@ __global__ void __launch_bounds__(256, NHIP_ROWS_WAVES) k_hash_rows(const uint64
     }
 }
 
-// The same hashing with each wave's row words staged through LDS (round 5).  k_hash_rows gives
-// every lane its own row, so one load instruction of a wave touches 64 rows 3 KB apart (64 cache
-// lines, 8 bytes used of each per instruction) and the 80-byte chunks of a row straddle lines that
-// are evicted between chunks: the round-4 PMC pass counted 1.5x the row bytes fetched, waves
-// waiting 69% of their cycles.  Here a wave fetches chunk c of its 64 rows with five
-// global_load_lds_dwordx4 (each 16-byte piece P = 64 i + lane is part P % 5 of row P / 5, so ten
-// lanes read one row's 80 bytes back to back), the pieces landing lane-linear in the wave's 5 KB
-// LDS slice = row-major [64][10] words; each lane then reads its row's 10 words (ds_read at stride
-// 80 B: the 16 lanes of a b128 group start on 16 distinct 4-bank groups, conflict-free).  Chunk
-// c + 1 is requested right after chunk c is read, so its fetch runs under chunk c's permutation
-// (no VGPRs hold it: the DMA writes LDS).  The words and the sponge are k_hash_rows's, so every
-// digest is bit-identical.  NHIP_ROWS_LDS=1 selects it (A/B only: measured slower).
-typedef __attribute__((address_space(3))) void lds_void_t;
-static constexpr uint32_t ROWS_PIECES = TIP5_RATE / 2;  // 16-byte pieces per row chunk
-// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
-static constexpr int WAIT_VMCNT0 = 0x0F70, WAIT_LGKMCNT0 = 0xC07F;
-template <bool MW>
-__global__ void __launch_bounds__(256, NHIP_ROWS_WAVES)
-    k_hash_rows_lds(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc, uint32_t n_proofs,
-                    uint32_t k, StarkDims dims, uint64_t* __restrict__ dig, const uint32_t* __restrict__ fail) {
-    __shared__ Tip5Lds lds;
-    __shared__ __attribute__((aligned(16))) uint64_t rowbuf[4][64 * TIP5_RATE];
-    // per wave: each lane's row offset (~0: none) and digest slot, in LDS rather than registers so
-    // nothing but the sponge state is live across a permutation (84 VGPRs, 5 waves, no scratch)
-    __shared__ uint64_t rowbase[4][64], rowdig[4][64];
-    tip5_lds_init(lds);
-    const uint32_t tree = blockIdx.y;
-    const uint32_t width = tree == 0 ? dims.num_main : (tree == 1 ? 3 * dims.num_aux : 3 * dims.num_quot_seg);
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    uint64_t* const buf = rowbuf[wv];
-    const uint64_t rows = (uint64_t)n_proofs * k;
-    const uint32_t nchunks = width / TIP5_RATE + 1;
-    for (uint64_t tw = (uint64_t)blockIdx.x * blockDim.x + 64u * wv; tw < rows; tw += (uint64_t)gridDim.x * blockDim.x) {
-        {
-            const uint64_t t = tw + lane;
-            uint64_t base = ~0ull, o = 0;  // ~0: no row (past the end, or a failed proof)
-            if (t < rows) {
-                const uint32_t p = (uint32_t)(t / k), j = (uint32_t)(t % k);
-                if (!fail[p]) {
-                    const ProofDesc& d = desc[p];
-                    base = (tree == 0 ? d.main_rows_off : (tree == 1 ? d.aux_rows_off : d.quot_rows_off)) +
-                           (uint64_t)j * width;
-                    o = (((uint64_t)p * 3 + tree) * k + j) * 5;
-                }
-            }
-            rowbase[wv][lane] = base;
-            rowdig[wv][lane] = o;
-            __builtin_amdgcn_wave_barrier();
-        }
-        // request chunk c of the wave's 64 rows into buf (pieces past a row's last word are skipped;
-        // a piece holding the last word of an odd remainder reads one word past the row: the word
-        // buffer always has words after the rows, the claims and an 8-byte pad)
-        auto request = [&](uint32_t c) {
-            const uint32_t pos = c * TIP5_RATE;
-            const uint32_t rem = min(width - pos, (uint32_t)TIP5_RATE);
-            // the piece indices recomputed per chunk from an opaque copy of the lane id: hoisted out
-            // of the chunk loop they would hold ten more VGPRs across every permutation
-            uint32_t ln = lane;
-            asm volatile("" : "+v"(ln));
-#pragma unroll
-            for (uint32_t i = 0; i < ROWS_PIECES; ++i) {
-                const uint32_t P = i * 64u + ln, r = (P * 13108u) >> 16, part = P - ROWS_PIECES * r;  // P / 5 for P < 320
-                const uint64_t rb = rowbase[wv][r];
-                if (rb != ~0ull && 2 * part < rem)
-                    __builtin_amdgcn_global_load_lds((const void*)(words + rb + pos + 2 * part), (lds_void_t*)(buf + i * 128u),
-                                                     16, 0, 0);
-            }
-        };
-        uint64_t s[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) s[q] = 0;
-        request(0);
-        for (uint32_t c = 0; c < nchunks; ++c) {
-            const uint32_t pos = c * TIP5_RATE;
-            const bool last = c + 1 == nchunks;
-            __builtin_amdgcn_s_waitcnt(WAIT_VMCNT0);  // chunk c has landed (hipcc does not count LDS-DMA)
-            const uint64_t* mine = buf + lane * TIP5_RATE;
-            if (!last) {
-#pragma unroll
-                for (int q = 0; q < TIP5_RATE; ++q) s[q] = word_mont<MW>(mine[q]);
-            } else {
-                const uint32_t rem = width - pos;
-#pragma unroll
-                for (int q = 0; q < TIP5_RATE; ++q) {
-                    const uint32_t qq = (uint32_t)q;
-                    s[q] = qq < rem ? word_mont<MW>(mine[q]) : (qq == rem ? MONT_ONE : 0ull);
-                }
-            }
-            __builtin_amdgcn_s_waitcnt(WAIT_LGKMCNT0);  // the reads are done before the buffer is refilled
-            if (!last) request(c + 1);                  // fetched under this chunk's permutation
-            tip5_rounds_0_3(s, lds.lut);
-            tip5_last_sbox(s, lds.lut);
-            if (!last) tip5_last_mds<10, 16>(s);
-            else tip5_last_mds<0, 5>(s);
-        }
-        if (rowbase[wv][lane] != ~0ull) {
-            uint64_t* __restrict__ o = dig + rowdig[wv][lane];
-#pragma unroll
-            for (int q = 0; q < 5; ++q) o[q] = s[q];
-        }
-        __builtin_amdgcn_wave_barrier();  // every lane's reads of rowbase / rowdig precede the next writes
-    }
-}
-
 // ------------------------------------------------------------------ workgroup helpers
 __device__ __forceinline__ void hash_pair_raw(const uint64_t* l, const uint64_t* r, uint64_t* out,
                                               const uint8_t* __restrict__ lut) {
@@ -1696,7 +1592,7 @@ __global__ void k_verdicts(const uint32_t* __restrict__ fail, uint32_t n, uint8_
 // (NHIP_OOD_WIDE_MAX overrides, A/B runs), else 256
 static bool ood_wide(uint32_t n) {
     static const uint32_t lim = [] {
-        const char* v = std::getenv("NHIP_OOD_WIDE_MAX");
+        const char* v = nhip::ab_env("NHIP_OOD_WIDE_MAX");
         return v ? (uint32_t)std::strtoul(v, nullptr, 10) : OOD_WIDE_MAX_PROOFS;
     }();
     return n <= lim;
@@ -1708,14 +1604,20 @@ static bool ood_wide(uint32_t n) {
 // deep tree are launch-bound, not VALU-bound.  Measured (profiles/r05z/ab/climb_from_ab_r05q.txt):
 // config 5's 64 proofs +3-6% at 4,096 ops; config 4's trees (<= 19 levels) are not affected (at
 // 4,096 ops without the depth gate: 512 proofs -2 to -4%, 4,096 equal; 16K / 64K ops: worse).
-// NHIP_CLIMB_FROM_OPS overrides the threshold for every depth (0 = never).
+// nhip_set_climb_from_ops sets the threshold for every depth (tests: 0 = never).
 static constexpr uint32_t CLIMB_FROM_MIN_LEVELS = 24;
 static constexpr uint64_t CLIMB_FROM_OPS_DEFAULT = 4096;
+static std::atomic<int64_t>& climb_from_forced() {
+    static std::atomic<int64_t> v(-1);
+    return v;
+}
+int set_climb_from_ops(int64_t ops) {
+    if (ops < -1) return -1;
+    climb_from_forced().store(ops, std::memory_order_relaxed);
+    return 0;
+}
 static uint64_t climb_from_ops(uint32_t hash_levels) {
-    static const int64_t v = [] {
-        const char* e = std::getenv("NHIP_CLIMB_FROM_OPS");
-        return e ? (int64_t)std::strtoull(e, nullptr, 10) : (int64_t)-1;
-    }();
+    const int64_t v = climb_from_forced().load(std::memory_order_relaxed);
     if (v >= 0) return (uint64_t)v;
     return hash_levels >= CLIMB_FROM_MIN_LEVELS ? CLIMB_FROM_OPS_DEFAULT : 0ull;
 }
@@ -1724,7 +1626,7 @@ static uint64_t climb_from_ops(uint32_t hash_levels) {
 // NHIP_FS_ROW_LAT_MAX; default 0 = never)
 static uint32_t fs_row_lat_max() {
     static const uint32_t v = [] {
-        const char* e = std::getenv("NHIP_FS_ROW_LAT_MAX");
+        const char* e = nhip::ab_env("NHIP_FS_ROW_LAT_MAX");
         return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
     }();
     return v;
@@ -1737,7 +1639,7 @@ enum FsForm { FS_ROW = 0, FS_PAIR = 1, FS_QUAD = 2 };
 // k_fs_replay_quad workgroup size (NHIP_QUAD_WG = 64..1024 overrides, A/B runs)
 static uint32_t quad_wg() {
     static const uint32_t v = [] {
-        const char* e = std::getenv("NHIP_QUAD_WG");
+        const char* e = nhip::ab_env("NHIP_QUAD_WG");
         const uint32_t w = e ? (uint32_t)std::strtoul(e, nullptr, 10) : FS_QUAD_WG;
         return (w >= 64 && w <= 1024 && w % 64 == 0) ? w : FS_QUAD_WG;
     }();
@@ -1745,7 +1647,7 @@ static uint32_t quad_wg() {
 }
 static std::atomic<int>& fs_form_forced() {
     static std::atomic<int> f([] {
-        if (const char* v = std::getenv("NHIP_FS_FORM")) {
+        if (const char* v = nhip::ab_env("NHIP_FS_FORM")) {
             if (v[0] == 'q') return (int)FS_QUAD;
             if (v[0] == 'p') return (int)FS_PAIR;
             if (v[0] == 'r') return (int)FS_ROW;
@@ -1761,7 +1663,7 @@ int set_fs_form(int form) {
 }
 static FsForm fs_form(uint32_t n) {
     static const uint32_t quad_min = [] {
-        const char* v = std::getenv("NHIP_FS_QUAD_MIN");
+        const char* v = nhip::ab_env("NHIP_FS_QUAD_MIN");
         return v ? (uint32_t)std::strtoul(v, nullptr, 10) : FS_QUAD_MIN_PROOFS;
     }();
     const int forced = fs_form_forced().load(std::memory_order_relaxed);
@@ -1786,7 +1688,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     // batches in flight one level up, for batches of at least AGE_PRIO_MIN_PROOFS (A/B knobs:
     // NHIP_AGE_PRIO=k sets k for every size, 0 = off; NHIP_AGE_PRIO_FS=1 raises the sponge too)
     static const int64_t age_env = [] {
-        const char* e = std::getenv("NHIP_AGE_PRIO");
+        const char* e = nhip::ab_env("NHIP_AGE_PRIO");
         return e ? (int64_t)std::strtoul(e, nullptr, 10) : (int64_t)-1;
     }();
     const uint32_t age_k = age_env >= 0 ? (uint32_t)age_env : (n >= AGE_PRIO_MIN_PROOFS ? AGE_PRIO_OLDEST : 0u);
@@ -1795,7 +1697,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     (void)hipGetDevice(&dev);
     const AgePrio age{seq_ctr[(uint32_t)dev & 63u].fetch_add(1u, std::memory_order_relaxed), age_k};
     static const bool age_fs = [] {  // NHIP_AGE_PRIO_FS=1 (A/B): the sponge replay raised as well
-        const char* e = std::getenv("NHIP_AGE_PRIO_FS");
+        const char* e = nhip::ab_env("NHIP_AGE_PRIO_FS");
         return e && e[0] == '1';
     }();
     const AgePrio age_sponge{age.seq, age_fs ? age.k : 0u};
@@ -1822,7 +1724,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
                            b.ops, n, b.xs, b.idx, b.fail, age_sponge);
     else if (ff == FS_QUAD)
         hipLaunchKernelGGL(k_fs_replay_quad<MW>, dim3((n * 4 + quad_wg() - 1) / quad_wg()), dim3(quad_wg()), 0, sa, b.words, b.desc, b.ops, n,
-                           b.xs, b.idx, b.fail, age);
+                           b.xs, b.idx, b.fail, age_sponge);
     else if (n < fs_row_lat_max())
         hipLaunchKernelGGL((k_fs_replay_wide<false, MW, true>), dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words,
                            b.desc, b.ops, n, b.xs, b.idx, b.fail, age_sponge);
@@ -1842,18 +1744,10 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
         const uint64_t rows = (uint64_t)n * k;
         unsigned gx = (unsigned)((rows + 255) / 256);
         if (gx > 16384) gx = 16384;
-        static const bool rows_lds = [] {  // NHIP_ROWS_LDS=1: the LDS-staged row loads (A/B, measured slower)
-            const char* v = std::getenv("NHIP_ROWS_LDS");
-            return v && std::strtoul(v, nullptr, 10) != 0;
-        }();
         // dispatch begin / end events (the row kernel's own duration, as the kernel trace has it)
         hipEvent_t r0 = tm->launch_events ? tm->rev[0] : nullptr, r1 = tm->launch_events ? tm->rev[1] : nullptr;
-        if (rows_lds)
-            hipExtLaunchKernelGGL(k_hash_rows_lds<MW>, dim3(gx, 3), dim3(256), 0, st, r0, r1, 0, b.words, b.desc, n, k,
-                                  b.dims, b.dig, b.fail);
-        else
-            hipExtLaunchKernelGGL(k_hash_rows<MW>, dim3(gx, 3), dim3(256), 0, st, r0, r1, 0, b.words, b.desc, n, k,
-                                  b.dims, b.dig, b.fail, age);
+        hipExtLaunchKernelGGL(k_hash_rows<MW>, dim3(gx, 3), dim3(256), 0, st, r0, r1, 0, b.words, b.desc, n, k,
+                              b.dims, b.dig, b.fail, age);
     }
     mark(2, st);
     if (small) {
@@ -1909,7 +1803,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     const uint32_t log2_lcw = 31 - __builtin_clz(b.max_lcw);
     const uint32_t hash_levels = b.mp.levels > log2_lcw ? b.mp.levels : log2_lcw;
     static const uint32_t mp_small_max = [] {
-        const char* v = std::getenv("NHIP_MP_SMALL_MAX");
+        const char* v = nhip::ab_env("NHIP_MP_SMALL_MAX");
         return v ? (uint32_t)std::strtoul(v, nullptr, 10) : MP_SMALL_MAX_PROOFS;
     }();
     // first level of the tail climbed in one launch (every level from it on is small)

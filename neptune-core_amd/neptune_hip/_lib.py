@@ -117,6 +117,7 @@ SIGNATURES = {
     "nhip_verdicts_all_dev": ([_vp, _vp, _sz, ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
     "nhip_stark_params_default": ([ctypes.POINTER(StarkParams)], None),
     "nhip_air_create": ([_u64p, _sz, _pp], ctypes.c_int),
+    "nhip_air_create_ex": ([_u64p, _sz, ctypes.c_void_p, _pp], ctypes.c_int),
     "nhip_air_destroy": ([_vp], None),
     "nhip_air_info": ([_vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                        ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
@@ -174,7 +175,20 @@ SIGNATURES = {
                                  _sz, _u8p, ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
     "nhip_group_stream_create": ([_vp, _vp, ctypes.POINTER(StarkParams), ctypes.POINTER(_vp)], ctypes.c_int),
     "nhip_group_stream_submit": ([_vp, ctypes.POINTER(Claim), ctypes.POINTER(Proof), _sz, _vp, _vp], ctypes.c_int),
+    "nhip_group_stream_submit_placed": ([_vp, ctypes.POINTER(Claim), ctypes.POINTER(Proof), _vp, _sz, _vp, _vp],
+                                        ctypes.c_int),
     "nhip_group_stream_finish": ([_vp], ctypes.c_int),
+    "nhip_queue_latencies": ([_vp, _vp, _sz, ctypes.POINTER(_sz), ctypes.c_int], ctypes.c_int),
+    "nhip_arena_create": ([_vp, _sz, ctypes.POINTER(_vp)], ctypes.c_int),
+    "nhip_arena_destroy": ([_vp], None),
+    "nhip_arena_reset": ([_vp], ctypes.c_int),
+    "nhip_arena_member_info": ([_vp, _sz, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "nhip_arena_ingest_spans": ([_vp, _vp, _sz, _vp, _sz, ctypes.POINTER(Proof), _vp], ctypes.c_int),
+    "nhip_arena_ingest_txs": ([_vp, _vp, _sz, _sz, ctypes.POINTER(Proof), _vp, _sz, ctypes.POINTER(_sz),
+                               ctypes.POINTER(_sz), ctypes.POINTER(_sz)], ctypes.c_int),
+    "nhip_arena_ingest_blocks": ([_vp, _vp, _sz, ctypes.c_uint32, ctypes.POINTER(Proof), _vp, _vp, _sz,
+                                  ctypes.POINTER(_sz), ctypes.POINTER(_sz)], ctypes.c_int),
     "nhip_group_stream_stats": ([_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
@@ -188,6 +202,7 @@ SIGNATURES = {
     "nhip_batch_wait": ([_vp, _vp, _u8p, ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
     "nhip_batch_stats": ([_vp, ctypes.POINTER(Stats)], ctypes.c_int),
     "nhip_set_fs_form": ([ctypes.c_int], ctypes.c_int),
+    "nhip_set_climb_from_ops": ([ctypes.c_int64], ctypes.c_int),
     "nhip_batch_set_launch_timing": ([_vp, ctypes.c_int], ctypes.c_int),
     "nhip_batch_set_streams": ([_vp, ctypes.c_int], ctypes.c_int),
     "nhip_batch_transcript": ([_vp, _vp, _sz, _u64p, _sz, ctypes.POINTER(ctypes.c_uint32), _sz,

@@ -59,6 +59,31 @@ def on_rank0(fn, dist, key: str = "nhip_rank0_leg", timeout_s: float = 900.0):
         store.set(key, "1")
 
 
+def agreed_max(vals, dist, fast=None):
+    """All-reduce(MAX) of the float list `vals` that every rank completes the same way.
+
+    `fast(vals)` (e.g. one RCCL all-reduce over xGMI on a group made for it, its result synchronized
+    to the host INSIDE the call, so a device-side fault raises there) is tried first; then one host
+    all-reduce(MIN) of a per-rank success flag on the default (gloo) group decides for every rank
+    at once: all succeeded -> the fast result; any failed -> every rank reduces on the host group.
+    So a fault on one rank can never leave the ranks issuing different collectives.  Returns
+    (values, fast_used, this rank's error or None)."""
+    import torch
+    res, err = None, None
+    if fast is not None:
+        try:
+            res = [float(x) for x in fast(list(vals))]
+        except Exception as e:  # noqa: BLE001 - any fault of the fast path falls back, on every rank
+            res, err = None, f"{type(e).__name__}: {e}"[:300]
+    flag = torch.tensor([1 if res is not None else 0], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 1:
+        return res, True, None
+    t = torch.tensor([float(x) for x in vals], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()], False, err
+
+
 def _device_for(dist):
     import torch
     backend = dist.get_backend()

@@ -102,11 +102,15 @@ class Claim:
 class Air:
     """AIR circuit descriptor (format: DESIGN.md §9)."""
 
-    def __init__(self, words: Sequence[int]):
+    def __init__(self, words: Sequence[int], lds_slots: int = 0, step_width: int = 0, slot_budget: int = 0):
+        """lds_slots / step_width / slot_budget: the OOD program compiler's options
+        (nhip_air_create_ex; 0 = default): tests of the compiler and of the global-slot path."""
         self.lib = _lib.load()
         w = np.ascontiguousarray(np.asarray(words, dtype=np.uint64))
         h = ctypes.c_void_p()
-        check(self.lib.nhip_air_create(w, w.size, ctypes.byref(h)), "nhip_air_create")
+        opts = (ctypes.c_uint32 * 3)(lds_slots, step_width, slot_budget)
+        check(self.lib.nhip_air_create_ex(w, w.size, ctypes.cast(opts, ctypes.c_void_p), ctypes.byref(h)),
+              "nhip_air_create_ex")
         self.handle = h.value
 
     def info(self):
@@ -302,6 +306,16 @@ class Queue:
         check(self.ctx.lib.nhip_queue_profile_read(self.handle, ctypes.byref(pr), int(reset)), "nhip_queue_profile_read")
         return pr.as_dict()
 
+    def latencies_ms(self, reset: bool = False) -> np.ndarray:
+        """Per-request latency (arrival -> verdicts delivered) of the last <= 65,536 requests, as the
+        library measured it (nhip_queue_latencies), oldest first, in milliseconds."""
+        n = ctypes.c_size_t()
+        check(self.ctx.lib.nhip_queue_latencies(self.handle, None, 0, ctypes.byref(n), 0), "nhip_queue_latencies")
+        out = np.zeros(max(n.value, 1), dtype=np.float32)
+        check(self.ctx.lib.nhip_queue_latencies(self.handle, out.ctypes.data, n.value, ctypes.byref(n), int(reset)),
+              "nhip_queue_latencies")
+        return out[:n.value].astype(np.float64) / 1e3
+
     def close(self):
         if self.handle:
             self.ctx.lib.nhip_queue_destroy(self.handle)
@@ -440,6 +454,20 @@ class GroupStream:
     def submit(self, pairs: Sequence[Tuple[Claim, Sequence[int]]]):
         return self.submit_marshalled(_Marshal([c for c, _ in pairs], [p for _, p in pairs]))
 
+    def submit_placed(self, claims: "_Marshal", placed: "Placed"):
+        """nhip_group_stream_submit_placed: the proofs an Arena decoded, each to the member it was
+        placed on (`claims`: marshal(claims, []) in the proofs' order)."""
+        n = placed.n
+        if claims.n < n:
+            raise ValueError("fewer claims than placed proofs")
+        v = np.zeros(max(n, 1), dtype=np.uint8)
+        ok = (ctypes.c_uint8 * 1)()
+        check(self.lib.nhip_group_stream_submit_placed(self.handle, claims.claims, placed.proofs,
+                                                       ctypes.addressof(placed.member_of), n, v.ctypes.data,
+                                                       ctypes.addressof(ok)), "nhip_group_stream_submit_placed")
+        prev, self._prev = self._prev, (v[:n], ok, n)
+        return None if prev is None else ([bool(x) for x in prev[0]], bool(prev[1][0]))
+
     def finish(self):
         check(self.lib.nhip_group_stream_finish(self.handle), "nhip_group_stream_finish")
         prev, self._prev = self._prev, None
@@ -463,6 +491,114 @@ class GroupStream:
 
     def __exit__(self, *exc):
         self.close()
+
+
+class Placed:
+    """Proofs an Arena decoded: the C proof records (pointing into the arenas), each proof's member,
+    and the wire bytes they came from (kept alive with them)."""
+
+    def __init__(self, cap: int, data=None):
+        self.proofs = (_lib.Proof * max(cap, 1))()
+        self.member_of = (ctypes.c_uint32 * max(cap, 1))()
+        self.n = 0
+        self.data = data
+
+    def words(self, i: int) -> np.ndarray:
+        """Proof i's words (a view of the pinned arena)."""
+        p = self.proofs[i]
+        if not p.len:
+            return np.zeros(0, dtype=np.uint64)
+        return np.ctypeslib.as_array(p.words, shape=(p.len,))
+
+    def members(self) -> List[int]:
+        return [int(self.member_of[i]) for i in range(self.n)]
+
+
+def _byte_buffer(data):
+    a = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
+    return a, len(data)
+
+
+class Arena:
+    """Per-member pinned proof arenas of a group (nhip_arena_*): wire bytes (bincode
+    TransferTransactions, blk files, or explicit word spans) decoded straight into pinned memory on
+    each member GPU's NUMA node, each proof on the least-loaded member, ready for
+    ``GroupStream.submit_placed``.  The words are canonical values (Stark input_form canonical)."""
+
+    def __init__(self, group: Group, bytes_per_member: int):
+        self.group = group
+        self.lib = group.lib
+        h = ctypes.c_void_p()
+        check(self.lib.nhip_arena_create(group.handle, int(bytes_per_member), ctypes.byref(h)), "nhip_arena_create")
+        self.handle = h.value
+
+    def reset(self) -> None:
+        check(self.lib.nhip_arena_reset(self.handle), "nhip_arena_reset")
+
+    def member_info(self, i: int) -> dict:
+        u, c, nd = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+        check(self.lib.nhip_arena_member_info(self.handle, i, ctypes.byref(u), ctypes.byref(c), ctypes.byref(nd)),
+              "nhip_arena_member_info")
+        return {"used_words": u.value, "cap_words": c.value, "page_node": nd.value}
+
+    def ingest_txs(self, data, max_txs: int = None, proof_cap: int = None):
+        """Back-to-back TransferTransactions -> (Placed, transactions taken, bytes consumed); stops
+        before the first transaction that does not fit (then reset after submitting, and continue)."""
+        a, n = _byte_buffer(data)
+        cap = proof_cap if proof_cap is not None else max(1, n // 8)
+        pl = Placed(cap, a)
+        nt, npf, used = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        rc = self.lib.nhip_arena_ingest_txs(self.handle, a.ctypes.data, n, max_txs if max_txs is not None else n,
+                                            pl.proofs, ctypes.addressof(pl.member_of), cap, ctypes.byref(nt),
+                                            ctypes.byref(npf), ctypes.byref(used))
+        pl.n = npf.value
+        if rc == _lib.NHIP_ERR_DECODE:
+            raise ValueError(f"malformed TransferTransaction after {nt.value} transactions ({used.value} bytes)")
+        check(rc, "nhip_arena_ingest_txs")
+        return pl, nt.value, used.value
+
+    def ingest_blocks(self, data, pow_tree_height: int):
+        """A blk file's bytes -> (Placed, block index of each SingleProof)."""
+        a, n = _byte_buffer(data)
+        cnt = ctypes.c_size_t()
+        check(self.lib.nhip_blk_scan(a.ctypes.data, n, pow_tree_height, None, 0, ctypes.byref(cnt)), "nhip_blk_scan")
+        cap = max(cnt.value, 1)
+        pl = Placed(cap, a)
+        block_of = np.zeros(cap, dtype=np.uint64)
+        npf, nb = ctypes.c_size_t(), ctypes.c_size_t()
+        check(self.lib.nhip_arena_ingest_blocks(self.handle, a.ctypes.data, n, pow_tree_height, pl.proofs,
+                                                ctypes.addressof(pl.member_of), block_of.ctypes.data, cap,
+                                                ctypes.byref(npf), ctypes.byref(nb)), "nhip_arena_ingest_blocks")
+        pl.n = npf.value
+        return pl, [int(x) for x in block_of[:pl.n]]
+
+    def ingest_spans(self, data, spans: Sequence[Tuple[int, int]]):
+        """Proofs at (byte offset, words) of `data` -> Placed."""
+        a, n = _byte_buffer(data)
+        sp = np.ascontiguousarray(np.asarray(spans, dtype=np.uint64).reshape(-1))
+        k = sp.size // 2
+        pl = Placed(k, a)
+        check(self.lib.nhip_arena_ingest_spans(self.handle, a.ctypes.data, n, sp.ctypes.data, k, pl.proofs,
+                                               ctypes.addressof(pl.member_of)), "nhip_arena_ingest_spans")
+        pl.n = k
+        return pl
+
+    def close(self):
+        if self.handle:
+            self.lib.nhip_arena_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def proof_decodes(air: Air, stark: Stark, claim: Claim, proof: Sequence[int]) -> bool:

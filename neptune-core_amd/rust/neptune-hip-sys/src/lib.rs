@@ -30,7 +30,7 @@ pub const NHIP_HW_QUEUES_RECOMMENDED: u32 = 8;
 macro_rules! opaque {
     ($($name:ident),*) => { $( #[repr(C)] pub struct $name { _p: [u8; 0] } )* };
 }
-opaque!(nhip_ctx, nhip_air, nhip_batch, nhip_group, nhip_group_stream, nhip_queue, nhip_pow_buffer);
+opaque!(nhip_ctx, nhip_air, nhip_batch, nhip_group, nhip_group_stream, nhip_queue, nhip_pow_buffer, nhip_arena);
 
 /// `Stark::default()` plus the table dimensions (`nhip_stark_params_default`).
 #[repr(C)]
@@ -44,6 +44,15 @@ pub struct nhip_stark_params {
     pub num_quotient_segments: u32,
     /// `NHIP_INPUT_CANONICAL` or `NHIP_INPUT_MONTGOMERY` (claims' and proofs' field elements)
     pub input_form: u32,
+}
+
+/// The OOD program compiler's options (`nhip_air_create_ex`; 0 = default for each).
+#[repr(C)]
+#[derive(Default, Clone, Copy, Debug)]
+pub struct nhip_air_options {
+    pub lds_slots: u32,
+    pub step_width: u32,
+    pub slot_budget: u32,
 }
 
 /// `triton_vm::proof::Claim { program_digest, version, input, output }`, words in the params'
@@ -181,6 +190,8 @@ extern "C" {
     pub fn nhip_verdicts_all_dev(ctx: *mut nhip_ctx, d_verdicts: *const u8, n: usize, all_ok: *mut u8) -> c_int;
     pub fn nhip_stark_params_default(out: *mut nhip_stark_params);
     pub fn nhip_air_create(words: *const u64, n_words: usize, out: *mut *mut nhip_air) -> c_int;
+    pub fn nhip_air_create_ex(words: *const u64, n_words: usize, options: *const nhip_air_options,
+                              out: *mut *mut nhip_air) -> c_int;
     pub fn nhip_air_destroy(air: *mut nhip_air);
     pub fn nhip_air_info(air: *const nhip_air, num_nodes: *mut u32, num_levels: *mut u32,
                          num_constraints: *mut u32) -> c_int;
@@ -219,6 +230,7 @@ extern "C" {
                                  fail_bits: *mut u32, n_xfe: *mut usize) -> c_int;
     pub fn nhip_batch_destroy(batch: *mut nhip_batch);
     pub fn nhip_set_fs_form(form: c_int) -> c_int;
+    pub fn nhip_set_climb_from_ops(ops: i64) -> c_int;
     pub fn nhip_batch_set_launch_timing(batch: *mut nhip_batch, on: c_int) -> c_int;
     pub fn nhip_batch_set_streams(batch: *mut nhip_batch, streams: c_int) -> c_int;
     pub fn nhip_queue_create(ctx: *mut nhip_ctx, air: *mut nhip_air, params: *const nhip_stark_params,
@@ -227,6 +239,8 @@ extern "C" {
                              n: usize, verdicts: *mut u8) -> c_int;
     pub fn nhip_queue_stats(queue: *const nhip_queue, batches: *mut u64, proofs: *mut u64) -> c_int;
     pub fn nhip_queue_profile_read(queue: *const nhip_queue, out: *mut nhip_queue_profile, reset: c_int) -> c_int;
+    pub fn nhip_queue_latencies(queue: *const nhip_queue, us_out: *mut f32, cap: usize, n: *mut usize,
+                                reset: c_int) -> c_int;
     pub fn nhip_queue_destroy(queue: *mut nhip_queue);
     pub fn nhip_group_create(devices: *const c_int, n_devices: usize, out: *mut *mut nhip_group) -> c_int;
     pub fn nhip_group_init(device_mask: u32, out: *mut *mut nhip_group) -> c_int;
@@ -241,6 +255,9 @@ extern "C" {
                                     out: *mut *mut nhip_group_stream) -> c_int;
     pub fn nhip_group_stream_submit(stream: *mut nhip_group_stream, claims: *const nhip_claim,
                                     proofs: *const nhip_proof, n: usize, verdicts: *mut u8, all_ok: *mut u8) -> c_int;
+    pub fn nhip_group_stream_submit_placed(stream: *mut nhip_group_stream, claims: *const nhip_claim,
+                                           proofs: *const nhip_proof, member_of: *const u32, n: usize,
+                                           verdicts: *mut u8, all_ok: *mut u8) -> c_int;
     pub fn nhip_group_stream_finish(stream: *mut nhip_group_stream) -> c_int;
     pub fn nhip_group_stream_stats(stream: *const nhip_group_stream, batches: *mut u64, proofs: *mut u64,
                                    ms_stage: *mut f64, ms_upload: *mut f64, ms_device: *mut f64) -> c_int;
@@ -257,6 +274,19 @@ extern "C" {
                            claims: *mut nhip_claim) -> c_int;
     pub fn nhip_le_words(bytes: *const u8, n_bytes: usize, offset: u64, n: usize, out: *mut u64) -> c_int;
     pub fn nhip_tx_scan(bytes: *const u8, n_bytes: usize, tx: *mut nhip_tx) -> c_int;
+    pub fn nhip_arena_create(group: *mut nhip_group, bytes_per_member: usize, out: *mut *mut nhip_arena) -> c_int;
+    pub fn nhip_arena_destroy(arena: *mut nhip_arena);
+    pub fn nhip_arena_reset(arena: *mut nhip_arena) -> c_int;
+    pub fn nhip_arena_member_info(arena: *const nhip_arena, member: usize, used_words: *mut u64,
+                                  cap_words: *mut u64, page_node: *mut c_int) -> c_int;
+    pub fn nhip_arena_ingest_spans(arena: *mut nhip_arena, bytes: *const u8, n_bytes: usize, spans: *const u64,
+                                   n: usize, proofs: *mut nhip_proof, member_of: *mut u32) -> c_int;
+    pub fn nhip_arena_ingest_txs(arena: *mut nhip_arena, bytes: *const u8, n_bytes: usize, max_txs: usize,
+                                 proofs: *mut nhip_proof, member_of: *mut u32, proof_cap: usize, n_txs: *mut usize,
+                                 n_proofs: *mut usize, consumed: *mut usize) -> c_int;
+    pub fn nhip_arena_ingest_blocks(arena: *mut nhip_arena, bytes: *const u8, n_bytes: usize, pow_tree_height: u32,
+                                    proofs: *mut nhip_proof, member_of: *mut u32, block_of: *mut u64,
+                                    proof_cap: usize, n_proofs: *mut usize, n_blocks: *mut usize) -> c_int;
     pub fn nhip_tx_parts(bytes: *const u8, n_bytes: usize, tx: *const nhip_tx, seq_words: *mut u64,
                          seq_offsets: *mut u64, proof_spans: *mut u64, digests: *mut u64) -> c_int;
     pub fn nhip_pow_mast_commit(ctx: *mut nhip_ctx, mast: *const nhip_pow_mast_paths, out: *mut u64) -> c_int;

@@ -31,6 +31,28 @@ int main() {
             for (size_t len = 0; len <= 300; ++len) one(doff, soff, len);
     for (size_t len : {4095u, 4096u, 4097u, 100003u})
         for (size_t doff = 0; doff < 2; ++doff) one(doff, 3, len);
+    // the wire decode: little-endian bytes at every byte offset, values around p reduced mod p
+    const uint64_t P = 0xFFFFFFFF00000001ull;
+    const uint64_t edge[] = {0, 1, P - 1, P, P + 1, 0xFFFFFFFF00000000ull, ~0ull, 0xFFFFFFFEFFFFFFFFull,
+                             0x00000000FFFFFFFFull, 0xFFFFFFFF80000000ull};
+    std::vector<uint8_t> bytes((1 << 15) * 8 + 16);
+    std::vector<uint64_t> vals(1 << 15);
+    for (size_t i = 0; i < vals.size(); ++i) vals[i] = i % 3 ? g() : edge[(i / 3) % 10];
+    auto le_one = [&](size_t doff, size_t boff, size_t len) {
+        ++n;
+        const uint64_t GUARD = 0x5A5A5A5ADEADBEEFull;
+        for (size_t i = 0; i < len; ++i) std::memcpy(bytes.data() + boff + 8 * i, &vals[i], 8);
+        std::fill(dst.begin(), dst.begin() + doff + len + 16, GUARD);
+        nhip::copy_le_words_nt(dst.data() + 8 + doff, bytes.data() + boff, len);
+        _mm_sfence();
+        for (size_t i = 0; i < len; ++i) bad += dst[8 + doff + i] != (vals[i] >= P ? vals[i] - P : vals[i]);
+        for (size_t i = 0; i < 8 + doff; ++i) bad += dst[i] != GUARD;
+        for (size_t i = 8 + doff + len; i < doff + len + 16; ++i) bad += dst[i] != GUARD;
+    };
+    for (size_t doff = 0; doff < 4; ++doff)
+        for (size_t boff = 0; boff < 9; ++boff)
+            for (size_t len = 0; len <= 100; ++len) le_one(doff, boff, len);
+    for (size_t len : {4095u, 4096u, 32767u}) le_one(1, 5, len);
     printf("checked %llu, bad %llu\n", n, bad);
     return bad != 0;
 }

@@ -1,0 +1,107 @@
+"""bench.py's multi-GPU launch (CPU): `--gpus N` with no launcher relaunches N ranks under
+torch.distributed.run, a launcher's WORLD_SIZE must equal N, and the final cross-rank reduction
+(shard.agreed_max) ends the same way on every rank when the RCCL attempt fails on some of them
+(world-size-2 gloo).  Reference: the batch callers shard at proof granularity
+(proof_collection.rs:342-388, state/mod.rs:2226-2272); the only exchange is the verdict."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_plan_one_gpu_runs_here():
+    assert bench.launch_plan(1, {}, [])["action"] == "run"
+    assert bench.launch_plan(1, {"WORLD_SIZE": "1"}, [])["action"] == "run"
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_plan_relaunches_n_ranks(n):
+    argv = ["--gpus", str(n), "--steps", "20", "--warmup", "5"]
+    p = bench.launch_plan(n, {}, argv, n_visible=8, port=29999)
+    assert p["action"] == "relaunch" and p["world"] == n
+    cmd = p["cmd"]
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == str(n)
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[cmd.index("--master-port") + 1] == "29999"
+    assert cmd[-len(argv) - 1].endswith("bench.py") and cmd[-len(argv):] == argv
+
+
+def test_plan_under_a_launcher_is_one_rank():
+    p = bench.launch_plan(8, {"WORLD_SIZE": "8", "RANK": "3"}, [])
+    assert p == {"action": "run", "world": 8}
+
+
+@pytest.mark.parametrize("gpus,env,visible", [(2, {"WORLD_SIZE": "4"}, None), (8, {"WORLD_SIZE": "1"}, None),
+                                               (8, {}, 1), (0, {}, None)])
+def test_plan_mismatch_is_an_error(gpus, env, visible):
+    p = bench.launch_plan(gpus, env, [], n_visible=visible)
+    assert p["action"] == "error" and p["message"]
+
+
+def test_mismatch_exits_nonzero_before_any_work():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3"], env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 2 and "WORLD_SIZE=2 but --gpus 3" in out.stderr
+    assert out.stdout == ""
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _agree_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from neptune_hip import shard
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    vals = [1.5 + rank, float(rank == 1), 0.0]
+
+    def fails_on_rank1(v):
+        if dist.get_rank() == 1:
+            raise RuntimeError("simulated RCCL fault")
+        return [x * 100 for x in v]  # a value the host path never produces: shows which path was taken
+
+    def works(v):
+        return [x + 1000 for x in v]
+
+    a = shard.agreed_max(vals, dist, fails_on_rank1)
+    b = shard.agreed_max(vals, dist, works)
+    c = shard.agreed_max(vals, dist, None)
+    # the collectives after the reduction still line up on every rank
+    perms = shard.all_ok(True, dist)
+    q.put((rank, a, b, c, perms))
+    dist.destroy_process_group()
+
+
+def test_agreed_fallback_when_one_rank_fails():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    (r0, a0, b0, c0, p0), (r1, a1, b1, c1, p1) = res
+    want = [2.5, 1.0, 0.0]  # the MAX over ranks, on the host group
+    assert a0[0] == a1[0] == want and a0[1] is False and a1[1] is False
+    assert a0[2] is None and "simulated RCCL fault" in a1[2]
+    assert b0[1] is True and b1[1] is True and b0[0] == [1001.5, 1000.0, 1000.0] and b1[0] == [1002.5, 1001.0, 1000.0]
+    assert c0[0] == c1[0] == want and not c0[1] and not c1[1]
+    assert p0 is True and p1 is True

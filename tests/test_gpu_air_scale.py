@@ -3,7 +3,7 @@ Cargo.lock:4194, ~600 constraints, tens of thousands of circuit nodes after degr
 the synthetic AIR with 620 constraints, bloated to ~22k nodes by identically-zero terms
 (stark_ref.bloat_air: same constraint values, real evaluation work).  Its compiled program (the
 liveness-priority schedule of stark_host.cpp air_compile) keeps every value in LDS; the same circuit
-with the LDS part capped (NHIP_OOD_LDS_SLOTS at creation) runs k_ood_air's global-memory slot
+with the LDS part capped (nhip_air_create_ex's lds_slots) runs k_ood_air's global-memory slot
 overflow.  An accepting proof and mutated ones give the oracle's verdicts either way, and the
 Fiat-Shamir transcript is the oracle's."""
 import numpy as np
@@ -16,7 +16,7 @@ import tip5_ref as T
 pytestmark = pytest.mark.gpu
 
 
-def test_triton_air_sized_circuit_matches_oracle_in_lds_and_with_global_slots(ctx, monkeypatch):
+def test_triton_air_sized_circuit_matches_oracle_in_lds_and_with_global_slots(ctx):
     import neptune_hip.stark as NS
     T.use_c_backend()
     params = S.StarkParams()
@@ -28,9 +28,7 @@ def test_triton_air_sized_circuit_matches_oracle_in_lds_and_with_global_slots(ct
     gair = NS.Air(big.to_words())
     info = gair.info()
     assert info["global_slots"] == 0 and info["lds_slots"] < 4000, info  # the schedule fits LDS
-    monkeypatch.setenv("NHIP_OOD_LDS_SLOTS", "600")
-    gair_g = NS.Air(big.to_words())
-    monkeypatch.delenv("NHIP_OOD_LDS_SLOTS")
+    gair_g = NS.Air(big.to_words(), lds_slots=600)
     info_g = gair_g.info()
     assert info_g["lds_slots"] == 600 and info_g["global_slots"] > 1000, info_g  # the overflow path
     items = S.decode_proof(proof, params)

@@ -67,16 +67,11 @@ def _run_program(off, ins, consts, inputs, n_cons, n_slots):
                                                         ("triton-size", 1024, None, None),
                                                         ("triton-size", 512, 600, None),
                                                         ("triton-size", 512, None, 1200)])
-def test_compiled_program_is_a_race_free_schedule_of_the_circuit(airs, monkeypatch, name, width, lds_cap, budget):
+def test_compiled_program_is_a_race_free_schedule_of_the_circuit(airs, name, width, lds_cap, budget):
     import neptune_hip.stark as NS
     air = airs[name]
-    if width:
-        monkeypatch.setenv("NHIP_OOD_STEP_WIDTH", str(width))
-    if lds_cap:
-        monkeypatch.setenv("NHIP_OOD_LDS_SLOTS", str(lds_cap))
-    if budget:  # a tight working-slot budget: nodes wait unless they retire a value
-        monkeypatch.setenv("NHIP_OOD_SLOT_BUDGET", str(budget))
-    g = NS.Air(air.to_words())
+    # budget: a tight working-slot budget (nodes wait unless they retire a value)
+    g = NS.Air(air.to_words(), lds_slots=lds_cap or 0, step_width=width or 0, slot_budget=budget or 0)
     info = g.info()
     off, ins = g.program()
     steps = len(off) - 1
