@@ -1145,7 +1145,7 @@ def main():
     ap.add_argument("--input-form", default="montgomery", choices=("montgomery", "canonical"),
                     help="how the proof / claim words reach the library: twenty-first's in-memory Montgomery "
                          "words (default: what the Rust drop-in hands over, Proof.0 as it lies) or canonical values")
-    ap.add_argument("--group-batches", type=int, default=6,
+    ap.add_argument("--group-batches", type=int, default=16,
                     help="group_stream leg: submissions of the job's batch through nhip_group_stream over every GPU "
                          "of the job from rank 0 (0 = skip)")
     ap.add_argument("--iso-steps", type=int, default=ISO_STEPS,
@@ -1170,7 +1170,7 @@ def main():
                     help="steps in flight of the config-5 leg (default: the bench's depth for its size)")
     ap.add_argument("--config5-proofs", type=int, default=64,
                     help="config-5 leg at N = 1: proofs at log2 padded height 23 (0 = skip)")
-    ap.add_argument("--node-batches", type=int, default=6,
+    ap.add_argument("--node-batches", type=int, default=16,
                     help="node leg (config 4): batches of wire bytes decoded into per-GPU pinned arenas and "
                          "verified through nhip_group_stream_submit_placed from rank 0 (0 = skip)")
     ap.add_argument("--stream-batches", type=int, default=6,
@@ -1782,6 +1782,14 @@ def main():
         t = time.time()
         res["config5"] = config5_leg(ctx, gair, stark, args.config5_proofs, inflight=args.config5_inflight)
         correct = correct and res["config5"]["verdicts_correct"]
+        if args.config5_proofs >= 16:
+            # the N = 8 rank's share of config 5 (64 / 8 = 8 proofs per GPU), in the same shape
+            sh5 = config5_leg(ctx, gair, stark, args.config5_proofs // 8)
+            correct = correct and sh5["verdicts_correct"]
+            res["config5"]["share_n8"] = {k: sh5[k] for k in ("value", "unit", "ms_per_step", "steps", "inflight",
+                                                              "alone_ms", "transcript_equals_oracle",
+                                                              "verdicts_correct")}
+            res["config5"]["share_n8"]["proofs"] = args.config5_proofs // 8
         log(f"[config5] {res['config5']['value']:.0f} proofs/s ({time.time() - t:.1f}s)")
     if world == 1 and args.config1_seconds > 0 and not args.no_cpu:
         res["config1_latency"] = config1_latency(ctx, gair, stark, air_words, args.config1_seconds)

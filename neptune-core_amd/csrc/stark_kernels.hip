@@ -162,11 +162,9 @@ __global__ void __launch_bounds__(64) k_decode(const uint64_t* __restrict__ word
 // the two-row "pair" Tip5 (one proof per 32 lanes, PAIR = true: about a quarter fewer dependent
 // instructions per permutation again, at ~1.5x the lane-instructions; used for batches small
 // enough that the sponge replay is on the critical path with most SIMDs idle).  Both rows of a
-// pair hold the same state; only row 0 writes.  LAT: the row form with the carry-light arithmetic
-// (mont_mul_lat / mds_reduce_ark_lat: a shorter dependent chain per permutation, more
-// instructions), for batches whose sponge replay sits on the critical path (A/B:
-// NHIP_FS_ROW_LAT_MAX).
-template <bool PAIR, bool MW, bool LAT = false>
+// pair hold the same state; only row 0 writes.  (The row form with the carry-light arithmetic was
+// measured for the mid sizes and not kept: history §3.)
+template <bool PAIR, bool MW>
 __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restrict__ words,
                                                         const ProofDesc* __restrict__ desc,
                                                         const FsOp* __restrict__ ops, uint32_t n_proofs,
@@ -188,7 +186,7 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
     for (int j = 0; j < 8; ++j) cm[j] = h ? TIP5_MDS[j + 8] : TIP5_MDS[j];
     auto permute = [&](uint64_t st) {
         if constexpr (PAIR) return tip5_permute_pair(st, e, h, rc, cm, lds.lut);
-        else return tip5_permute_wide<LAT>(st, e, rc, lds.lut);
+        else return tip5_permute_wide<false>(st, e, rc, lds.lut);
     };
     const bool writer = h == 0;
     const ProofDesc& d = desc[g];
@@ -384,6 +382,52 @@ __global__ void __launch_bounds__(256, NHIP_ROWS_WAVES) k_hash_rows(const uint64
 #pragma unroll
         for (int q = 0; q < 5; ++q) o[q] = s[q];
     }
+}
+
+// Small batches: the same row hashing with one 16-lane DPP row per revealed row (tip5_permute_wide,
+// carry-light).  The lane form above gives each row one lane, so a main row's 38 absorbs are 38
+// dependent lane-form permutations (~7,000 VALU each on one lane): 1.8 ms for config 5's 8 / 64 proofs
+// alone, the longest phase of a small batch and the one the Merkle climb waits for.  Here a
+// permutation is ~10x fewer dependent instructions (at ~1.7x the lane form's VALU per permutation,
+// which a small batch's idle SIMDs absorb); each lane e keeps state word e, lanes 0..9 load the
+// chunk's words (10 lanes read a row's 80 contiguous bytes), the next chunk's word is loaded before
+// the permutation so its latency hides behind it.  Every digest is the lane form's (same sponge:
+// hash_varlen with the rate overwritten per chunk, padding 1 then 0s).
+template <bool MW>
+__global__ void __launch_bounds__(256) k_hash_rows_wide(const uint64_t* __restrict__ words,
+                                                        const ProofDesc* __restrict__ desc, uint32_t n_proofs,
+                                                        uint32_t k, StarkDims dims, uint64_t* __restrict__ dig,
+                                                        const uint32_t* __restrict__ fail) {
+    latency_priority();
+    __shared__ Tip5Lds t5;
+    tip5_lds_init(t5);  // includes the barrier: every exit below comes after it
+    const uint32_t tree = blockIdx.y;
+    const uint32_t width = tree == 0 ? dims.num_main : (tree == 1 ? 3 * dims.num_aux : 3 * dims.num_quot_seg);
+    const uint32_t e = threadIdx.x & 15u;
+    const uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;  // uniform within the row
+    if (t >= (uint64_t)n_proofs * k) return;
+    const uint32_t p = (uint32_t)(t / k), j = (uint32_t)(t % k);
+    if (fail[p]) return;
+    const ProofDesc& d = desc[p];
+    const uint64_t* __restrict__ row =
+        words + (tree == 0 ? d.main_rows_off : (tree == 1 ? d.aux_rows_off : d.quot_rows_off)) + (uint64_t)j * width;
+    uint64_t rcs[TIP5_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < TIP5_ROUNDS; ++r) rcs[r] = c_tip5_rc_raw[r * 16 + e];
+    const uint32_t nchunks = width / TIP5_RATE + 1;
+    auto chunk_word = [&](uint32_t c) -> uint64_t {
+        const uint32_t pos = c * TIP5_RATE;
+        if (c + 1 < nchunks) return e < TIP5_RATE ? word_mont<MW>(row[pos + e]) : 0ull;
+        const uint32_t rem = width - pos;  // the padded chunk: words, then 1, then 0s
+        return e < rem ? word_mont<MW>(row[pos + e]) : (e == rem ? MONT_ONE : 0ull);
+    };
+    uint64_t s = 0, next = chunk_word(0);
+    for (uint32_t c = 0; c < nchunks; ++c) {
+        if (e < TIP5_RATE) s = next;  // absorb: the rate is overwritten, the capacity kept
+        if (c + 1 < nchunks) next = chunk_word(c + 1);
+        s = tip5_permute_wide<true>(s, e, rcs, t5.lut);
+    }
+    if (e < 5) dig[(((uint64_t)p * 3 + tree) * k + j) * 5 + e] = s;
 }
 
 // ------------------------------------------------------------------ workgroup helpers
@@ -1622,12 +1666,13 @@ static uint64_t climb_from_ops(uint32_t hash_levels) {
     return hash_levels >= CLIMB_FROM_MIN_LEVELS ? CLIMB_FROM_OPS_DEFAULT : 0ull;
 }
 
-// row-form batches below this many proofs replay with the carry-light arithmetic (A/B knob
-// NHIP_FS_ROW_LAT_MAX; default 0 = never)
-static uint32_t fs_row_lat_max() {
+
+// batches of at most this many proofs hash their revealed rows in the 16-lane form (k_hash_rows_wide)
+static constexpr uint32_t ROWS_WIDE_MAX_PROOFS = 32;
+static uint32_t rows_wide_max() {
     static const uint32_t v = [] {
-        const char* e = nhip::ab_env("NHIP_FS_ROW_LAT_MAX");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+        const char* e = nhip::ab_env("NHIP_ROWS_WIDE_MAX");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : ROWS_WIDE_MAX_PROOFS;
     }();
     return v;
 }
@@ -1725,9 +1770,6 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     else if (ff == FS_QUAD)
         hipLaunchKernelGGL(k_fs_replay_quad<MW>, dim3((n * 4 + quad_wg() - 1) / quad_wg()), dim3(quad_wg()), 0, sa, b.words, b.desc, b.ops, n,
                            b.xs, b.idx, b.fail, age_sponge);
-    else if (n < fs_row_lat_max())
-        hipLaunchKernelGGL((k_fs_replay_wide<false, MW, true>), dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words,
-                           b.desc, b.ops, n, b.xs, b.idx, b.fail, age_sponge);
     else
         hipLaunchKernelGGL((k_fs_replay_wide<false, MW>), dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
                            b.ops, n, b.xs, b.idx, b.fail, age_sponge);
@@ -1746,8 +1788,12 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
         if (gx > 16384) gx = 16384;
         // dispatch begin / end events (the row kernel's own duration, as the kernel trace has it)
         hipEvent_t r0 = tm->launch_events ? tm->rev[0] : nullptr, r1 = tm->launch_events ? tm->rev[1] : nullptr;
-        hipExtLaunchKernelGGL(k_hash_rows<MW>, dim3(gx, 3), dim3(256), 0, st, r0, r1, 0, b.words, b.desc, n, k,
-                              b.dims, b.dig, b.fail, age);
+        if (n <= rows_wide_max())
+            hipExtLaunchKernelGGL(k_hash_rows_wide<MW>, dim3((unsigned)((rows * 16 + 255) / 256), 3), dim3(256), 0, st,
+                                  r0, r1, 0, b.words, b.desc, n, k, b.dims, b.dig, b.fail);
+        else
+            hipExtLaunchKernelGGL(k_hash_rows<MW>, dim3(gx, 3), dim3(256), 0, st, r0, r1, 0, b.words, b.desc, n, k,
+                                  b.dims, b.dig, b.fail, age);
     }
     mark(2, st);
     if (small) {

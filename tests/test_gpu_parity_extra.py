@@ -4,8 +4,8 @@ Tip5: DESIGN.md §4), compared transcript for transcript with the oracle on the 
   * tests/golden/config5_distinct.npz: 4 DISTINCT accepting proofs at BASELINE config 5's log2 padded
     height 23 (FRI domain 2^26, 16 folding rounds, sparse synthetic prover: non-zero codewords in every
     round, non-empty last polynomial), each with its own claim and seed;
-  * authentication-structure mutants of those proofs: one word of a main / aux / quotient
-    AuthenticationStructure item or of a FRI response's authentication path.  Fiat-Shamir does not
+  * authentication-structure mutants of those proofs: a word of a main / aux / quotient
+    AuthenticationStructure item (two per item).  Fiat-Shamir does not
     absorb these items, so the transcript stays the accepting proof's and only the Merkle check can
     reject; the 26-level trees climb per tree from the level with <= 4,096 hash ops
     (k_mp_climb from a start level) by default, and level by level with that form off
@@ -78,17 +78,15 @@ def test_config5_distinct_height23_transcripts(ctx, air_words):
 
 
 def _auth_mutants(case, params):
-    """One word of each authentication structure (main, aux, quotient) and of the first and last FRI
-    responses' authentication paths (a FriResponse is [auth digests.., revealed leaves..])."""
+    """Two words of each authentication structure (main, aux, quotient): one inside the first
+    digests, the structure's last word.  (A FRI response's words start with structural lengths,
+    which the decoder rejects before any Merkle check: covered by test_gpu_decode_fuzz.)"""
     sp = _spans(case["proof"], params)
     out = []
     auths = [s for s in sp if s[0] == S.AUTH_STRUCTURE]
-    fri = [s for s in sp if s[0] == S.FRI_RESPONSE]
+    assert len(auths) == 3
     for k, (_, lo, hi) in enumerate(auths):
-        pos = lo + 1 + (7 + 5 * k) % max(1, hi - lo - 1)
-        out.append(pos)
-    for _, lo, hi in (fri[0], fri[-1]):
-        out.append(lo + 2)  # inside the first digest of the authentication path
+        out += [lo + 1 + (7 + 5 * k) % max(1, hi - lo - 1), hi - 1]
     res = []
     for pos in out:
         m = case["proof"].copy()
