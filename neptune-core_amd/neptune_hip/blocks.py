@@ -13,7 +13,9 @@ natively (csrc/bincode.cpp) straight into the verifier's inputs.
   MAST sequences and the `TransactionProof` (SingleProof words or a `ProofCollection`), ready for
   `verifier.transactions_are_valid`.
 Proof words are copied once, reduced mod p, from the file bytes into numpy buffers that the
-verifier stages without further conversion.
+verifier stages without further conversion, or, given an `arena` (`stark.Arena`, round 6), straight
+into pinned memory on a GPU's NUMA node (nhip_arena_ingest_blocks / _spans), from where the
+verifier DMAs them as they lie.
 """
 from __future__ import annotations
 
@@ -66,8 +68,14 @@ class BlockRecord:
     proof: Optional[np.ndarray]
 
 
-def blocks_from_bytes(data, pow_tree_height: int = POW_TREE_HEIGHT) -> List[BlockRecord]:
+def blocks_from_bytes(data, pow_tree_height: int = POW_TREE_HEIGHT, arena=None) -> List[BlockRecord]:
+    """`arena`: decode the block proofs into it (pinned, on its GPUs' nodes) instead of numpy
+    buffers; each record's `proof` is then a view of the arena (valid until the arena's reset)."""
     lib = _lib.load()
+    in_arena = {}
+    if arena is not None:
+        placed, block_of = arena.ingest_blocks(data, pow_tree_height)
+        in_arena = {b: placed.words(i) for i, b in enumerate(block_of)}
     a, n = _buf(data)
     count = ctypes.c_size_t(0)
     rc = lib.nhip_blk_scan(a.ctypes.data, n, pow_tree_height, None, 0, ctypes.byref(count))
@@ -92,20 +100,21 @@ def blocks_from_bytes(data, pow_tree_height: int = POW_TREE_HEIGHT) -> List[Bloc
         claims = [Claim([int(x) for x in c.program_digest], int(c.version),
                         [int(c.input[k]) for k in range(c.input_len)],
                         [int(c.output[k]) for k in range(c.output_len)]) for c in cl[:b.n_claims]]
-        proof = (_words(lib, a, n, int(b.proof_offset), int(b.proof_len))
-                 if b.proof_kind == SINGLE_PROOF_KIND else None)
+        proof = None
+        if b.proof_kind == SINGLE_PROOF_KIND:
+            proof = in_arena[i] if i in in_arena else _words(lib, a, n, int(b.proof_offset), int(b.proof_len))
         out.append(BlockRecord(int(b.offset), int(b.size), int(b.height), int(b.timestamp),
                                tuple(int(x) for x in b.prev_block_digest), seqs[:8], seqs[8:], claims,
                                int(b.proof_kind), proof))
     return out
 
 
-def blocks_from_file_without_record(path: str, pow_tree_height: int = POW_TREE_HEIGHT) -> List[BlockRecord]:
+def blocks_from_file_without_record(path: str, pow_tree_height: int = POW_TREE_HEIGHT, arena=None) -> List[BlockRecord]:
     """import_blocks_from_files.rs:100-115 (the file is memory-mapped, as there)."""
     if os.path.getsize(path) == 0:
         return []
     with open(path, "rb") as f, mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ) as m:
-        return blocks_from_bytes(m, pow_tree_height)
+        return blocks_from_bytes(m, pow_tree_height, arena)
 
 
 def blocks_to_validate(ctx, records: Sequence[BlockRecord]):
@@ -123,10 +132,11 @@ def blocks_to_validate(ctx, records: Sequence[BlockRecord]):
 
 
 def validate_block_file(ctx, path: str, verifier, programs, network=None,
-                        pow_tree_height: int = POW_TREE_HEIGHT) -> List[Optional[str]]:
-    """Rules 1.a-1.d for every block of a blk file, all block proofs in one verifier batch."""
+                        pow_tree_height: int = POW_TREE_HEIGHT, arena=None) -> List[Optional[str]]:
+    """Rules 1.a-1.d for every block of a blk file, all block proofs in one verifier batch;
+    `arena`: the block proofs decoded straight into pinned memory (DMA'd from there)."""
     from .verifier import Network, validate_block_proofs
-    recs = blocks_from_file_without_record(path, pow_tree_height)
+    recs = blocks_from_file_without_record(path, pow_tree_height, arena)
     return validate_block_proofs(ctx, blocks_to_validate(ctx, recs), verifier, programs,
                                  network if network is not None else Network.MAIN)
 
@@ -140,7 +150,8 @@ class TransferTransaction:
     size: int
 
     @staticmethod
-    def from_bytes(data) -> "TransferTransaction":
+    def from_bytes(data, arena=None) -> "TransferTransaction":
+        """`arena`: the member proofs decoded straight into it (pinned, nhip_arena_ingest_spans)."""
         from .verifier import PROOF_COLLECTION, SINGLE_PROOF, ProofCollection, TransactionProof
         lib = _lib.load()
         a, n = _buf(data)
@@ -156,7 +167,11 @@ class TransferTransaction:
         check(lib.nhip_tx_parts(a.ctypes.data, n, ctypes.byref(t), seq.ctypes.data, offs.ctypes.data,
                                 spans.ctypes.data, dig.ctypes.data), "nhip_tx_parts")
         seqs = [seq[int(offs[j]):int(offs[j + 1])] for j in range(8)]
-        proofs = [_words(lib, a, n, int(spans[2 * i]), int(spans[2 * i + 1])) for i in range(t.n_proofs)]
+        if arena is not None:
+            pl = arena.ingest_spans(a[:n], [(int(spans[2 * i]), int(spans[2 * i + 1])) for i in range(t.n_proofs)])
+            proofs = [pl.words(i) for i in range(t.n_proofs)]
+        else:
+            proofs = [_words(lib, a, n, int(spans[2 * i]), int(spans[2 * i + 1])) for i in range(t.n_proofs)]
         if t.kind == 1:
             return TransferTransaction(seqs, TransactionProof(SINGLE_PROOF, proofs[0]), int(t.size))
         d = [tuple(int(x) for x in dig[5 * i:5 * i + 5]) for i in range(t.n_digests)]

@@ -344,6 +344,131 @@ impl GpuNode {
     pub fn arenas(&self, cap_words: usize) -> Result<Vec<ProofArena>, GpuFault> {
         (0..self.gpus()).map(|m| ProofArena::new(self, m, cap_words)).collect()
     }
+
+    /// Wire bytes to verdicts, batch after batch: each batch is a buffer of back-to-back bincode
+    /// `TransferTransaction`s as peers send them (`transfer_transaction.rs:31-47`,
+    /// `peer_loop.rs:315-323`).  The library decodes every proof straight into a pinned arena on the
+    /// NUMA node of the GPU it places the proof on (`nhip_arena_ingest_txs`) and each GPU DMAs its
+    /// share as it lies (`nhip_group_stream_submit_placed`); two arena sets, so batch k + 1 decodes on
+    /// a scoped thread while batch k uploads.  `claims(i, bytes)` returns batch i's claims in proof
+    /// order (a SingleProof's `single_proof_claim(kernel MAST hash)`, a ProofCollection's member
+    /// claims, `proof_collection.rs:286-339`); `on_verdicts(i, verdicts, all_ok)` is called in order.
+    /// The arena words are canonical (the wire form), so this stream runs `NHIP_INPUT_CANONICAL`
+    /// with canonical claim words.  A malformed transaction is `NHIP_ERR_DECODE` for its batch.
+    pub fn verify_wire_batches<'a, I, C, F>(&self, batches: I, bytes_per_gpu: usize, mut claims: C,
+                                            mut on_verdicts: F) -> Result<(), GpuFault>
+    where
+        I: IntoIterator<Item = &'a [u8]>,
+        C: FnMut(usize, &[u8]) -> Vec<Claim>,
+        F: FnMut(usize, Vec<bool>, bool),
+    {
+        struct Arena(*mut sys::nhip_arena);
+        unsafe impl Send for Arena {}
+        impl Drop for Arena {
+            fn drop(&mut self) {
+                unsafe { sys::nhip_arena_destroy(self.0) }
+            }
+        }
+        struct Stream(*mut sys::nhip_group_stream);
+        impl Drop for Stream {
+            fn drop(&mut self) {
+                unsafe { sys::nhip_group_stream_destroy(self.0) }
+            }
+        }
+        // one decoded batch: proof records into an arena and each proof's GPU
+        struct Placed(Vec<sys::nhip_proof>, Vec<u32>);
+        unsafe impl Send for Placed {}
+        let new_arena = || -> Result<Arena, GpuFault> {
+            let mut a = ptr::null_mut();
+            ok(unsafe { sys::nhip_arena_create(self.group, bytes_per_gpu, &mut a) })?;
+            Ok(Arena(a))
+        };
+        let arenas = [new_arena()?, new_arena()?];
+        let mut params = self.params;
+        params.input_form = sys::NHIP_INPUT_CANONICAL;
+        let mut st = ptr::null_mut();
+        ok(unsafe { sys::nhip_group_stream_create(self.group, self.air.0, &params, &mut st) })?;
+        let st = Stream(st);
+        let decode = |a: &Arena, bytes: &[u8]| -> Result<Placed, GpuFault> {
+            let cap = bytes.len() / 8 + 1;
+            let mut p = Placed(vec![sys::nhip_proof { words: ptr::null(), len: 0 }; cap], vec![0u32; cap]);
+            let (mut ntx, mut np, mut used) = (0usize, 0usize, 0usize);
+            ok(unsafe { sys::nhip_arena_reset(a.0) })?;
+            ok(unsafe {
+                sys::nhip_arena_ingest_txs(a.0, bytes.as_ptr(), bytes.len(), usize::MAX, p.0.as_mut_ptr(),
+                                           p.1.as_mut_ptr(), cap, &mut ntx, &mut np, &mut used)
+            })?;
+            if used != bytes.len() {
+                return Err(GpuFault(sys::NHIP_ERR_OOM));  // the batch does not fit bytes_per_gpu
+            }
+            p.0.truncate(np);
+            p.1.truncate(np);
+            Ok(p)
+        };
+        let batches: Vec<&[u8]> = batches.into_iter().collect();
+        let mut bufs: [(Vec<u8>, u8); 2] = [(Vec::new(), 0), (Vec::new(), 0)];
+        let mut next = if batches.is_empty() { None } else { Some(decode(&arenas[0], batches[0])?) };
+        for k in 0..batches.len() {
+            let cur = next.take().expect("decoded batch");
+            let cs: Vec<sys::nhip_claim> = canonical_claims(&claims(k, batches[k]));
+            if cs.len() != cur.0.len() {
+                return Err(GpuFault(sys::NHIP_ERR_ARG));
+            }
+            let slot = k & 1;
+            bufs[slot].0 = vec![0u8; cur.0.len()];
+            let (vp, ap) = (bufs[slot].0.as_mut_ptr(), &mut bufs[slot].1 as *mut u8);
+            // batch k uploads (and batch k - 1's verdicts come back) while batch k + 1 decodes
+            let (submitted, decoded) = std::thread::scope(|scope| {
+                let h = (k + 1 < batches.len()).then(|| {
+                    let (a, b) = (&arenas[(k + 1) & 1], batches[k + 1]);
+                    scope.spawn(move || decode(a, b))
+                });
+                let rc = unsafe {
+                    sys::nhip_group_stream_submit_placed(st.0, cs.as_ptr(), cur.0.as_ptr(), cur.1.as_ptr(), cur.0.len(),
+                                                         vp, ap)
+                };
+                (ok(rc), h.map(|h| h.join().unwrap_or(Err(GpuFault(sys::NHIP_ERR_HIP)))))
+            });
+            submitted?;
+            next = decoded.transpose()?;
+            if k > 0 {
+                let (v, all) = &bufs[slot ^ 1];
+                on_verdicts(k - 1, v.iter().map(|&b| b == 1).collect(), *all == 1);
+            }
+        }
+        ok(unsafe { sys::nhip_group_stream_finish(st.0) })?;
+        if let Some(k) = batches.len().checked_sub(1) {
+            let (v, all) = &bufs[k & 1];
+            on_verdicts(k, v.iter().map(|&b| b == 1).collect(), *all == 1);
+        }
+        Ok(())
+    }
+}
+
+/// Claims as canonical words (for the wire-bytes path, whose proof words are canonical): the
+/// digest, input and output `value()`s, owned by the returned structs' backing vectors.
+fn canonical_claims(claims: &[Claim]) -> Vec<sys::nhip_claim> {
+    thread_local! { static WORDS: std::cell::RefCell<Vec<Vec<u64>>> = std::cell::RefCell::new(Vec::new()); }
+    WORDS.with(|w| {
+        let mut w = w.borrow_mut();
+        w.clear();
+        claims
+            .iter()
+            .map(|c| {
+                w.push(c.input.iter().map(|b| b.value()).collect());
+                w.push(c.output.iter().map(|b| b.value()).collect());
+                let (i, o) = (&w[w.len() - 2], &w[w.len() - 1]);
+                sys::nhip_claim {
+                    program_digest: c.program_digest.values().map(|b| b.value()),
+                    version: c.version,
+                    input: i.as_ptr(),
+                    input_len: i.len(),
+                    output: o.as_ptr(),
+                    output_len: o.len(),
+                }
+            })
+            .collect()
+    })
 }
 
 impl Drop for GpuNode {

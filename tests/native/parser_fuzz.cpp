@@ -17,8 +17,12 @@
 #include <vector>
 
 #include "../../include/neptune_hip.h"
+#include "../../neptune-core_amd/csrc/host_copy.hpp"
 #include "../../neptune-core_amd/csrc/proof_codec.hpp"
 
+namespace nhip {
+bool tx_proof_spans(const uint8_t* bytes, size_t n, std::vector<uint64_t>& spans, uint64_t& size);
+}
 using namespace nhip;
 
 // ingest.cpp's nhip_claim_hash calls the GPU hash; the parsers under test never reach it
@@ -55,7 +59,7 @@ Dims dims_of(uint32_t checks, uint32_t main, uint32_t aux) {
     return D;
 }
 
-uint64_t g_ok = 0, g_runs = 0;
+uint64_t g_ok = 0, g_runs = 0, g_mismatch = 0;
 
 // the walk reads exactly words[0, n): parse from a heap copy of that size so ASan sees any overrun.
 // Both input forms (canonical values, Montgomery words): the same bytes, different structural values.
@@ -113,15 +117,30 @@ void run_blk(const std::vector<uint8_t>& b, uint32_t height) {
 void run_tx(const std::vector<uint8_t>& b) {
     nhip_tx tx{};
     ++g_runs;
-    if (nhip_tx_scan(b.data(), b.size(), &tx) != NHIP_OK) return;
+    // the arena ingest's scanner (nhip::tx_proof_spans, csrc/bincode.cpp) on an exact-size heap copy:
+    // it must agree with the scan below on validity and, when valid, on every proof span
+    std::vector<uint64_t> arena_spans;
+    uint64_t arena_size = 0;
+    const bool arena_ok = nhip::tx_proof_spans(b.data(), b.size(), arena_spans, arena_size);
+    if (nhip_tx_scan(b.data(), b.size(), &tx) != NHIP_OK) {
+        if (arena_ok) g_mismatch++;
+        return;
+    }
+    if (!arena_ok || arena_size != tx.size || arena_spans.size() != 2ull * tx.n_proofs) g_mismatch++;
     if (tx.seq_words > (1u << 24) || tx.n_proofs > (1u << 16) || tx.n_digests > (1u << 16)) return;
     std::vector<uint64_t> seq(tx.seq_words + 1), spans(2ull * tx.n_proofs + 2), dig(5ull * tx.n_digests + 5);
     uint64_t offs[9];
     if (nhip_tx_parts(b.data(), b.size(), &tx, seq.data(), offs, spans.data(), dig.data()) == NHIP_OK) {
         for (uint32_t p = 0; p < tx.n_proofs; ++p) {
+            if (arena_ok && (arena_spans[2 * p] != spans[2 * p] || arena_spans[2 * p + 1] != spans[2 * p + 1]))
+                g_mismatch++;
             if (spans[2 * p + 1] > (1u << 24)) continue;
-            std::vector<uint64_t> pw(spans[2 * p + 1] + 1);
+            std::vector<uint64_t> pw(spans[2 * p + 1] + 1), aw(spans[2 * p + 1] + 2);
             nhip_le_words(b.data(), b.size(), spans[2 * p], spans[2 * p + 1], pw.data());
+            // the arena's streaming decode of the same span (into an odd-aligned destination)
+            nhip::copy_le_words_nt(aw.data() + 1, b.data() + spans[2 * p], spans[2 * p + 1]);
+            _mm_sfence();
+            if (std::memcmp(aw.data() + 1, pw.data(), spans[2 * p + 1] * 8) != 0) g_mismatch++;
         }
         ++g_ok;
     }
@@ -197,6 +216,7 @@ int main(int argc, char** argv) {
         else if (kind == "be") fuzz(in, mutations, 8, [&](const std::vector<uint8_t>& x) { run_be(x); });
         else return 2;
     }
-    std::printf("runs %llu ok %llu\n", (unsigned long long)g_runs, (unsigned long long)g_ok);
-    return 0;
+    std::printf("runs %llu ok %llu mismatch %llu\n", (unsigned long long)g_runs, (unsigned long long)g_ok,
+                (unsigned long long)g_mismatch);
+    return g_mismatch ? 1 : 0;
 }

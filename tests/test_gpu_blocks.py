@@ -64,6 +64,11 @@ def test_block_file_validation(ctx, tmp_path):
     assert [list(t.body_mast_hash) for t in tv[:3]] == [list(h) for h in body]
     out = NB.validate_block_file(ctx, str(path), ver, progs, pow_tree_height=H)
     assert out == [None, None, V.PROOF_VALIDITY, V.PROOF_QUALITY]
+    # the same file with the block proofs decoded straight into a pinned arena on the GPU's node
+    with NS.Group([0]) as grp, NS.Arena(grp, 32 << 20) as arena:
+        out_a = NB.validate_block_file(ctx, str(path), ver, progs, pow_tree_height=H, arena=arena)
+        assert arena.member_info(0)["used_words"] == sum(len(p) for p in (proofs[0], proofs[1], proofs[0]))
+    assert out_a == out
     # the oracle accepts the two good block proofs for the same claims
     assert all(oracle_accepts(c, p) for c, p in zip(bclaims[:2], proofs[:2]))
 
@@ -97,3 +102,9 @@ def test_transfer_transactions_is_valid(ctx):
     decoded = [NB.TransferTransaction.from_bytes(B.encode_transfer_transaction(t)) for t in txs]
     items = [(tt.kernel_sequences, tt.proof) for tt in decoded]
     assert V.transactions_are_valid(ctx, items, ver, progs) == [True, True, False, True, False]
+    # member proofs decoded straight into a pinned arena (two members: each proof on the lighter one)
+    with NS.Group([0, 0]) as grp, NS.Arena(grp, 16 << 20) as arena:
+        dec_a = [NB.TransferTransaction.from_bytes(B.encode_transfer_transaction(t), arena=arena) for t in txs]
+        items_a = [(tt.kernel_sequences, tt.proof) for tt in dec_a]
+        assert V.transactions_are_valid(ctx, items_a, ver, progs) == [True, True, False, True, False]
+        assert min(arena.member_info(m)["used_words"] for m in range(2)) > 0

@@ -54,8 +54,10 @@ def test_parsers_clean_under_asan_ubsan(fuzz_bin, tmp_path):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
     r = subprocess.run([fuzz_bin, "3000"] + args, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
-    runs, ok = (int(x) for x in r.stdout.split()[1::2])
-    assert runs > 20000 and ok > 0, r.stdout
+    runs, ok, mismatch = (int(x) for x in r.stdout.split()[1::2])
+    # mismatch: the arena ingest's scanner or its streaming decode disagreeing with nhip_tx_scan /
+    # nhip_tx_parts / nhip_le_words on any (mutated) transaction
+    assert runs > 20000 and ok > 0 and mismatch == 0, r.stdout
 
 
 def test_queue_receive_ring_under_asan_ubsan(fuzz_bin):
