@@ -742,6 +742,9 @@ def queue_leg(ctx, gair, stark, claims, proofs, expect, callers: int = 64, round
     return {"callers": callers, "calls": len(calls), "value": len(calls) / dt, "unit": "proofs/s",
             "serialized_one_proof_calls": rate_ser, "vs_serialized": len(calls) / dt / rate_ser,
             "latency_ms": _pcts(lib_lat), "latency_ms_python_caller": _pcts(np.asarray(lat) * 1e3),
+            # without each caller's first call (the 64 callers released at once by the barrier)
+            "latency_ms_python_caller_after_first": _pcts(np.asarray([x for j, x in enumerate(lat) if j % rounds])
+                                                          * 1e3),
             "proofs_per_batch": prof.get("proofs", 0) / nb, "batches": prof.get("batches", 0),
             "per_batch_ms": {k: prof.get(k, 0.0) / nb for k in ("ms_window", "ms_stage", "ms_upload", "ms_launch",
                                                                  "ms_device", "ms_wait", "ms_turnaround")},

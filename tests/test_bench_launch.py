@@ -105,3 +105,22 @@ def test_agreed_fallback_when_one_rank_fails():
     assert b0[1] is True and b1[1] is True and b0[0] == [1001.5, 1000.0, 1000.0] and b1[0] == [1002.5, 1001.0, 1000.0]
     assert c0[0] == c1[0] == want and not c0[1] and not c1[1]
     assert p0 is True and p1 is True
+
+
+def test_tx_stream_is_what_the_node_leg_decodes():
+    """bench.tx_stream (the node leg's wire bytes): back-to-back SingleProof TransferTransactions that
+    the native scanner (host only) splits back into exactly the proofs, in order."""
+    sys.path.insert(0, os.path.join(ROOT, "neptune-core_amd"))
+    import numpy as np
+    from neptune_hip import blocks as NB
+    _, pool = bench.load_pool()
+    proofs = [pool[h]["proof"] for h in sorted(pool)][:3] * 2
+    buf = bench.tx_stream(proofs)
+    pos, got = 0, []
+    while pos < buf.size:
+        tt = NB.TransferTransaction.from_bytes(buf[pos:])
+        got.append(tt.proof.payload)
+        pos += tt.size
+    assert pos == buf.size and len(got) == len(proofs)
+    for a, b in zip(got, proofs):
+        assert np.array_equal(np.asarray(a, dtype=np.uint64), np.asarray(b, dtype=np.uint64))
