@@ -339,6 +339,10 @@ def pipelined(batches, steps: int, inflight: int, expect):
     return time.perf_counter() - t, ok
 
 
+# resident batches of at most this many proofs replay their launches from a HIP graph
+# (nhip_batch_set_graph)
+GRAPH_MAX = 1024
+
 # batches of at most this many proofs run every phase on one stream (nhip_batch_set_streams) at
 # twice the depth: config 5's 8 / 64 proofs +17% / +13%; config 4's 512-4,096 lose 10-23% that way
 # (profiles/r05z/ab/single_stream_ab_r05l.txt)
@@ -559,12 +563,14 @@ def config1_latency(ctx, gair, stark, air_words, cpu_seconds: float, reps: int =
                         f"(oracle/stark_oracle.c)"}
 
 
-def config5_leg(ctx, gair, stark, proofs_n: int = 64, steps: int = 20, inflight: int = None):
+def config5_leg(ctx, gair, stark, proofs_n: int = 64, steps: int = 200, inflight: int = None):
     """BASELINE config 5 beside the headline: `proofs_n` proofs at log2 padded height 23 (FRI domain
     2^26, 16 folding rounds) on one GPU.  The proof is tests/golden/deep_fri.npz's height-23 case
     (the sparse synthetic prover: every FRI codeword non-zero, a non-empty last polynomial), its
     words copied once per proof; `inflight` resident batches (default: the bench's depth for that
-    batch size, 10 below 1,024 proofs), `steps` steps after 3 warm-up steps.
+    batch size, 20 for <= 64 proofs on one stream each), `steps` steps after 3 warm-up steps (200: a
+    stream of tiny batches in its steady state; 20 steps at 20 in flight would time one pipeline fill,
+    the host enqueueing 20 batches back to back while the first ones run).
     Beside the rate: one batch alone (phase split; the sequential Fiat-Shamir sponge replay's share
     of that batch's device time) and proof 0's transcript against the oracle's, stored with the
     fixture."""
@@ -582,12 +588,14 @@ def config5_leg(ctx, gair, stark, proofs_n: int = 64, steps: int = 20, inflight:
     nstreams = int(os.environ.get("NHIP_BENCH_C5_STREAMS", "0")) or streams_for(proofs_n)  # A/B: 2 = two streams
     ring = [NS.Batch(ctx, gair, stark, ncl, prs).set_streams(nstreams) for _ in range(inflight)]
     ok = True
-    # alone: phase split and the transcript
+    # alone: phase split (a direct launch) and the transcript; then every batch replays its graph
     v, _ = ring[0].run()
     alone = ring[0].stats()
     xs, idx, fail = ring[0].transcript(0)
     transcript_ok = fail == 0 and xs == samples and idx == indices
     ok = ok and bool(np.asarray(v, dtype=bool).all()) and transcript_ok
+    for b in ring:
+        b.set_graph(True)
 
     def region(k):
         nonlocal ok
@@ -1356,7 +1364,9 @@ def main():
     stark = NS.Stark.default().montgomery() if mont else NS.Stark.default()
     ncl = [NS.Claim(*c) for c in dev_claims]
     # R resident copies of the raw proof words (each step decodes them on the device again)
-    ring = [NS.Batch(ctx, gair, stark, ncl, dev_proofs).set_streams(streams_for(n)) for _ in range(R)]
+    # resident batches of <= 1,024 proofs (the N >= 4 ranks' shares) replay a captured HIP graph
+    ring = [NS.Batch(ctx, gair, stark, ncl, dev_proofs).set_streams(streams_for(n)).set_graph(n <= GRAPH_MAX)
+            for _ in range(R)]
     prep_s = time.time() - t0
     st0 = ring[0].stats()
     log(f"[rank {rank}] batch ready: {n} proofs x {R} resident copies, {st0['proof_words']} words, "
@@ -1745,7 +1755,7 @@ def main():
         scl, spr = device_form(sc, sp, mont)
         sn = [NS.Claim(*c) for c in scl]
         Rs = default_inflight(len(sp))  # the rank's own depth (its default host exchange holds no GPU streams)
-        sring = [NS.Batch(ctx, gair, stark, sn, spr) for _ in range(Rs)]
+        sring = [NS.Batch(ctx, gair, stark, sn, spr).set_graph(len(spr) <= GRAPH_MAX) for _ in range(Rs)]
         kernel_timing(sring, region_timing)
         pipelined(sring, args.warmup, Rs, se)
         ctx.synchronize()

@@ -261,6 +261,13 @@ int nhip_batch_set_launch_timing(nhip_batch *batch, int on);
  * every phase in order on one stream (one hardware queue), so twice as many batches fit in flight —
  * for many tiny batches at once (e.g. 8-64 proofs each).  NHIP_ERR_ARG while in flight. */
 int nhip_batch_set_streams(nhip_batch *batch, int streams);
+/* on != 0: every later untimed launch replays the batch's launch sequence from a captured HIP graph
+ * (one submission instead of ~25 runtime calls), captured now and again after a refill or a stream
+ * change — for resident batches of at most 1,024 proofs relaunched many times (a pipeline enqueueing
+ * batches back to back otherwise delays each batch's device start by the host enqueues before it).
+ * A replayed launch reports no phase split (nhip_stats phase fields 0; launch timing on = direct).
+ * NHIP_ERR_ARG while in flight or past 1,024 proofs. */
+int nhip_batch_set_graph(nhip_batch *batch, int on);
 /* Fiat-Shamir replay form of later launches, process-wide (tests and A/B runs): -1 = chosen by the
  * batch size (default), 0 = 16-lane row, 1 = two-row pair, 2 = quad.  NHIP_ERR_ARG otherwise. */
 int nhip_set_fs_form(int form);

@@ -145,7 +145,8 @@ extern "C" {
 // nhip_set_host_threads)
 // 2200: nhip_batch_set_launch_timing (per-dispatch timestamps off by default), nhip_batch_set_streams
 // 2300: nhip_air_create_ex (compiler options instead of environment variables), nhip_set_climb_from_ops,
-// the per-member proof arenas (nhip_arena_*, nhip_group_stream_submit_placed)
+// the per-member proof arenas (nhip_arena_*, nhip_group_stream_submit_placed), nhip_queue_latencies,
+// nhip_batch_set_graph
 int nhip_abi_version(void) { return 2300; }
 
 int nhip_set_fs_form(int form) { return nhip::set_fs_form(form) == 0 ? NHIP_OK : NHIP_ERR_ARG; }

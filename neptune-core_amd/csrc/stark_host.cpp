@@ -199,6 +199,14 @@ struct nhip_batch {
         double decode, fs, rows, plan, hash, roots, ood, fri, deep, total;
     } ph{};
     double stage_ms = 0, upload_ms = 0;
+    // The batch's launch sequence captured into a HIP graph (nhip_batch_set_graph): replayed by every
+    // untimed launch while the contents and streams are unchanged, captured again at the next launch
+    // after a refill or a stream change.  The capture records its own fork / join events (gev): an
+    // event once captured into a graph cannot be recorded on a stream again.
+    hipGraphExec_t gexec = nullptr;
+    bool graph_on = false;
+    bool last_graph = false;  // the last launch replayed the graph (no phase timestamps)
+    hipEvent_t gev[STARK_EVENTS] = {};
     double mp_hash_exec_ms = 0;  // summed dispatch durations of the hash launches
     double row_hash_exec_ms = 0;  // the row-hashing launch's dispatch duration
     uint64_t merkle_perms = 0;
@@ -1050,8 +1058,14 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
 static int launch_resources(nhip_batch* b);
 // A resident batch: prepared, and its launch resources made now rather than at its first launch (a
 // failure there is left to the launch to report)
+static void drop_graph(nhip_batch* b);
+
 static int prepare_resident(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, const nhip_claim* claims,
                             const nhip_proof* proofs, size_t n, nhip_batch** out, nhip_batch* reuse) {
+    if (reuse && !reuse->in_flight) {  // new contents: the captured launch sequence is stale
+        const DeviceScope device_scope(reuse->device);
+        drop_graph(reuse);
+    }
     const int rc = batch_prepare(ctx, air, sp, claims, proofs, n, out, nullptr, reuse);
     if (rc != NHIP_OK || !*out) return rc;
     std::lock_guard<std::mutex> g(*nhip_internal_mutex(ctx));
@@ -1140,6 +1154,66 @@ static int launch_resources(nhip_batch* b) {
     return NHIP_OK;
 }
 
+// Every device phase of the batch, its counter resets and its readback, on the batch's streams.
+static hipError_t enqueue_batch(nhip_batch* b) {
+    hipStream_t st = b->main;
+    const uint32_t n = b->dev.n_proofs;
+    const size_t cnt_bytes = (size_t)b->dev.mp.levels * MP_SHARDS * 4;
+    hipError_t e = hipMemsetAsync(b->dev.counters, 0, CNT_N * 8, st);
+    if (e == hipSuccess && cnt_bytes) e = hipMemsetAsync(b->dev.mp.counter, 0, cnt_bytes, st);
+    if (e == hipSuccess) e = launch_stark_phases(b->dev, st, b->aux, &b->tm);
+    if (e == hipSuccess) e = hipMemcpyAsync(b->h_out, b->dev.counters, CNT_N * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && cnt_bytes) e = hipMemcpyAsync(b->h_out + OUT_HDR, b->dev.mp.counter, cnt_bytes, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && n) e = hipMemcpyAsync(b->h_out + OUT_HDR + cnt_bytes, b->dev.verdicts, n, hipMemcpyDeviceToHost, st);
+    return e;
+}
+
+static void drop_graph(nhip_batch* b) {
+    if (b->gexec) (void)hipGraphExecDestroy(b->gexec);
+    b->gexec = nullptr;
+}
+
+// The graph bakes in the launch-order wave priority, which applies from 2,048 proofs on: larger
+// batches always launch directly.
+static constexpr uint32_t GRAPH_MAX_PROOFS = 1024;
+static bool graphs_enabled() {  // NHIP_GRAPHS=0 (A/B builds only): every launch direct
+    static const bool on = [] {
+        const char* e = nhip::ab_env("NHIP_GRAPHS");
+        return !e || e[0] != '0';
+    }();
+    return on;
+}
+
+// Capture the batch's launch sequence (its two streams joined, as enqueue_batch leaves them) into an
+// executable graph, with the capture's own events; false (and no graph) if the runtime cannot
+// capture it: the direct launch is used then.
+static bool capture_graph(nhip_batch* b) {
+    if (!b->gev[0])
+        for (int i = 0; i < STARK_EVENTS; ++i)
+            if (hipEventCreateWithFlags(&b->gev[i], hipEventDisableTiming) != hipSuccess) return false;
+    hipGraph_t graph = nullptr;
+    if (hipStreamBeginCapture(b->main, hipStreamCaptureModeThreadLocal) != hipSuccess) return false;
+    StarkPhaseTimer saved = b->tm;
+    for (int i = 0; i < STARK_EVENTS; ++i) b->tm.ev[i] = b->gev[i];
+    const hipError_t e = enqueue_batch(b);
+    b->tm = saved;
+    const hipError_t ee = hipStreamEndCapture(b->main, &graph);
+    if (e != hipSuccess || ee != hipSuccess || !graph) {
+        if (graph) (void)hipGraphDestroy(graph);
+        (void)hipGetLastError();
+        return false;
+    }
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ei != hipSuccess || !exec) {
+        (void)hipGetLastError();
+        return false;
+    }
+    b->gexec = exec;
+    return true;
+}
+
 // Enqueue every device phase of the batch on the batch's own two streams (no host wait).  Batches
 // launched back to back run concurrently on the device.
 int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
@@ -1148,20 +1222,35 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
     const DeviceScope device_scope(b->device);
     if (b->in_flight) return NHIP_ERR_ARG;
     if (int rc = launch_resources(b)) return rc;
-    hipStream_t st = b->main;
-    const uint32_t n = b->dev.n_proofs;
     hipError_t e = hipSuccess;
-    const size_t cnt_bytes = (size_t)b->dev.mp.levels * MP_SHARDS * 4;
-    e = hipMemsetAsync(b->dev.counters, 0, CNT_N * 8, st);
-    if (e == hipSuccess && cnt_bytes) e = hipMemsetAsync(b->dev.mp.counter, 0, cnt_bytes, st);
-    if (e != hipSuccess) return hipfail(e);
-    e = launch_stark_phases(b->dev, st, b->aux, &b->tm);
-    if (e != hipSuccess) return hipfail(e);
-    if (e == hipSuccess) e = hipMemcpyAsync(b->h_out, b->dev.counters, CNT_N * 8, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess && cnt_bytes) e = hipMemcpyAsync(b->h_out + OUT_HDR, b->dev.mp.counter, cnt_bytes, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess && n) e = hipMemcpyAsync(b->h_out + OUT_HDR + cnt_bytes, b->dev.verdicts, n, hipMemcpyDeviceToHost, st);
+    const bool graphable = b->graph_on && !b->tm.launch_events && b->dev.n_proofs <= GRAPH_MAX_PROOFS;
+    if (graphable && !b->gexec) (void)capture_graph(b);  // after a refill or a stream change
+    b->last_graph = graphable && b->gexec;
+    if (b->last_graph) e = hipGraphLaunch(b->gexec, b->main);
+    else e = enqueue_batch(b);
     if (e != hipSuccess) return hipfail(e);
     b->in_flight = true;
+    return NHIP_OK;
+}
+
+// Replay the batch's launch sequence from a captured HIP graph (on != 0): one submission per launch
+// instead of ~25 runtime calls, for resident batches of at most 1,024 proofs relaunched many times
+// (a pipeline enqueueing R batches back to back delays the device's start of the last one by R host
+// enqueues, ~0.2 ms each at 512 proofs).  A launch with launch timing on is always direct; a replayed
+// launch reports no phase split (nhip_stats phase fields 0).  NHIP_ERR_ARG while in flight or for a
+// batch past 1,024 proofs; a runtime that cannot capture leaves the direct launch (NHIP_OK).
+int nhip_batch_set_graph(nhip_batch* b, int on) {
+    if (!b || b->in_flight || b->scratch) return NHIP_ERR_ARG;
+    if (on && b->dev.n_proofs > GRAPH_MAX_PROOFS) return NHIP_ERR_ARG;
+    if (on && !graphs_enabled()) return NHIP_OK;  // an A/B build with graphs off: direct launches
+    const DeviceScope device_scope(b->device);
+    b->graph_on = on != 0;
+    if (!b->graph_on) {
+        drop_graph(b);
+        return NHIP_OK;
+    }
+    if (int rc = launch_resources(b)) return rc;
+    if (!b->gexec) (void)capture_graph(b);  // now, before the batch's first replay
     return NHIP_OK;
 }
 
@@ -1170,7 +1259,7 @@ int nhip_batch_launch(nhip_ctx* ctx, nhip_batch* b) {
 // they cost a small batch ~2% of its rate and the product paths do not read them.
 int nhip_batch_set_launch_timing(nhip_batch* b, int on) {
     if (!b || b->in_flight) return NHIP_ERR_ARG;
-    b->tm.launch_events = on != 0;
+    b->tm.launch_events = on != 0;  // a timed launch is never the graph (its events are per launch)
     return NHIP_OK;
 }
 
@@ -1184,15 +1273,19 @@ int nhip_batch_set_streams(nhip_batch* b, int streams) {
     if (!b || b->in_flight || b->scratch || (streams != 1 && streams != 2)) return NHIP_ERR_ARG;
     const DeviceScope device_scope(b->device);
     if (int rc = launch_resources(b)) return rc;
+    const bool had_graph = b->gexec != nullptr;
     if (streams == 1 && b->aux != b->main) {
+        drop_graph(b);
         (void)hipStreamSynchronize(b->aux);
         (void)hipStreamDestroy(b->aux);
         b->aux = b->main;
     } else if (streams == 2 && b->aux == b->main) {
+        drop_graph(b);
         hipStream_t s2 = nullptr;
         if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess) return NHIP_ERR_HIP;
         b->aux = s2;
     }
+    if (had_graph && b->graph_on && !b->gexec) (void)capture_graph(b);  // the new stream layout, now
     return NHIP_OK;
 }
 
@@ -1246,7 +1339,9 @@ int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* al
         (void)hipEventElapsedTime(&ms, b->tm.ev[a], b->tm.ev[c]);
         return (double)ms;
     };
-    if (n) {
+    if (b->last_graph) {
+        b->ph = {};  // a replayed launch: its events are the graph's own, untimed
+    } else if (n) {
         b->ph.decode = el(12, 0);
         b->ph.fs = el(0, 1);
         b->ph.rows = el(0, 2);
@@ -1336,6 +1431,9 @@ void nhip_batch_destroy(nhip_batch* b) {
     if (!b) return;
     const DeviceScope device_scope(b->device);
     if (b->in_flight && b->main) (void)hipStreamSynchronize(b->main);
+    drop_graph(b);
+    for (hipEvent_t e : b->gev)
+        if (e) (void)hipEventDestroy(e);
     if (b->scratch) {  // resources belong to the context's verify scratch
         delete b;
         return;

@@ -1632,6 +1632,16 @@ __global__ void k_verdicts(const uint32_t* __restrict__ fail, uint32_t n, uint8_
 }
 
 // ------------------------------------------------------------------ launchers
+// A launch with dispatch begin / end events when given (hipExtLaunchKernel: the launch-timing
+// passes), a plain launch otherwise, so an untimed batch's launch sequence can be captured into a
+// HIP graph (nhip_batch_launch).
+template <typename K, typename... A>
+static void launch_ev(K kernel, dim3 grid, dim3 block, size_t shm, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+                      A... args) {
+    if (e0 || e1) hipExtLaunchKernelGGL(kernel, grid, block, shm, s, e0, e1, 0, args...);
+    else hipLaunchKernelGGL(kernel, grid, block, shm, s, args...);
+}
+
 // OOD evaluator workgroup: 1,024 threads for batches of at most OOD_WIDE_MAX_PROOFS proofs
 // (NHIP_OOD_WIDE_MAX overrides, A/B runs), else 256
 static bool ood_wide(uint32_t n) {
@@ -1789,10 +1799,10 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
         // dispatch begin / end events (the row kernel's own duration, as the kernel trace has it)
         hipEvent_t r0 = tm->launch_events ? tm->rev[0] : nullptr, r1 = tm->launch_events ? tm->rev[1] : nullptr;
         if (n <= rows_wide_max())
-            hipExtLaunchKernelGGL(k_hash_rows_wide<MW>, dim3((unsigned)((rows * 16 + 255) / 256), 3), dim3(256), 0, st,
-                                  r0, r1, 0, b.words, b.desc, n, k, b.dims, b.dig, b.fail);
+            launch_ev(k_hash_rows_wide<MW>, dim3((unsigned)((rows * 16 + 255) / 256), 3), dim3(256), 0, st,
+                                  r0, r1, b.words, b.desc, n, k, b.dims, b.dig, b.fail);
         else
-            hipExtLaunchKernelGGL(k_hash_rows<MW>, dim3(gx, 3), dim3(256), 0, st, r0, r1, 0, b.words, b.desc, n, k,
+            launch_ev(k_hash_rows<MW>, dim3(gx, 3), dim3(256), 0, st, r0, r1, b.words, b.desc, n, k,
                                   b.dims, b.dig, b.fail, age);
     }
     mark(2, st);
@@ -1840,8 +1850,8 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
         launch_aux_chain();
         aux_started = true;
         const bool timed = tm->launch_events && tm->lev[0] != nullptr;
-        hipExtLaunchKernelGGL(k_mp_climb<MW>, dim3(n, tpp + 1), dim3(MP_CLIMB_THREADS), 0, st,
-                              timed ? tm->lev[0] : nullptr, timed ? tm->lev[1] : nullptr, 0, b.words, b.dig, b.mp,
+        launch_ev(k_mp_climb<MW>, dim3(n, tpp + 1), dim3(MP_CLIMB_THREADS), 0, st,
+                              timed ? tm->lev[0] : nullptr, timed ? tm->lev[1] : nullptr, b.words, b.dig, b.mp,
                               tpp, b.desc, n, (const uint32_t*)b.fail, LcwTree{b.lcw, b.max_lcw}, 0u);
         launches = 1;
     }
@@ -1874,7 +1884,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
             const uint64_t ops_l = (l < b.mp.levels ? b.mp_cap_host[l] : 0) + (uint64_t)(b.max_lcw >> (l + 1)) * n;
             const uint64_t cf = climb_from_ops(hash_levels);
             if (cf && ops_l <= cf && hash_levels - l >= 3) {
-                hipExtLaunchKernelGGL(k_mp_climb<MW>, dim3(n, tpp + 1), dim3(MP_CLIMB_THREADS), 0, st, e0, e1, 0, b.words,
+                launch_ev(k_mp_climb<MW>, dim3(n, tpp + 1), dim3(MP_CLIMB_THREADS), 0, st, e0, e1, b.words,
                                       b.dig, b.mp, tpp, b.desc, n, (const uint32_t*)b.fail, lcw, l);
                 ++launches;
                 break;
@@ -1883,7 +1893,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
         if (l == tail0) {
             TailCaps caps{};
             for (uint32_t t = l; t < hash_levels; ++t) caps.cap[t - l] = t < b.mp.levels ? (uint32_t)b.mp_cap_host[t] : 0u;
-            hipExtLaunchKernelGGL(k_mp_hash_tail<MW>, dim3(1), dim3(MP_TAIL_THREADS), 0, st, e0, e1, 0, b.words, b.dig,
+            launch_ev(k_mp_hash_tail<MW>, dim3(1), dim3(MP_TAIL_THREADS), 0, st, e0, e1, b.words, b.dig,
                                   b.mp, l, hash_levels, caps, b.desc, n, (const uint32_t*)b.fail, lcw);
             ++launches;
             break;
@@ -1898,13 +1908,13 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
         // (what the rocprofv3 kernel trace reports): the launch's duration without the dispatch
         // gap before it, which a plain event pair around back-to-back launches would also hold
         if (wide)
-            hipExtLaunchKernelGGL(k_mp_hash_wide<MW>, dim3((unsigned)(((cap + per * n) * 16 + 255) / 256)), dim3(256), 0,
-                                  st, e0, e1, 0, b.words, b.dig, b.mp, l, cap, b.desc, n, (const uint32_t*)b.fail, lcw);
+            launch_ev(k_mp_hash_wide<MW>, dim3((unsigned)(((cap + per * n) * 16 + 255) / 256)), dim3(256), 0,
+                                  st, e0, e1, b.words, b.dig, b.mp, l, cap, b.desc, n, (const uint32_t*)b.fail, lcw);
         else if (n < mp_small_max)
-            hipExtLaunchKernelGGL((k_mp_hash<NHIP_MP_WAVES_SMALL, MW>), dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0,
-                                  e1, 0, b.words, b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw, age);
+            launch_ev((k_mp_hash<NHIP_MP_WAVES_SMALL, MW>), dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0,
+                                  e1, b.words, b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw, age);
         else
-            hipExtLaunchKernelGGL((k_mp_hash<NHIP_MP_WAVES, MW>), dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0, e1, 0,
+            launch_ev((k_mp_hash<NHIP_MP_WAVES, MW>), dim3(mp_blocks + lcw_blocks), dim3(256), 0, st, e0, e1,
                                   b.words, b.dig, b.mp, l, mp_blocks, b.desc, n, (const uint32_t*)b.fail, lcw, age);
         ++launches;
     }

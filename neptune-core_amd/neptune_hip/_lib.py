@@ -205,6 +205,7 @@ SIGNATURES = {
     "nhip_set_climb_from_ops": ([ctypes.c_int64], ctypes.c_int),
     "nhip_batch_set_launch_timing": ([_vp, ctypes.c_int], ctypes.c_int),
     "nhip_batch_set_streams": ([_vp, ctypes.c_int], ctypes.c_int),
+    "nhip_batch_set_graph": ([_vp, ctypes.c_int], ctypes.c_int),
     "nhip_batch_transcript": ([_vp, _vp, _sz, _u64p, _sz, ctypes.POINTER(ctypes.c_uint32), _sz,
                                ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "nhip_batch_destroy": ([_vp], None),

@@ -226,6 +226,12 @@ class Batch:
         check(self.ctx.lib.nhip_batch_set_streams(self.handle, int(streams)), "nhip_batch_set_streams")
         return self
 
+    def set_graph(self, on: bool = True) -> "Batch":
+        """Replay later untimed launches from a captured HIP graph (nhip_batch_set_graph): resident
+        batches of at most 1,024 proofs relaunched many times; a replayed launch has no phase split."""
+        check(self.ctx.lib.nhip_batch_set_graph(self.handle, 1 if on else 0), "nhip_batch_set_graph")
+        return self
+
     def stats(self) -> dict:
         s = _lib.Stats()
         check(self.ctx.lib.nhip_batch_stats(self.handle, ctypes.byref(s)), "nhip_batch_stats")

@@ -233,6 +233,7 @@ extern "C" {
     pub fn nhip_set_climb_from_ops(ops: i64) -> c_int;
     pub fn nhip_batch_set_launch_timing(batch: *mut nhip_batch, on: c_int) -> c_int;
     pub fn nhip_batch_set_streams(batch: *mut nhip_batch, streams: c_int) -> c_int;
+    pub fn nhip_batch_set_graph(batch: *mut nhip_batch, on: c_int) -> c_int;
     pub fn nhip_queue_create(ctx: *mut nhip_ctx, air: *mut nhip_air, params: *const nhip_stark_params,
                              max_batch: u32, max_wait_us: u32, out: *mut *mut nhip_queue) -> c_int;
     pub fn nhip_queue_verify(queue: *mut nhip_queue, claims: *const nhip_claim, proofs: *const nhip_proof,
