@@ -339,9 +339,9 @@ def pipelined(batches, steps: int, inflight: int, expect):
     return time.perf_counter() - t, ok
 
 
-# resident batches of at most this many proofs replay their launches from a HIP graph
-# (nhip_batch_set_graph)
-GRAPH_MAX = 1024
+# resident one-stream batches (<= SINGLE_STREAM_MAX_PROOFS) replay their launches from a HIP graph
+# (nhip_batch_set_graph): config 5's 64 / 8 proofs +3.5% / +5% at 20 in flight; a two-stream batch's
+# graph measured slower (512 proofs -12%: profiles/r06/ab_graphs.txt), so those launch directly
 
 # batches of at most this many proofs run every phase on one stream (nhip_batch_set_streams) at
 # twice the depth: config 5's 8 / 64 proofs +17% / +13%; config 4's 512-4,096 lose 10-23% that way
@@ -595,7 +595,7 @@ def config5_leg(ctx, gair, stark, proofs_n: int = 64, steps: int = 200, inflight
     transcript_ok = fail == 0 and xs == samples and idx == indices
     ok = ok and bool(np.asarray(v, dtype=bool).all()) and transcript_ok
     for b in ring:
-        b.set_graph(True)
+        b.set_graph(nstreams == 1)
 
     def region(k):
         nonlocal ok
@@ -1364,8 +1364,8 @@ def main():
     stark = NS.Stark.default().montgomery() if mont else NS.Stark.default()
     ncl = [NS.Claim(*c) for c in dev_claims]
     # R resident copies of the raw proof words (each step decodes them on the device again)
-    # resident batches of <= 1,024 proofs (the N >= 4 ranks' shares) replay a captured HIP graph
-    ring = [NS.Batch(ctx, gair, stark, ncl, dev_proofs).set_streams(streams_for(n)).set_graph(n <= GRAPH_MAX)
+    # resident one-stream batches (<= 64 proofs per GPU) replay a captured HIP graph
+    ring = [NS.Batch(ctx, gair, stark, ncl, dev_proofs).set_streams(streams_for(n)).set_graph(streams_for(n) == 1)
             for _ in range(R)]
     prep_s = time.time() - t0
     st0 = ring[0].stats()
@@ -1755,7 +1755,7 @@ def main():
         scl, spr = device_form(sc, sp, mont)
         sn = [NS.Claim(*c) for c in scl]
         Rs = default_inflight(len(sp))  # the rank's own depth (its default host exchange holds no GPU streams)
-        sring = [NS.Batch(ctx, gair, stark, sn, spr).set_graph(len(spr) <= GRAPH_MAX) for _ in range(Rs)]
+        sring = [NS.Batch(ctx, gair, stark, sn, spr) for _ in range(Rs)]
         kernel_timing(sring, region_timing)
         pipelined(sring, args.warmup, Rs, se)
         ctx.synchronize()

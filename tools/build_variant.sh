@@ -1,7 +1,8 @@
 #!/bin/bash
 # Build a complete variant of libneptune_hip.so with extra compile flags, for A/B runs:
 #   bash tools/build_variant.sh NAME "-DFLAG=V ..."  ->  neptune-core_amd/build/variants/libneptune_hip_NAME.so
-# (select it at run time with NHIP_LIB=...).  All objects are rebuilt with the same flags.
+# (select it at run time with NHIP_LIB=...).  All objects are rebuilt with the same flags, as an A/B
+# build (-DNHIP_AB_BUILD: the NHIP_* tuning switches are read, csrc/ab_env.hpp).
 set -e
 NAME=$1; FLAGS=$2
 cd "$(dirname "$0")/../neptune-core_amd"
@@ -10,7 +11,7 @@ OUT=build/v_$NAME; mkdir -p $OUT build/variants
 objs=""
 for s in $SRCS; do
   o=$OUT/$(basename ${s%.*}).o
-  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function $FLAGS -c $s -o $o &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function -DNHIP_AB_BUILD $FLAGS -c $s -o $o &
   objs="$objs $o"
 done
 wait
