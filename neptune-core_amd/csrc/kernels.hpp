@@ -152,6 +152,7 @@ struct StarkPhaseTimer {
     hipEvent_t lev[2 * MAX_HASH_LAUNCHES];  // per hash launch: dispatch begin / end (nullptr = untimed)
     hipEvent_t rev[2] = {nullptr, nullptr};  // the row-hashing launch: dispatch begin / end (nullptr = untimed)
     bool launch_events = false;  // use lev / rev on this launch (nhip_batch_set_launch_timing)
+    bool phase_marks = true;     // record the phase events (off in a captured graph: no phase split)
     uint32_t mp_hash_launches;
     uint32_t aux_after_level = 0;  // hash levels launched before the OOD/FRI/DEEP chain is released
 };

@@ -920,13 +920,16 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
                              N1 * 9 * 8,
                              N1 * 4,
                              N1 * sizeof(ProofIn),
-                             N1,
-                             CNT_N * 8,
+                             // the readback region, laid out as the pinned h_out: [device counters |
+                             // plan counters | verdicts], so one memset clears the counters and one
+                             // copy brings everything back (three fewer dependent packets per batch)
+                             OUT_HDR + (size_t)levels * MP_SHARDS * 4 + N1 + 8,
+                             0,
                              mp_total * 16 + 16,
                              mp_total * 40 + 40,
                              (size_t)levels * MP_SHARDS * 8 + 8,
                              (size_t)levels * MP_SHARDS * 8 + 8,
-                             (size_t)levels * MP_SHARDS * 4 + 4,
+                             0,
                              N1 * tpp * sizeof(MpRoot),
                              N1 * (1 + H.max_R) * k * 8,
                              N1 * (1 + H.max_R) * 4,
@@ -1000,13 +1003,13 @@ int batch_prepare(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* sp, con
         dv.ood = (uint64_t*)ptr[6];
         dv.fail = (uint32_t*)ptr[7];
         dv.in = (const ProofIn*)ptr[8];
-        dv.verdicts = (uint8_t*)ptr[9];
-        dv.counters = (unsigned long long*)ptr[10];
+        dv.counters = (unsigned long long*)ptr[9];
+        dv.verdicts = (uint8_t*)ptr[9] + OUT_HDR + (size_t)levels * MP_SHARDS * 4;
         dv.mp.ops = (uint64_t*)ptr[11];
         dv.mp.arena = (uint64_t*)ptr[12];
         dv.mp.shard_base = (const uint64_t*)ptr[13];
         dv.mp.shard_cap = (const uint64_t*)ptr[14];
-        dv.mp.counter = (uint32_t*)ptr[15];
+        dv.mp.counter = (uint32_t*)((char*)ptr[9] + OUT_HDR);
         dv.mp.roots = (MpRoot*)ptr[16];
         dv.mp.dups = (uint32_t*)ptr[17];
         dv.mp.ndup = (uint32_t*)ptr[18];
@@ -1159,12 +1162,10 @@ static hipError_t enqueue_batch(nhip_batch* b) {
     hipStream_t st = b->main;
     const uint32_t n = b->dev.n_proofs;
     const size_t cnt_bytes = (size_t)b->dev.mp.levels * MP_SHARDS * 4;
-    hipError_t e = hipMemsetAsync(b->dev.counters, 0, CNT_N * 8, st);
-    if (e == hipSuccess && cnt_bytes) e = hipMemsetAsync(b->dev.mp.counter, 0, cnt_bytes, st);
+    // [device counters | plan counters | verdicts] are one device region in h_out's layout
+    hipError_t e = hipMemsetAsync(b->dev.counters, 0, OUT_HDR + cnt_bytes, st);
     if (e == hipSuccess) e = launch_stark_phases(b->dev, st, b->aux, &b->tm);
-    if (e == hipSuccess) e = hipMemcpyAsync(b->h_out, b->dev.counters, CNT_N * 8, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess && cnt_bytes) e = hipMemcpyAsync(b->h_out + OUT_HDR, b->dev.mp.counter, cnt_bytes, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess && n) e = hipMemcpyAsync(b->h_out + OUT_HDR + cnt_bytes, b->dev.verdicts, n, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(b->h_out, b->dev.counters, OUT_HDR + cnt_bytes + n, hipMemcpyDeviceToHost, st);
     return e;
 }
 
@@ -1195,6 +1196,7 @@ static bool capture_graph(nhip_batch* b) {
     if (hipStreamBeginCapture(b->main, hipStreamCaptureModeThreadLocal) != hipSuccess) return false;
     StarkPhaseTimer saved = b->tm;
     for (int i = 0; i < STARK_EVENTS; ++i) b->tm.ev[i] = b->gev[i];
+    b->tm.phase_marks = false;
     const hipError_t e = enqueue_batch(b);
     b->tm = saved;
     const hipError_t ee = hipStreamEndCapture(b->main, &graph);

@@ -1733,7 +1733,18 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     if (n == 0) return hipSuccess;
     const uint32_t k = b.dims.num_checks;
     const uint32_t tpp = 4 + b.max_R;
-    auto mark = [&](int i, hipStream_t s) { (void)hipEventRecord(tm->ev[i], s); };
+    // Events: the phase timestamps (every one, when tm->phase_marks) and the cross-stream fork / join
+    // points (SYNC: recorded whenever the batch runs on two streams).  A replayed graph of a
+    // one-stream batch (no phase split, nhip_batch_set_graph) records none and waits on none: each
+    // record or wait is one more packet in the batch's dependent chain.
+    const bool two = st != sa;
+    constexpr uint32_t SYNC = (1u << 12) | (1u << 0) | (1u << 1) | (1u << 3) | (1u << 7) | (1u << 10) | (1u << 8);
+    auto mark = [&](int i, hipStream_t s) {
+        if (tm->phase_marks || (two && ((SYNC >> i) & 1u))) (void)hipEventRecord(tm->ev[i], s);
+    };
+    auto wait = [&](hipStream_t s, int i) {
+        if (two) (void)hipStreamWaitEvent(s, tm->ev[i], 0);
+    };
     // small batches: every Merkle tree climbed in one launch (k_mp_climb), and FRI on the main
     // stream (it needs only the sponge samples) concurrent with the plan and OOD on the aux stream;
     // DEEP (which needs both) waits for it.  With the climb that short, OOD -> FRI -> DEEP in a row
@@ -1758,7 +1769,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     const AgePrio age_sponge{age.seq, age_fs ? age.k : 0u};
     // fork: the aux stream starts after everything already queued on st (counter resets)
     mark(12, st);
-    (void)hipStreamWaitEvent(sa, tm->ev[12], 0);
+    wait(sa, 12);
     // proof-stream decode of every proof (descriptors, Fiat-Shamir programs, fail words), on the
     // aux stream: the Fiat-Shamir replay is the next packet of that queue, so it is dispatched
     // the moment decode ends, before the row hashing (main stream, waiting on the same event) can
@@ -1767,7 +1778,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     hipLaunchKernelGGL(k_decode<MW>, dim3(n), dim3(64), 0, sa, b.words, b.in, n, b.D, b.fs_stride, b.xs_stride, b.desc,
                        b.ops, b.fail, b.counters);
     mark(0, sa);
-    (void)hipStreamWaitEvent(st, tm->ev[0], 0);
+    wait(st, 0);
     // ---- aux stream: latency-bound chain
     // small batches: the sponge replay is the critical path and most SIMDs are idle, so two rows
     // per proof (pair form) for a shorter permutation; large ones: one row per proof (fewer
@@ -1807,18 +1818,18 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     }
     mark(2, st);
     if (small) {
-        (void)hipStreamWaitEvent(st, tm->ev[1], 0);  // sponge replay done
+        wait(st, 1);  // sponge replay done
         mark(13, st);
         hipLaunchKernelGGL(k_fri<MW>, dim3(n), dim3(256), 0, st, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
         mark(7, st);
     }
-    (void)hipStreamWaitEvent(st, tm->ev[3], 0);  // plan done
+    wait(st, 3);  // plan done
     // The OOD / FRI / DEEP chain only needs the Fiat-Shamir samples, but its kernels are latency-bound
     // and hold CU resources for long; started after the first `aux_after_level` (wide, VALU-bound)
     // hash levels it overlaps the narrow, latency-bound top levels instead.
     auto launch_aux_chain = [&]() {
         mark(10, st);
-        if (!small) (void)hipStreamWaitEvent(sa, tm->ev[10], 0);  // small: OOD right after the plan
+        if (!small) wait(sa, 10);  // small: OOD right after the plan
         mark(11, sa);
 #define NHIP_OOD_LAUNCH(BLK, GS, THREADS)                                                                       \
     hipLaunchKernelGGL((k_ood_air<BLK, MW, GS>), dim3(n), dim3(THREADS), b.air_lds_bytes, sa, b.words, b.desc, n,    \
@@ -1835,7 +1846,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
 #undef NHIP_OOD_LAUNCH
         mark(6, sa);
         if (small) {
-            (void)hipStreamWaitEvent(sa, tm->ev[7], 0);  // FRI done (main stream)
+            wait(sa, 7);  // FRI done (main stream)
         } else {
             hipLaunchKernelGGL(k_fri<MW>, dim3(n), dim3(256), 0, sa, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
             mark(7, sa);
@@ -1925,7 +1936,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     hipLaunchKernelGGL(k_mp_roots<MW>, dim3((nrec + n + 255) / 256), dim3(256), 0, st, b.words, b.desc, b.dig, b.mp, nrec,
                        tpp, k, b.fail, n, lcw);
     mark(5, st);
-    (void)hipStreamWaitEvent(st, tm->ev[8], 0);  // join the aux chain
+    wait(st, 8);  // join the aux chain
     hipLaunchKernelGGL(k_verdicts, dim3((n + 255) / 256), dim3(256), 0, st, b.fail, n, b.verdicts);
     mark(9, st);
     return hipGetLastError();
