@@ -1181,7 +1181,7 @@ def main():
                     help="steps in flight of the config-5 leg (default: the bench's depth for its size)")
     ap.add_argument("--config5-proofs", type=int, default=64,
                     help="config-5 leg at N = 1: proofs at log2 padded height 23 (0 = skip)")
-    ap.add_argument("--node-batches", type=int, default=16,
+    ap.add_argument("--node-batches", type=int, default=32,
                     help="node leg (config 4): batches of wire bytes decoded into per-GPU pinned arenas and "
                          "verified through nhip_group_stream_submit_placed from rank 0 (0 = skip)")
     ap.add_argument("--stream-batches", type=int, default=6,
