@@ -675,6 +675,14 @@ def queue_leg(ctx, gair, stark, claims, proofs, expect, callers: int = 64, round
     try:
         with NS.Queue(ctx, gair, stark, max_wait_us=200) as q:
             q.verify(ncl[0], proofs[0])
+            # warm-up burst: every caller once at the same time, so the queue's second batch slot and
+            # its grown device buffers exist before the timed loop (a node's queue is warm after its
+            # first few batches; allocating them synchronizes the device)
+            warm = [threading.Thread(target=q.verify, args=(ncl[i % n], proofs[i % n])) for i in range(callers)]
+            for th in warm:
+                th.start()
+            for th in warm:
+                th.join()
             q.profile(reset=True)
             q.latencies_ms(reset=True)
             barrier = threading.Barrier(callers + 1)

@@ -1097,6 +1097,8 @@ int nhip_batch_refill(nhip_ctx* ctx, nhip_batch* b, nhip_air* air, const nhip_st
 // quarter of its rate).
 static int launch_resources(nhip_batch* b) {
     if (!b->timed) {
+        const char* pm = nhip::ab_env("NHIP_PHASE_MARKS");  // A/B: 0 = the phase events off
+        b->tm.phase_marks = !(pm && pm[0] == '0');
         const char* al = nhip::ab_env("NHIP_AUX_AFTER_LEVEL");
         b->tm.aux_after_level = al ? (uint32_t)std::strtoul(al, nullptr, 10) : AUX_AFTER_LEVEL_DEFAULT;
         const size_t out_bytes = OUT_HDR + (size_t)b->dev.mp.levels * MP_SHARDS * 4 + b->dev.n_proofs + 16;
@@ -1198,7 +1200,9 @@ static bool capture_graph(nhip_batch* b) {
     for (int i = 0; i < STARK_EVENTS; ++i) b->tm.ev[i] = b->gev[i];
     b->tm.phase_marks = false;
     const hipError_t e = enqueue_batch(b);
+    const uint32_t launches = b->tm.mp_hash_launches;  // the captured sequence's hash launches
     b->tm = saved;
+    b->tm.mp_hash_launches = launches;
     const hipError_t ee = hipStreamEndCapture(b->main, &graph);
     if (e != hipSuccess || ee != hipSuccess || !graph) {
         if (graph) (void)hipGraphDestroy(graph);
@@ -1341,8 +1345,8 @@ int nhip_batch_wait(nhip_ctx* ctx, nhip_batch* b, uint8_t* verdicts, uint8_t* al
         (void)hipEventElapsedTime(&ms, b->tm.ev[a], b->tm.ev[c]);
         return (double)ms;
     };
-    if (b->last_graph) {
-        b->ph = {};  // a replayed launch: its events are the graph's own, untimed
+    if (b->last_graph || !b->tm.phase_marks) {
+        b->ph = {};  // a replayed launch (its events are the graph's own, untimed) or one without marks
     } else if (n) {
         b->ph.decode = el(12, 0);
         b->ph.fs = el(0, 1);

@@ -1731,6 +1731,7 @@ template <bool MW>
 static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStream_t sa, StarkPhaseTimer* tm) {
     const uint32_t n = b.n_proofs;
     if (n == 0) return hipSuccess;
+    (void)hipGetLastError();  // the launch errors below are this launch's, not an earlier call's
     const uint32_t k = b.dims.num_checks;
     const uint32_t tpp = 4 + b.max_R;
     // Events: the phase timestamps (every one, when tm->phase_marks) and the cross-stream fork / join

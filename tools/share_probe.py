@@ -8,7 +8,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "neptune-core_amd"), ROOT, os.path.join(ROOT, "oracle")]
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "22")
+os.environ["GPU_MAX_HW_QUEUES"] = "22"  # the bench's budget (the boxes export 4)
 import bench  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
