@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "../../include/neptune_hip.h"
+#include "ab_env.hpp"
 #include "pinned_ring.hpp"
 
 // stark_host.cpp: true once every phase of a launched batch has completed (a stream query, no wait)
@@ -78,10 +79,16 @@ struct nhip_queue {
     size_t pending_proofs = 0;
     bool stop = false;
     std::thread worker;
-    // two batch slots: one runs on the device while the next is collected and staged
-    nhip_batch* slot[2] = {nullptr, nullptr};
-    std::vector<Req*> in_slot[2];
-    bool in_flight[2] = {false, false};
+    // batch slots: up to slots_used batches on the device while the next is collected and staged (a
+    // batch is launched when its window closes and a slot is free; the worker polls the batches on the
+    // device instead of blocking on the oldest, so a request arriving meanwhile opens its window at
+    // once).  Two slots measured best (profiles/r06/ab_queue_slots.txt): three or four split the same
+    // load into smaller batches of nearly the same device time each, and the tail grows.
+    static constexpr int QUEUE_SLOTS = 4;
+    int slots_used = 2;  // A/B build: NHIP_QUEUE_SLOTS (1-4)
+    nhip_batch* slot[QUEUE_SLOTS] = {};
+    std::vector<Req*> in_slot[QUEUE_SLOTS];
+    bool in_flight[QUEUE_SLOTS] = {};
     std::vector<nhip_claim> claims;
     std::vector<nhip_proof> proofs;
     std::vector<uint8_t> verdicts;
@@ -90,7 +97,7 @@ struct nhip_queue {
     // nhip_queue_profile: written by the worker under prof_mu, read by nhip_queue_profile_read
     mutable std::mutex prof_mu;
     nhip_queue_profile prof{};
-    Clock::time_point oldest[2];  // per slot: the earliest arrival among its requests
+    Clock::time_point oldest[QUEUE_SLOTS];  // per slot: the earliest arrival among its requests
 
     static double ms_since(Clock::time_point t0, Clock::time_point t1) {
         return std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -191,34 +198,55 @@ struct nhip_queue {
     }
 
     void run() {
-        int s = 0;
+        std::deque<int> flying;  // slots with a batch on the device, oldest first (worker-only state)
+        auto complete = [&](std::unique_lock<std::mutex>& lk, int f) {
+            lk.unlock();
+            finish(f);
+            lk.lock();
+        };
+        // answer every batch on the device that has completed, in any order
+        auto answer_done = [&](std::unique_lock<std::mutex>& lk) {
+            for (size_t i = 0; i < flying.size();) {
+                const int f = flying[i];
+                if (nhip_internal_batch_done(slot[f])) {
+                    flying.erase(flying.begin() + (ptrdiff_t)i);
+                    complete(lk, f);
+                } else {
+                    ++i;
+                }
+            }
+        };
         std::unique_lock<std::mutex> lk(mu);
         for (;;) {
             if (pending.empty()) {
-                if (in_flight[s ^ 1]) {  // nothing new: complete the batch on the device first
-                    lk.unlock();
-                    finish(s ^ 1);
-                    lk.lock();
-                    continue;
+                if (stop) break;  // drained; the batches still on the device are answered below
+                if (flying.empty()) {
+                    cv_in.wait(lk, [&] { return stop || !pending.empty(); });
+                } else {  // nothing new: poll the batches on the device, take a request as it comes
+                    cv_in.wait_until(lk, Clock::now() + POLL_SLICE, [&] { return stop || !pending.empty(); });
+                    answer_done(lk);
                 }
-                cv_in.wait(lk, [&] { return stop || !pending.empty(); });
-                if (pending.empty()) break;  // stop, drained
+                continue;
             }
             // coalescing window from the oldest request's arrival, ended early by a full batch.  The
-            // batch still on the device is answered as soon as it completes, not after the window
-            // and the next batch's staging: while it runs the window is waited in short slices that
-            // poll its stream.
+            // batches on the device are answered as soon as each completes: while the window is open
+            // their streams are polled in short slices.
             const Clock::time_point deadline = pending.front()->arrived + max_wait;
             for (;;) {
-                if (in_flight[s ^ 1] && nhip_internal_batch_done(slot[s ^ 1])) {
-                    lk.unlock();
-                    finish(s ^ 1);
-                    lk.lock();
-                }
+                answer_done(lk);
                 if (stop || pending_proofs >= max_batch || Clock::now() >= deadline) break;
                 const Clock::time_point until =
-                    in_flight[s ^ 1] ? std::min(deadline, Clock::now() + POLL_SLICE) : deadline;
+                    !flying.empty() ? std::min(deadline, Clock::now() + POLL_SLICE) : deadline;
                 cv_in.wait_until(lk, until, [&] { return stop || pending_proofs >= max_batch; });
+            }
+            // a free slot; with every slot busy, the oldest batch completes first
+            int s = -1;
+            for (int q = 0; q < slots_used && s < 0; ++q)
+                if (!in_flight[q]) s = q;
+            if (s < 0) {
+                s = flying.front();
+                flying.pop_front();
+                complete(lk, s);
             }
             size_t taken = 0;
             while (!pending.empty() && (taken == 0 || taken + pending.front()->n <= max_batch) &&
@@ -235,13 +263,11 @@ struct nhip_queue {
             } catch (const std::bad_alloc&) {
                 deliver(in_slot[s], NHIP_ERR_OOM, nullptr);
             }
-            finish(s ^ 1);
-            s ^= 1;
             lk.lock();
+            if (in_flight[s]) flying.push_back(s);
         }
         lk.unlock();
-        finish(s ^ 1);
-        finish(s);
+        for (int f : flying) finish(f);
     }
 };
 
@@ -270,6 +296,8 @@ int nhip_queue_create(nhip_ctx* ctx, nhip_air* air, const nhip_stark_params* par
         // a slot holds at most max_batch requests (each of >= 1 proof): the worker's push_back
         // under its lock never allocates
         for (auto& v : q->in_slot) v.reserve(std::min<size_t>(q->max_batch, 1u << 16) + 1);
+        if (const char* e = nhip::ab_env("NHIP_QUEUE_SLOTS"))
+            q->slots_used = std::max(1, std::min(nhip_queue::QUEUE_SLOTS, std::atoi(e)));
         q->worker = std::thread([q] { q->run(); });
     } catch (const std::system_error&) {
         if (q->ring.base) nhip_host_free(q->ring.base);
