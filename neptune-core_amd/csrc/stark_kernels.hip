@@ -164,19 +164,17 @@ __global__ void __launch_bounds__(64) k_decode(const uint64_t* __restrict__ word
 // enough that the sponge replay is on the critical path with most SIMDs idle).  Both rows of a
 // pair hold the same state; only row 0 writes.  (The row form with the carry-light arithmetic was
 // measured for the mid sizes and not kept: history §3.)
+// (the body, for workgroup bx of the replay's grid: also run by k_fs_rows_small)
 template <bool PAIR, bool MW>
-__global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restrict__ words,
-                                                        const ProofDesc* __restrict__ desc,
-                                                        const FsOp* __restrict__ ops, uint32_t n_proofs,
-                                                        uint64_t* __restrict__ xs, uint32_t* __restrict__ idx_out,
-                                                        const uint32_t* __restrict__ fail, AgePrio age) {
-    age_priority(age, NHIP_LAT_PRIO);
-    __shared__ Tip5Lds lds;
-    tip5_lds_init(lds);
+__device__ __forceinline__ void fs_replay_wide_body(uint32_t bx, const Tip5Lds& lds, const uint64_t* __restrict__ words,
+                                                    const ProofDesc* __restrict__ desc,
+                                                    const FsOp* __restrict__ ops, uint32_t n_proofs,
+                                                    uint64_t* __restrict__ xs, uint32_t* __restrict__ idx_out,
+                                                    const uint32_t* __restrict__ fail) {
     constexpr uint32_t LANES = PAIR ? 32u : 16u;
     const uint32_t e = threadIdx.x & 15u;
     const uint32_t h = PAIR ? (threadIdx.x >> 4) & 1u : 0u;
-    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / LANES;
+    const uint32_t g = (bx * blockDim.x + threadIdx.x) / LANES;
     if (g >= n_proofs || fail[g]) return;  // uniform within the proof's lanes
     uint64_t rc[TIP5_ROUNDS];
 #pragma unroll
@@ -237,6 +235,17 @@ __global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restri
             icur += op.n;
         }
     }
+}
+template <bool PAIR, bool MW>
+__global__ void __launch_bounds__(256) k_fs_replay_wide(const uint64_t* __restrict__ words,
+                                                        const ProofDesc* __restrict__ desc,
+                                                        const FsOp* __restrict__ ops, uint32_t n_proofs,
+                                                        uint64_t* __restrict__ xs, uint32_t* __restrict__ idx_out,
+                                                        const uint32_t* __restrict__ fail, AgePrio age) {
+    age_priority(age, NHIP_LAT_PRIO);
+    __shared__ Tip5Lds lds;
+    tip5_lds_init(lds);
+    fs_replay_wide_body<PAIR, MW>(blockIdx.x, lds, words, desc, ops, n_proofs, xs, idx_out, fail);
 }
 
 // The same program on the quad Tip5 (tip5_permute_quad: one proof per 4 lanes, ~0.63x the 16-lane
@@ -393,18 +402,16 @@ __global__ void __launch_bounds__(256, NHIP_ROWS_WAVES) k_hash_rows(const uint64
 // chunk's words (10 lanes read a row's 80 contiguous bytes), the next chunk's word is loaded before
 // the permutation so its latency hides behind it.  Every digest is the lane form's (same sponge:
 // hash_varlen with the rate overwritten per chunk, padding 1 then 0s).
+// (the body, for workgroup bx of tree `tree`: also run by k_fs_rows_small)
 template <bool MW>
-__global__ void __launch_bounds__(256) k_hash_rows_wide(const uint64_t* __restrict__ words,
-                                                        const ProofDesc* __restrict__ desc, uint32_t n_proofs,
-                                                        uint32_t k, StarkDims dims, uint64_t* __restrict__ dig,
-                                                        const uint32_t* __restrict__ fail) {
-    latency_priority();
-    __shared__ Tip5Lds t5;
-    tip5_lds_init(t5);  // includes the barrier: every exit below comes after it
-    const uint32_t tree = blockIdx.y;
+__device__ __forceinline__ void hash_rows_wide_body(uint32_t bx, uint32_t tree, const Tip5Lds& t5,
+                                                    const uint64_t* __restrict__ words,
+                                                    const ProofDesc* __restrict__ desc, uint32_t n_proofs,
+                                                    uint32_t k, StarkDims dims, uint64_t* __restrict__ dig,
+                                                    const uint32_t* __restrict__ fail) {
     const uint32_t width = tree == 0 ? dims.num_main : (tree == 1 ? 3 * dims.num_aux : 3 * dims.num_quot_seg);
     const uint32_t e = threadIdx.x & 15u;
-    const uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;  // uniform within the row
+    const uint64_t t = ((uint64_t)bx * blockDim.x + threadIdx.x) >> 4;  // uniform within the row
     if (t >= (uint64_t)n_proofs * k) return;
     const uint32_t p = (uint32_t)(t / k), j = (uint32_t)(t % k);
     if (fail[p]) return;
@@ -428,6 +435,42 @@ __global__ void __launch_bounds__(256) k_hash_rows_wide(const uint64_t* __restri
         s = tip5_permute_wide<true>(s, e, rcs, t5.lut);
     }
     if (e < 5) dig[(((uint64_t)p * 3 + tree) * k + j) * 5 + e] = s;
+}
+template <bool MW>
+__global__ void __launch_bounds__(256) k_hash_rows_wide(const uint64_t* __restrict__ words,
+                                                        const ProofDesc* __restrict__ desc, uint32_t n_proofs,
+                                                        uint32_t k, StarkDims dims, uint64_t* __restrict__ dig,
+                                                        const uint32_t* __restrict__ fail) {
+    latency_priority();
+    __shared__ Tip5Lds t5;
+    tip5_lds_init(t5);  // includes the barrier: every exit in the body comes after it
+    hash_rows_wide_body<MW>(blockIdx.x, blockIdx.y, t5, words, desc, n_proofs, k, dims, dig, fail);
+}
+
+// One-stream small batches: the pair-form sponge replay (workgroups [0, fs_blocks)) and the 16-lane
+// row hashing (the rest, rows_gx per tree) in ONE launch.  The row hashing needs no Fiat-Shamir
+// sample, so it runs beside the replay instead of after it, and the batch's dependent chain is one
+// packet shorter (each dependent packet costs ~38 us of a small batch's latency when 20 batches are
+// in flight: profiles/r06/ab_pad_packets.txt).  The replay's workgroups come first in dispatch order.
+template <bool MW>
+__global__ void __launch_bounds__(256) k_fs_rows_small(const uint64_t* __restrict__ words,
+                                                       const ProofDesc* __restrict__ desc,
+                                                       const FsOp* __restrict__ ops, uint32_t n_proofs,
+                                                       uint64_t* __restrict__ xs, uint32_t* __restrict__ idx_out,
+                                                       const uint32_t* __restrict__ fail, AgePrio age,
+                                                       uint32_t fs_blocks, uint32_t rows_gx, uint32_t k,
+                                                       StarkDims dims, uint64_t* __restrict__ dig) {
+    const uint32_t bx = blockIdx.x;
+    if (bx < fs_blocks) age_priority(age, NHIP_LAT_PRIO);
+    else latency_priority();
+    __shared__ Tip5Lds lds;
+    tip5_lds_init(lds);
+    if (bx < fs_blocks) {
+        fs_replay_wide_body<true, MW>(bx, lds, words, desc, ops, n_proofs, xs, idx_out, fail);
+    } else {
+        const uint32_t r = bx - fs_blocks;
+        hash_rows_wide_body<MW>(r % rows_gx, r / rows_gx, lds, words, desc, n_proofs, k, dims, dig, fail);
+    }
 }
 
 // ------------------------------------------------------------------ workgroup helpers
@@ -1727,6 +1770,12 @@ static FsForm fs_form(uint32_t n) {
     return n >= quad_min ? FS_QUAD : FS_ROW;
 }
 
+#ifdef NHIP_AB_BUILD
+// A/B build only: an empty kernel, NHIP_PAD_PACKETS of them after each kernel of the batch (what one
+// more dependent packet in a batch's chain costs under load)
+__global__ void k_pad_packet() {}
+#endif
+
 template <bool MW>
 static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStream_t sa, StarkPhaseTimer* tm) {
     const uint32_t n = b.n_proofs;
@@ -1746,6 +1795,17 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     auto wait = [&](hipStream_t s, int i) {
         if (two) (void)hipStreamWaitEvent(s, tm->ev[i], 0);
     };
+#ifdef NHIP_AB_BUILD
+    static const int pad_n = [] {
+        const char* e = nhip::ab_env("NHIP_PAD_PACKETS");
+        return e ? std::atoi(e) : 0;
+    }();
+    auto pad = [&](hipStream_t s) {
+        for (int i = 0; i < pad_n; ++i) hipLaunchKernelGGL(k_pad_packet, dim3(1), dim3(64), 0, s);
+    };
+#else
+    auto pad = [](hipStream_t) {};
+#endif
     // small batches: every Merkle tree climbed in one launch (k_mp_climb), and FRI on the main
     // stream (it needs only the sponge samples) concurrent with the plan and OOD on the aux stream;
     // DEEP (which needs both) waits for it.  With the climb that short, OOD -> FRI -> DEEP in a row
@@ -1778,6 +1838,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     // and stretched the latency-bound sponge replay 1.6 -> 5.0 ms (config 4, one step in flight).
     hipLaunchKernelGGL(k_decode<MW>, dim3(n), dim3(64), 0, sa, b.words, b.in, n, b.D, b.fs_stride, b.xs_stride, b.desc,
                        b.ops, b.fail, b.counters);
+    pad(sa);
     mark(0, sa);
     wait(st, 0);
     // ---- aux stream: latency-bound chain
@@ -1786,7 +1847,19 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     // lane-instructions while the other steps' hashing fills the GPU); the largest: four lanes per
     // proof (quad form, fewer lane-instructions again).  NHIP_FS_FORM forces one.
     const FsForm ff = fs_form(n);
-    if (ff == FS_PAIR)
+    // one stream, pair form, 16-lane rows: the replay and the row hashing in one launch
+    static const bool fuse_env = [] {  // A/B build: NHIP_FUSE_SMALL=0 launches them apart
+        const char* e = nhip::ab_env("NHIP_FUSE_SMALL");
+        return !(e && e[0] == '0');
+    }();
+    const bool fused = fuse_env && !two && ff == FS_PAIR && n <= rows_wide_max();
+    const uint64_t rows = (uint64_t)n * k;
+    if (fused) {
+        const uint32_t fs_blocks = (n * 32 + 255) / 256;
+        const uint32_t rows_gx = (uint32_t)((rows * 16 + 255) / 256);
+        hipLaunchKernelGGL(k_fs_rows_small<MW>, dim3(fs_blocks + 3 * rows_gx), dim3(256), 0, sa, b.words, b.desc,
+                           b.ops, n, b.xs, b.idx, b.fail, age_sponge, fs_blocks, rows_gx, k, b.dims, b.dig);
+    } else if (ff == FS_PAIR)
         hipLaunchKernelGGL((k_fs_replay_wide<true, MW>), dim3((n * 32 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
                            b.ops, n, b.xs, b.idx, b.fail, age_sponge);
     else if (ff == FS_QUAD)
@@ -1795,6 +1868,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     else
         hipLaunchKernelGGL((k_fs_replay_wide<false, MW>), dim3((n * 16 + 255) / 256), dim3(256), 0, sa, b.words, b.desc,
                            b.ops, n, b.xs, b.idx, b.fail, age_sponge);
+    pad(sa);
     mark(1, sa);
     if (k <= 128)
         hipLaunchKernelGGL(k_mp_plan<128>, dim3(n, 1 + b.max_R), dim3(128), 0, sa, b.words, b.desc, n, k, tpp, b.dig,
@@ -1802,10 +1876,10 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     else
         hipLaunchKernelGGL(k_mp_plan<256>, dim3(n, 1 + b.max_R), dim3(256), 0, sa, b.words, b.desc, n, k, tpp, b.dig,
                            b.idx, b.mp, b.fail, b.counters + CNT_MP_SKIPPED);
+    pad(sa);
     mark(3, sa);
     // ---- main stream: VALU-bound hashing
-    {
-        const uint64_t rows = (uint64_t)n * k;
+    if (!fused) {
         unsigned gx = (unsigned)((rows + 255) / 256);
         if (gx > 16384) gx = 16384;
         // dispatch begin / end events (the row kernel's own duration, as the kernel trace has it)
@@ -1817,11 +1891,13 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
             launch_ev(k_hash_rows<MW>, dim3(gx, 3), dim3(256), 0, st, r0, r1, b.words, b.desc, n, k,
                                   b.dims, b.dig, b.fail, age);
     }
+    pad(st);
     mark(2, st);
     if (small) {
         wait(st, 1);  // sponge replay done
         mark(13, st);
         hipLaunchKernelGGL(k_fri<MW>, dim3(n), dim3(256), 0, st, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
+        pad(st);
         mark(7, st);
     }
     wait(st, 3);  // plan done
@@ -1845,6 +1921,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
             else NHIP_OOD_LAUNCH(256, false, b.air_block);
         }
 #undef NHIP_OOD_LAUNCH
+        pad(sa);
         mark(6, sa);
         if (small) {
             wait(sa, 7);  // FRI done (main stream)
@@ -1854,6 +1931,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
         }
         hipLaunchKernelGGL(k_deep_rows8<MW>, dim3(n), dim3(256), deep_rows8_lds_bytes(b.dims), sa, b.words, b.desc, n,
                            b.dims, b.xs, b.xdom, b.ood, b.fail);
+        pad(sa);
         mark(8, sa);
     };
     uint32_t launches = 0;
@@ -1865,6 +1943,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
         launch_ev(k_mp_climb<MW>, dim3(n, tpp + 1), dim3(MP_CLIMB_THREADS), 0, st,
                               timed ? tm->lev[0] : nullptr, timed ? tm->lev[1] : nullptr, b.words, b.dig, b.mp,
                               tpp, b.desc, n, (const uint32_t*)b.fail, LcwTree{b.lcw, b.max_lcw}, 0u);
+        pad(st);
         launches = 1;
     }
     const LcwTree lcw{b.lcw, b.max_lcw};
@@ -1936,6 +2015,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     const uint32_t nrec = n * tpp;
     hipLaunchKernelGGL(k_mp_roots<MW>, dim3((nrec + n + 255) / 256), dim3(256), 0, st, b.words, b.desc, b.dig, b.mp, nrec,
                        tpp, k, b.fail, n, lcw);
+    pad(st);
     mark(5, st);
     wait(st, 8);  // join the aux chain
     hipLaunchKernelGGL(k_verdicts, dim3((n + 255) / 256), dim3(256), 0, st, b.fail, n, b.verdicts);

@@ -12,6 +12,8 @@ Tip5: DESIGN.md §4), compared transcript for transcript with the oracle on the 
     (nhip_set_climb_from_ops(0)): both reject, as the C oracle does;
   * tests/golden/pool4_fast.npz: 16 config-4-shaped proofs (heights 9-12) from the FULL synthetic
     prover (every column a low-degree polynomial), plus a MainRows mutant per height.
+Each batch runs on two streams (the library default) and on one stream (the bench's form for small
+batches: the sponge replay and the row hashing then share one launch, k_fs_rows_small).
 Reference: triton_vm::verify at verifier.rs:60-63, one proof at a time."""
 import json
 import os
@@ -56,22 +58,24 @@ def _spans(proof, params):
     return out
 
 
-def _run(ctx, air_words, cases, extra=()):
+def _run(ctx, air_words, cases, extra=(), streams=2):
     import neptune_hip.stark as NS
     claims = [c["claim"] for c in cases] + [c for c, _ in extra]
     proofs = [c["proof"] for c in cases] + [p for _, p in extra]
     b = NS.Batch(ctx, NS.Air(air_words), NS.Stark.default(), [NS.Claim(*c) for c in claims], proofs)
+    b.set_streams(streams)
     v, _ = b.run()
     tr = [b.transcript(i) for i in range(len(proofs))]
     b.close()
     return [bool(x) for x in v], tr, claims, proofs
 
 
-def test_config5_distinct_height23_transcripts(ctx, air_words):
+@pytest.mark.parametrize("streams", [2, 1])
+def test_config5_distinct_height23_transcripts(ctx, air_words, streams):
     cases = _load("config5_distinct.npz")
     assert len(cases) == 4 and len({tuple(c["proof"][:64].tolist()) for c in cases}) == 4
     assert all(c["info"]["log2_ph"] == 23 and c["info"]["last_poly_degree"] > 0 for c in cases)
-    got, tr, _, _ = _run(ctx, air_words, cases)
+    got, tr, _, _ = _run(ctx, air_words, cases, streams=streams)
     assert got == [True] * 4
     for c, (xs, idx, fail) in zip(cases, tr):
         assert fail == 0 and xs == c["samples"] and idx == c["indices"]
@@ -95,8 +99,8 @@ def _auth_mutants(case, params):
     return res
 
 
-@pytest.mark.parametrize("climb_from", [-1, 0])
-def test_auth_structure_mutants_reject_with_and_without_climb_from(ctx, air_words, climb_from):
+@pytest.mark.parametrize("climb_from,streams", [(-1, 2), (0, 2), (-1, 1)])
+def test_auth_structure_mutants_reject_with_and_without_climb_from(ctx, air_words, climb_from, streams):
     import neptune_hip._lib as L
     lib = L.load()
     cases = _load("config5_distinct.npz")[:2]
@@ -106,7 +110,7 @@ def test_auth_structure_mutants_reject_with_and_without_climb_from(ctx, air_word
         extra += _auth_mutants(c, params)
     assert lib.nhip_set_climb_from_ops(climb_from) == 0
     try:
-        got, tr, claims, proofs = _run(ctx, air_words, cases, extra)
+        got, tr, claims, proofs = _run(ctx, air_words, cases, extra, streams)
     finally:
         assert lib.nhip_set_climb_from_ops(-1) == 0
     want = [bool(x) for x in C.stark_verify_batch(air_words, params, claims, proofs, threads=8)]
@@ -119,7 +123,8 @@ def test_auth_structure_mutants_reject_with_and_without_climb_from(ctx, air_word
         assert fail != 0 and xs == src["samples"] and idx == src["indices"], j
 
 
-def test_pool4_fast_prover_transcripts_and_mutants(ctx, air_words):
+@pytest.mark.parametrize("streams", [2, 1])
+def test_pool4_fast_prover_transcripts_and_mutants(ctx, air_words, streams):
     cases = _load("pool4_fast.npz")
     assert len(cases) == 16 and {c["info"]["log2_ph"] for c in cases} == {9, 10, 11, 12}
     params = S.StarkParams()
@@ -129,7 +134,7 @@ def test_pool4_fast_prover_transcripts_and_mutants(ctx, air_words):
         m = c["proof"].copy()
         m[(lo + hi) // 2] = np.uint64((int(m[(lo + hi) // 2]) + 1) % S.P)
         extra.append((c["claim"], m))
-    got, tr, claims, proofs = _run(ctx, air_words, cases, extra)
+    got, tr, claims, proofs = _run(ctx, air_words, cases, extra, streams)
     want = [bool(x) for x in C.stark_verify_batch(air_words, params, claims, proofs, threads=8)]
     assert got == want == [True] * 16 + [False] * 4
     for c, (xs, idx, fail) in zip(cases, tr):
