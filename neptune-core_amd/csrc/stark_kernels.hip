@@ -566,15 +566,15 @@ struct MpPlanLds {
     uint32_t base, ndup;
 };
 
+// (the body, for proof p's tree group grp: also run by k_plan_fri_small)
 template <int B>
-__global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
-                                               uint32_t n_proofs, uint32_t k, uint32_t trees_per_proof,
-                                               const uint64_t* __restrict__ dig, const uint32_t* __restrict__ idx_all,
-                                               MpPlan plan, uint32_t* __restrict__ fail,
-                                               unsigned long long* __restrict__ perm_counter) {
-    latency_priority();
+__device__ __forceinline__ void mp_plan_body(uint32_t p, uint32_t grp, const uint64_t* __restrict__ words,
+                                             const ProofDesc* __restrict__ desc, uint32_t n_proofs, uint32_t k,
+                                             uint32_t trees_per_proof, const uint64_t* __restrict__ dig,
+                                             const uint32_t* __restrict__ idx_all, MpPlan plan,
+                                             uint32_t* __restrict__ fail, unsigned long long* __restrict__ perm_counter) {
     __shared__ MpPlanLds<B> L;
-    const uint32_t p = blockIdx.x, grp = blockIdx.y, tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x;
     if (p >= n_proofs) return;
     const ProofDesc& d = desc[p];
     const uint32_t NT = grp == 0 ? 4u : 1u;
@@ -745,6 +745,16 @@ __global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ word
             atomicOr(&fail[p], fail_bit[t]);
         }
     }
+}
+template <int B>
+__global__ void __launch_bounds__(B) k_mp_plan(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+                                               uint32_t n_proofs, uint32_t k, uint32_t trees_per_proof,
+                                               const uint64_t* __restrict__ dig, const uint32_t* __restrict__ idx_all,
+                                               MpPlan plan, uint32_t* __restrict__ fail,
+                                               unsigned long long* __restrict__ perm_counter) {
+    latency_priority();
+    mp_plan_body<B>(blockIdx.x, blockIdx.y, words, desc, n_proofs, k, trees_per_proof, dig, idx_all, plan, fail,
+                    perm_counter);
 }
 
 // The last FRI codeword's Merkle tree (every node; XFE leaves embedded as [c0, c1, c2, 0, 0]) is
@@ -1063,11 +1073,12 @@ __global__ void __launch_bounds__(MP_CLIMB_THREADS) k_mp_climb(const uint64_t* _
 
 // One lane per (proof, tree): duplicate leaf indices carry equal digests, final node == root.
 // Lanes n_records.. check the last codeword's Merkle root, one per proof.
+// (the body, for record i: also run by k_roots_verdicts_small)
 template <bool MW>
-__global__ void k_mp_roots(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
-                           const uint64_t* __restrict__ dig, MpPlan plan, uint32_t n_records, uint32_t trees_per_proof,
-                           uint32_t k, uint32_t* __restrict__ fail, uint32_t n_proofs, LcwTree lcw) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void mp_roots_body(uint32_t i, const uint64_t* __restrict__ words,
+                                              const ProofDesc* __restrict__ desc, const uint64_t* __restrict__ dig,
+                                              MpPlan plan, uint32_t n_records, uint32_t trees_per_proof, uint32_t k,
+                                              uint32_t* __restrict__ fail, uint32_t n_proofs, LcwTree lcw) {
     if (i >= n_records) {
         const uint32_t p = i - n_records;
         if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
@@ -1099,6 +1110,13 @@ __global__ void k_mp_roots(const uint64_t* __restrict__ words, const ProofDesc* 
 #pragma unroll
     for (int q = 0; q < 5; ++q) ok &= v[q] == word_mont<MW>(words[r.root_off + q]);
     if (!ok) atomicOr(&fail[p], r.fail_bit);
+}
+template <bool MW>
+__global__ void k_mp_roots(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+                           const uint64_t* __restrict__ dig, MpPlan plan, uint32_t n_records, uint32_t trees_per_proof,
+                           uint32_t k, uint32_t* __restrict__ fail, uint32_t n_proofs, LcwTree lcw) {
+    mp_roots_body<MW>(blockIdx.x * blockDim.x + threadIdx.x, words, desc, dig, plan, n_records, trees_per_proof, k,
+                      fail, n_proofs, lcw);
 }
 
 // ------------------------------------------------------------------ XFE block reduction
@@ -1351,16 +1369,16 @@ __device__ __forceinline__ uint64_t lds_pow(const uint64_t* __restrict__ sq, uin
 #ifndef NHIP_FRI_WAVES
 #define NHIP_FRI_WAVES 1
 #endif
+// (the body, for proof p: also run by k_plan_fri_small)
 template <bool MW>
-__global__ void __launch_bounds__(256, NHIP_FRI_WAVES) k_fri(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
-                                             uint32_t n_proofs, StarkDims dims, const uint64_t* __restrict__ xs,
-                                             const uint32_t* __restrict__ idx_all, uint64_t* __restrict__ xdom,
-                                             uint32_t* __restrict__ fail) {
-    latency_priority();
+__device__ __forceinline__ void fri_body(uint32_t p, const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+                                         uint32_t n_proofs, StarkDims dims, const uint64_t* __restrict__ xs,
+                                         const uint32_t* __restrict__ idx_all, uint64_t* __restrict__ xdom,
+                                         uint32_t* __restrict__ fail) {
     __shared__ Xfe red[256];
     __shared__ uint64_t gsq[33], wsq[33];
     __shared__ uint32_t lflag;
-    const uint32_t p = blockIdx.x, tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x;
     if (p >= n_proofs || (fail[p] & FAIL_DECODE)) return;
     const ProofDesc& d = desc[p];
     const SampleLayout sl = SampleLayout::of(dims, d.R);
@@ -1459,6 +1477,37 @@ __global__ void __launch_bounds__(256, NHIP_FRI_WAVES) k_fri(const uint64_t* __r
         if (!d.last_poly_degree_ok) f |= FAIL_FRI_DEGREE;
     }
     if (f) atomicOr(&fail[p], f);
+}
+template <bool MW>
+__global__ void __launch_bounds__(256, NHIP_FRI_WAVES) k_fri(const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc,
+                                             uint32_t n_proofs, StarkDims dims, const uint64_t* __restrict__ xs,
+                                             const uint32_t* __restrict__ idx_all, uint64_t* __restrict__ xdom,
+                                             uint32_t* __restrict__ fail) {
+    latency_priority();
+    fri_body<MW>(blockIdx.x, words, desc, n_proofs, dims, xs, idx_all, xdom, fail);
+}
+
+// One-stream small batches: the Merkle plan (workgroups [0, n * groups): proof bx % n, tree group
+// bx / n) and FRI (the next n workgroups, one per proof) in ONE launch.  Both need only the sponge
+// samples and decode's words, neither reads the other's output, so the batch's dependent chain is one
+// packet and one phase shorter.
+template <bool MW>
+__global__ void __launch_bounds__(256) k_plan_fri_small(const uint64_t* __restrict__ words,
+                                                        const ProofDesc* __restrict__ desc, uint32_t n_proofs,
+                                                        uint32_t k, uint32_t trees_per_proof, uint32_t groups,
+                                                        const uint64_t* __restrict__ dig,
+                                                        const uint32_t* __restrict__ idx_all, MpPlan plan,
+                                                        uint32_t* __restrict__ fail,
+                                                        unsigned long long* __restrict__ perm_counter,
+                                                        StarkDims dims, const uint64_t* __restrict__ xs,
+                                                        uint64_t* __restrict__ xdom) {
+    latency_priority();
+    const uint32_t bx = blockIdx.x, np = n_proofs * groups;
+    if (bx < np)
+        mp_plan_body<256>(bx % n_proofs, bx / n_proofs, words, desc, n_proofs, k, trees_per_proof, dig, idx_all, plan,
+                          fail, perm_counter);
+    else
+        fri_body<MW>(bx - np, words, desc, n_proofs, dims, xs, idx_all, xdom, fail);
 }
 
 // ------------------------------------------------------------------ DEEP
@@ -1673,6 +1722,22 @@ __global__ void k_verdicts(const uint32_t* __restrict__ fail, uint32_t n, uint8_
     if (i < n) v[i] = fail[i] == 0 ? 1 : 0;
     if (i == 0) atomicAdd(&g_batches_done, 1u);  // the batch's last kernel: one more finished launch
 }
+// Small batches (n_records + n_proofs <= ROOTS_ONE_WG): the root checks and the verdicts in one
+// workgroup, one launch (one dependent packet fewer).  The fail words are read back past the L1 (a
+// root check's atomicOr lands in L2) after every lane's atomics have completed (fence + barrier).
+static constexpr uint32_t ROOTS_ONE_WG = 1024;
+template <bool MW>
+__global__ void __launch_bounds__(ROOTS_ONE_WG) k_roots_verdicts_small(
+    const uint64_t* __restrict__ words, const ProofDesc* __restrict__ desc, const uint64_t* __restrict__ dig,
+    MpPlan plan, uint32_t n_records, uint32_t trees_per_proof, uint32_t k, uint32_t* __restrict__ fail,
+    uint32_t n_proofs, LcwTree lcw, uint8_t* __restrict__ v) {
+    const uint32_t i = threadIdx.x;
+    mp_roots_body<MW>(i, words, desc, dig, plan, n_records, trees_per_proof, k, fail, n_proofs, lcw);
+    __threadfence();
+    __syncthreads();
+    if (i < n_proofs) v[i] = __hip_atomic_load(&fail[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 ? 1 : 0;
+    if (i == 0) atomicAdd(&g_batches_done, 1u);  // the batch's last kernel: one more finished launch
+}
 
 // ------------------------------------------------------------------ launchers
 // A launch with dispatch begin / end events when given (hipExtLaunchKernel: the launch-timing
@@ -1870,7 +1935,18 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
                            b.ops, n, b.xs, b.idx, b.fail, age_sponge);
     pad(sa);
     mark(1, sa);
-    if (k <= 128)
+    // one stream, small, k <= 256: the plan and FRI in one launch
+    static const bool fuse2_env = [] {  // A/B build: NHIP_FUSE_PLAN_FRI=0 launches them apart
+        const char* e = nhip::ab_env("NHIP_FUSE_PLAN_FRI");
+        return !(e && e[0] == '0');
+    }();
+    const bool fused2 = fuse2_env && !two && small && k <= 256;
+    if (fused2) {
+        mark(13, sa);
+        hipLaunchKernelGGL(k_plan_fri_small<MW>, dim3(n * (1 + b.max_R) + n), dim3(256), 0, sa, b.words, b.desc, n,
+                           k, tpp, 1 + b.max_R, b.dig, b.idx, b.mp, b.fail, b.counters + CNT_MP_SKIPPED, b.dims, b.xs,
+                           b.xdom);
+    } else if (k <= 128)
         hipLaunchKernelGGL(k_mp_plan<128>, dim3(n, 1 + b.max_R), dim3(128), 0, sa, b.words, b.desc, n, k, tpp, b.dig,
                            b.idx, b.mp, b.fail, b.counters + CNT_MP_SKIPPED);
     else
@@ -1893,7 +1969,9 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     }
     pad(st);
     mark(2, st);
-    if (small) {
+    if (small && fused2) {
+        mark(7, st);  // FRI ran with the plan
+    } else if (small) {
         wait(st, 1);  // sponge replay done
         mark(13, st);
         hipLaunchKernelGGL(k_fri<MW>, dim3(n), dim3(256), 0, st, b.words, b.desc, n, b.dims, b.xs, b.idx, b.xdom, b.fail);
@@ -2013,12 +2091,18 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
     tm->mp_hash_launches = launches;
     mark(4, st);
     const uint32_t nrec = n * tpp;
-    hipLaunchKernelGGL(k_mp_roots<MW>, dim3((nrec + n + 255) / 256), dim3(256), 0, st, b.words, b.desc, b.dig, b.mp, nrec,
-                       tpp, k, b.fail, n, lcw);
-    pad(st);
-    mark(5, st);
-    wait(st, 8);  // join the aux chain
-    hipLaunchKernelGGL(k_verdicts, dim3((n + 255) / 256), dim3(256), 0, st, b.fail, n, b.verdicts);
+    if (!two && nrec + n <= ROOTS_ONE_WG) {  // one stream (the aux chain is already in order): one launch
+        hipLaunchKernelGGL(k_roots_verdicts_small<MW>, dim3(1), dim3(ROOTS_ONE_WG), 0, st, b.words, b.desc, b.dig,
+                           b.mp, nrec, tpp, k, b.fail, n, lcw, b.verdicts);
+        mark(5, st);
+    } else {
+        hipLaunchKernelGGL(k_mp_roots<MW>, dim3((nrec + n + 255) / 256), dim3(256), 0, st, b.words, b.desc, b.dig,
+                           b.mp, nrec, tpp, k, b.fail, n, lcw);
+        pad(st);
+        mark(5, st);
+        wait(st, 8);  // join the aux chain
+        hipLaunchKernelGGL(k_verdicts, dim3((n + 255) / 256), dim3(256), 0, st, b.fail, n, b.verdicts);
+    }
     mark(9, st);
     return hipGetLastError();
 }
