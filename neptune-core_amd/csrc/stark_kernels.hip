@@ -1917,7 +1917,7 @@ static hipError_t launch_phases(const StarkBatchDev& b, hipStream_t st, hipStrea
         const char* e = nhip::ab_env("NHIP_FUSE_SMALL");
         return !(e && e[0] == '0');
     }();
-    const bool fused = fuse_env && !two && ff == FS_PAIR && n <= rows_wide_max();
+    const bool fused = fuse_env && !two && ff == FS_PAIR && n <= rows_wide_max() && !tm->launch_events;
     const uint64_t rows = (uint64_t)n * k;
     if (fused) {
         const uint32_t fs_blocks = (n * 32 + 255) / 256;
