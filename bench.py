@@ -1179,8 +1179,10 @@ def main():
     ap.add_argument("--paths-log2", type=int, default=20, help="config-2 microbench size (0 = skip)")
     ap.add_argument("--product-steps", type=int, default=20,
                     help="steps of the product-depth leg (2 in flight) after the timed region (0 = skip)")
-    ap.add_argument("--share-steps", type=int, default=20,
-                    help="config 4 at N = 1: timed steps of the N = 8 rank's 512-proof share (0 = skip)")
+    ap.add_argument("--share-steps", type=int, default=100,
+                    help="config 4 at N = 1: timed steps of the N = 8 rank's 512-proof share (0 = skip); 100: the "
+                         "stream's steady state (at 20 steps the 10-deep pipeline's fill and drain are half the "
+                         "region: profiles/r06/share_shapes_20steps.txt vs _100steps.txt)")
     ap.add_argument("--queue-callers", type=int, default=64,
                     help="queue leg at N = 1: concurrent single-proof callers through nhip_queue (0 = skip)")
     ap.add_argument("--no-rank-path", dest="rank_path", action="store_false",
