@@ -36,8 +36,10 @@ __device__ __forceinline__ void latency_priority() {
 // replay keeps its own), so the in-flight steps drift apart (the oldest finishes first) instead of
 // moving through their phases in lockstep.  Measured
 // (profiles/r05z/ab/age_prio_ab_r05w.txt, 3 alternating repetitions per run): config 4 in the
-// driver's 20 steps at 4,096 proofs +1.4%, 2,048 +0.9%, 1,024 and 512 equal (raising the sponge too:
-// 4,096 +1.2-1.5%, 512 -1 to -2%), so from AGE_PRIO_MIN_PROOFS on.  g_batches_done counts the
+// driver's 20 steps at 4,096 proofs +1.4%, 2,048 +0.9%, 1,024 and 512 equal, so from
+// AGE_PRIO_MIN_PROOFS on.  Raising the sponge replay too (NHIP_AGE_PRIO_FS=1): 512 -1 to -2% (round 5);
+// 4,096 +0.6% and 2,048 equal, within the run-to-run spread (round 6, once the quad launch took
+// age_sponge: round 5's 4,096 arms were the same code; profiles/r06/ab_age_prio_fs.txt), so it stays off.  g_batches_done counts the
 // device's finished batch launches (k_verdicts); a launch's seq is its place in the device's launch
 // order.
 static constexpr uint32_t AGE_PRIO_OLDEST = 2;
