@@ -85,3 +85,8 @@ def test_structural_word_fuzz_device_decoder(ctx):
         n_decode_fail += 0 if host else 1
     b.close()
     assert bool(got[0]) and n_decode_fail > len(proofs) // 2  # clean proofs accept; most mutants fail to decode
+    # the same mutants in one-stream batches of 32 (the fused small-batch launches must skip every
+    # proof that failed to decode, whatever its neighbours in the launch)
+    from test_gpu_payload_sweep import _one_stream_chunks
+    small = _one_stream_chunks(ctx, NS, air_w, claims, proofs)
+    assert small == [bool(x) for x in want]

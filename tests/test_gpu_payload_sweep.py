@@ -9,6 +9,7 @@ written non-canonically: BFieldElement::new reads any u64 mod p, so the verdict 
 p - 1, and a random u64.  Whole items are also swapped with their neighbour, dropped and duplicated
 (the stream order is the Fiat-Shamir order).  One device batch holds every mutant; each verdict
 equals the C restatement's (oracle/stark_oracle.c), and the + p mutants of accepting proofs accept.
+The same mutants then run again in one-stream batches of 32 (the fused small-batch launches).
 """
 import json
 import os
@@ -52,6 +53,23 @@ def _restream(w, spans):
     n = np.uint64(len(spans))
     inner = np.concatenate([np.asarray([n], dtype=np.uint64)] + body)
     return np.concatenate([np.asarray([len(inner)], dtype=np.uint64), inner])
+
+
+def _one_stream_chunks(ctx, NS, air_w, claims, proofs, size=32):
+    air = NS.Air([int(w) for w in air_w])
+    out = []
+    b = None
+    for s0 in range(0, len(proofs), size):
+        cl = [NS.Claim(*c) for c in claims[s0:s0 + size]]
+        pr = proofs[s0:s0 + size]
+        if b is None:
+            b = NS.Batch(ctx, air, NS.Stark.default(), cl, pr).set_streams(1)
+        else:
+            b.refill(cl, pr)
+        v, _ = b.run()
+        out += [bool(x) for x in v]
+    b.close()
+    return out
 
 
 def test_item_stratified_payload_mutations_vs_c_oracle(ctx):
@@ -102,6 +120,11 @@ def test_item_stratified_payload_mutations_vs_c_oracle(ctx):
                           [(NS.Claim(*c), p) for c, p in zip(claims, proofs)])
     want = [bool(x) for x in C.stark_verify_batch(air_w, S.StarkParams(), claims, proofs, threads=16)]
     diff = [i for i in range(len(got)) if got[i] != want[i]]
+    assert not diff, diff[:20]
+    # the same proofs in one-stream batches of 32: the fused small-batch launches (replay + rows, plan +
+    # FRI, roots + verdicts in one launch each) on the same mutants
+    small = _one_stream_chunks(ctx, NS, air_w, claims, proofs)
+    diff = [i for i in range(len(small)) if small[i] != want[i]]
     assert not diff, diff[:20]
     assert all(want[i] for i in plus_p)  # the same field elements, written non-canonically
     n_accept = sum(want)
