@@ -834,57 +834,94 @@ def pcie_stream(ctx, gair, stark, claims, proofs, expect, batches: int, dist=Non
     (each from memory on its GPU's node), between two barriers: the multi-process node rate over
     `total_proofs`, its time the slowest rank's; the raw ceiling is measured by all ranks at once."""
     import neptune_hip.stark as NS
-    pinned = NS.PinnedProofs(proofs, near=ctx)  # the receive path: pinned, on the GPU's NUMA node
-    ncl = [NS.Claim(*c) for c in claims]
-    nbytes = sum(len(p) for p in proofs) * 8
+    # With several ranks every barrier below is reached by every rank whatever happens on its own GPU:
+    # a rank whose work raised skips the rest of its work (its error goes in the result) but still
+    # meets the others at each barrier, so one rank's fault cannot leave the others waiting.
+    st_ = {"err": None}
 
-    def sync():
-        ctx.synchronize()
+    def guarded(fn):
+        if st_["err"] is None:
+            try:
+                fn()
+            except Exception as e:  # noqa: BLE001 -- reported in the leg, never the headline
+                st_["err"] = e
+
+    def barrier():
         if dist is not None:
             dist.barrier()
 
-    # raw DMA of the proof bytes, pinned -> device (best of 3)
-    dbuf = ctx.alloc(nbytes)
-    raw = []
-    sync()
-    for _ in range(3):
-        t = time.perf_counter()
-        dbuf.upload(pinned.flat)
-        raw.append(nbytes / (time.perf_counter() - t))
-    dbuf.free()
-    a = NS.Batch(ctx, gair, stark, ncl, pinned.views)
-    b = NS.Batch(ctx, gair, stark, ncl, pinned.views)
-    a.run()
-    m = NS.marshal(ncl, pinned.views)  # the C arrays, built once (a node's receive loop fills them in place)
-    ok = True
-    sync()
-    t = time.perf_counter()
-    cur, nxt = a, b
-    cur.refill(None, marshalled=m)
-    cur.launch()
-    for _ in range(batches - 1):
-        nxt.refill(None, marshalled=m)
+    v_ = {}
+
+    def setup():
+        v_["pinned"] = NS.PinnedProofs(proofs, near=ctx)  # the receive path: pinned, on the GPU's NUMA node
+        v_["ncl"] = [NS.Claim(*c) for c in claims]
+        v_["nbytes"] = sum(len(p) for p in proofs) * 8
+        ctx.synchronize()
+
+    def raw_dma():  # raw DMA of the proof bytes, pinned -> device (best of 3)
+        dbuf = ctx.alloc(v_["nbytes"])
+        v_["raw"] = []
+        for _ in range(3):
+            t = time.perf_counter()
+            dbuf.upload(v_["pinned"].flat)
+            v_["raw"].append(v_["nbytes"] / (time.perf_counter() - t))
+        dbuf.free()
+
+    def prepare():
+        v_["a"] = NS.Batch(ctx, gair, stark, v_["ncl"], v_["pinned"].views)
+        v_["b"] = NS.Batch(ctx, gair, stark, v_["ncl"], v_["pinned"].views)
+        v_["a"].run()
+        # the C arrays, built once (a node's receive loop fills them in place)
+        v_["m"] = NS.marshal(v_["ncl"], v_["pinned"].views)
+        ctx.synchronize()
+
+    def stream():
+        ok = True
+        cur, nxt = v_["a"], v_["b"]
+        cur.refill(None, marshalled=v_["m"])
+        cur.launch()
+        for _ in range(batches - 1):
+            nxt.refill(None, marshalled=v_["m"])
+            v, _ = cur.wait()
+            ok = ok and bool((np.asarray(v, dtype=bool) == expect).all())
+            nxt.launch()
+            cur, nxt = nxt, cur
         v, _ = cur.wait()
-        ok = ok and bool((np.asarray(v, dtype=bool) == expect).all())
-        nxt.launch()
-        cur, nxt = nxt, cur
-    v, _ = cur.wait()
-    if dist is not None:
-        dist.barrier()  # the slowest rank's end
+        v_["ok"] = ok and bool((np.asarray(v, dtype=bool) == expect).all())
+
+    guarded(setup)
+    barrier()
+    guarded(raw_dma)
+    guarded(prepare)
+    barrier()
+    t = time.perf_counter()
+    guarded(stream)
+    barrier()  # the slowest rank's end
     dt = time.perf_counter() - t
-    ok = ok and bool((np.asarray(v, dtype=bool) == expect).all())
-    st = a.stats()
-    a.close()
-    b.close()
-    pinned.close()
+    st = {}
+
+    def teardown():
+        st.update(v_["a"].stats())
+
+    guarded(teardown)
+    for k in ("a", "b", "pinned"):
+        if k in v_:
+            try:
+                v_[k].close()
+            except Exception:  # noqa: BLE001
+                pass
+    if st_["err"] is not None:
+        return {"error": repr(st_["err"])[:300], "verdicts_correct": None,
+                "measured": "the leg raised on this rank (the headline is unaffected)"}
+    nbytes = v_["nbytes"]
     h2d = nbytes * batches / dt
-    peak = max(raw)
+    peak = max(v_["raw"])
     return {"value": (total_proofs or len(proofs)) * batches / dt, "unit": "proofs/s", "batches": batches,
             "ranks": 1 if dist is None else dist.get_world_size(),
             "proof_bytes_per_batch": nbytes, "h2d_GBps": h2d / 1e9, "h2d_peak_GBps": peak / 1e9,
             "frac_of_h2d_peak": h2d / peak, "bound": "pcie (host-to-device DMA)",
             "refill_ms": {"host_stage": st["ms_decode"], "upload_wait": st["ms_upload"]},
-            "verdicts_correct": ok,
+            "verdicts_correct": v_["ok"],
             "measured": f"{batches} batches from pinned host memory on the GPU's node, 2 alternating (refill overlaps "
                         f"the other's run)" + ("" if dist is None else
                                                f"; every rank its own shard to its own GPU at once, h2d figures "
@@ -1803,7 +1840,7 @@ def main():
         # every rank at once (its shard to its own GPU): the multi-process form of the node's feed
         pc = pcie_stream(ctx, gair, stark, dev_claims, dev_proofs, expect, args.stream_batches, dist, total)
         res["pcie_inclusive"] = pc
-        correct = correct and pc["verdicts_correct"]
+        correct = correct and pc["verdicts_correct"] is not False  # None: the leg raised (reported in it)
     if world == 1 and args.paths_log2 > 0:
         res["tip5_paths"] = tip5_paths(ctx, args.paths_log2, 5)
     if world == 1 and args.queue_callers > 0:
@@ -1866,29 +1903,36 @@ def main():
                     del stream
             except Exception as e:  # noqa: BLE001 -- a leg, never the headline
                 for k in ("pinned", "pageable", "node"):
-                    out.setdefault(k, {"error": repr(e)[:300], "verdicts_correct": False})
+                    out.setdefault(k, {"error": repr(e)[:300], "verdicts_correct": None})
             finally:
                 if dist is not None:
                     import torch
                     torch.cuda.set_device(dev_index)  # the members' threads ran on the other devices
             return out
 
+        def safe_leg():  # whatever raises in the leg stays in the leg (reported in its fields)
+            try:
+                return leg()
+            except Exception as e:  # noqa: BLE001
+                return {k: {"error": repr(e)[:300], "verdicts_correct": None} for k in ("pinned", "pageable")}
+
         t = time.time()
-        legs = shard.on_rank0(leg, dist, "nhip_group_stream_done")
+        legs = shard.on_rank0(safe_leg, dist, "nhip_group_stream_done")
         if rank == 0:
             g, gp = legs["pinned"], legs["pageable"]
             res["group_stream"] = g
             res["group_stream_pageable"] = gp
             for x in (g, gp):
-                if "pcie_inclusive" in res and "value" in x:
+                if "value" in res.get("pcie_inclusive", {}) and "value" in x:
                     x["vs_pcie_inclusive"] = x["value"] / res["pcie_inclusive"]["value"]
             if "value" in g and "value" in gp:
                 gp["vs_pinned"] = gp["value"] / g["value"]
-            correct = correct and g["verdicts_correct"] and gp["verdicts_correct"]
+            # None: a leg that raised (its error is in the line); False: wrong verdicts (fails the run)
+            correct = correct and g["verdicts_correct"] is not False and gp["verdicts_correct"] is not False
             if "node" in legs:
                 nd = legs["node"]
                 res["node_bytes_to_verdicts"] = nd
-                correct = correct and nd["verdicts_correct"]
+                correct = correct and nd["verdicts_correct"] is not False
                 if "value" in nd and "value" in g:
                     nd["vs_pinned_group"] = nd["value"] / g["value"]
             log(f"[group legs] over {world} GPU(s) ({time.time() - t:.1f}s)")
@@ -1900,6 +1944,8 @@ def main():
         nfh = {}
         src = res.get("node_bytes_to_verdicts") if "value" in res.get("node_bytes_to_verdicts", {}) else None
         pc = res.get("pcie_inclusive")
+        if pc is not None and "value" not in pc:
+            pc = None  # the leg raised (its error is in the line)
         if src is not None:
             nfh = {"value": src["value"], "unit": "proofs/s", "gpus": src["gpus"],
                    "path": "wire bytes -> per-GPU pinned arenas -> GPUs -> verdicts (node_bytes_to_verdicts)"}

@@ -107,6 +107,93 @@ def test_agreed_fallback_when_one_rank_fails():
     assert p0 is True and p1 is True
 
 
+def _pcie_worker(rank, world, port, q):
+    """bench.pcie_stream's barrier protocol with host fakes: rank 1's setup raises, rank 0 streams."""
+    sys.path[:0] = [os.path.join(ROOT, "neptune-core_amd"), ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import numpy as np
+    import torch.distributed as dist
+    import bench
+    import neptune_hip.stark as NS
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class Buf:
+        def upload(self, a):
+            pass
+
+        def free(self):
+            pass
+
+    class Ctx:
+        def synchronize(self):
+            pass
+
+        def alloc(self, n):
+            return Buf()
+
+    class Pinned:
+        def __init__(self, proofs, near=None):
+            if dist.get_rank() == 1:
+                raise RuntimeError("simulated pinned-allocation fault")
+            self.flat = np.zeros(8, dtype=np.uint64)
+            self.views = proofs
+
+        def close(self):
+            pass
+
+    class Batch:
+        def __init__(self, *a, **k):
+            self.n = len(a[4])
+
+        def run(self):
+            return [True] * self.n, True
+
+        def refill(self, *a, **k):
+            pass
+
+        def launch(self):
+            pass
+
+        def wait(self):
+            return [True] * self.n, True
+
+        def stats(self):
+            return {"ms_decode": 0.0, "ms_upload": 0.0}
+
+        def close(self):
+            pass
+
+    NS.PinnedProofs, NS.Batch, NS.marshal = Pinned, Batch, lambda c, p: None
+    NS.Claim = lambda *c: c
+    claims = [((0,) * 5, 0, [], [])] * 4
+    proofs = [np.zeros(16, dtype=np.uint64)] * 4
+    r = bench.pcie_stream(Ctx(), None, None, claims, proofs, np.ones(4, dtype=bool), 3, dist, 8)
+    from neptune_hip import shard
+    shard_ok = shard.all_ok(True, dist)  # the ranks' next collective still lines up
+    q.put((rank, r.get("verdicts_correct"), "error" in r, "value" in r, shard_ok))
+    dist.destroy_process_group()
+
+
+def test_pcie_leg_fault_on_one_rank_does_not_strand_the_others():
+    """Every rank reaches every barrier of the multi-rank PCIe leg even when its own work raised: the
+    faulting rank reports the error in its leg (verdicts_correct None, never fatal for the headline),
+    the others finish the leg, and the next collective lines up."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pcie_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    (r0, v0, e0, val0, ok0), (r1, v1, e1, val1, ok1) = res
+    assert v0 is True and not e0 and val0
+    assert v1 is None and e1 and not val1
+    assert ok0 is True and ok1 is True
+
+
 def test_tx_stream_is_what_the_node_leg_decodes():
     """bench.tx_stream (the node leg's wire bytes): back-to-back SingleProof TransferTransactions that
     the native scanner (host only) splits back into exactly the proofs, in order."""
