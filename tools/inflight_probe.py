@@ -39,6 +39,7 @@ with nh.Context(0) as ctx:
     for rep in range(2):
         tl = tw = 0.0
         dev = 0.0
+        phase = {}
         q, launched = [], 0
         ctx.synchronize()
         t0 = time.perf_counter()
@@ -48,7 +49,11 @@ with nh.Context(0) as ctx:
         while q:
             i = q.pop(0)
             a = time.perf_counter(); v, ok = ring[i].wait(); tw += time.perf_counter() - a
-            dev += ring[i].stats()["ms_device_total"]
+            stt = ring[i].stats()
+            dev += stt["ms_device_total"]
+            for kk, vv in stt.items():
+                if kk.startswith("ms_") and isinstance(vv, float):
+                    phase[kk] = phase.get(kk, 0.0) + vv
             if launched < steps:
                 a = time.perf_counter(); ring[i].launch(); tl += time.perf_counter() - a
                 q.append(i); launched += 1
@@ -57,6 +62,7 @@ with nh.Context(0) as ctx:
                           "wall_ms_per_step": wall / steps * 1e3, "launch_ms_per_step": tl / steps * 1e3,
                           "wait_ms_per_step": tw / steps * 1e3,
                           "other_host_ms_per_step": (wall - tl - tw) / steps * 1e3,
-                          "device_latency_ms_per_step": dev / steps}), flush=True)
+                          "device_latency_ms_per_step": dev / steps,
+                          "phase_ms_per_batch": {kk: round(vv / steps, 4) for kk, vv in phase.items()}}), flush=True)
     for b in ring:
         b.close()
